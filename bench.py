@@ -1,0 +1,172 @@
+#!/usr/bin/env python3
+"""bench.py — gates/s and achieved HBM bandwidth of the MI355X state-vector engine.
+
+Workload (BASELINE.json metric "gates/s + achieved HBM GB/s (% peak), 100-gate H+CNOT circuit @ n
+qubits"): W-HC, the seeded random {H, CNOT} depth-100 circuit (factory
+createRandomHCCircuit, mt19937 seed 42) on a complex<double> state of n qubits starting at |0..0>.
+Default n = 30: the one configuration that is both HBM-bound on one GPU (16 GiB state >> 256 MiB
+Infinity Cache) and the north_star's 1/2/4/8-GPU scaling case (BASELINE.json configs[4]); --qubits
+20 / 28 give configs[1] / configs[2].  A step = one run of the circuit (inputs resident in HBM).
+
+One process per GPU (torch.distributed launcher for N > 1): the state is sharded by its high
+qubits across ranks (strong scaling: the total work is fixed).  Rank 0 prints ONE JSON line.
+
+roofline: the dominant kernel's algorithmic bytes per launch (a fused pass reads and
+writes every amplitude once = 32 B x 2^n; per-gate kernels use the per-gate byte table) divided
+by its HIP-event-timed average duration over the timed region, against 8 TB/s.
+cpu_baseline: the oracle's single-threaded C++ restatement of the reference CPUSimulator
+(kind "port"), timed on this host on a bounded prefix of the same circuit.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "cuda-quantum-simulator_amd"))
+
+METRIC = "gates/s + achieved HBM GB/s (% peak), 100-gate H+CNOT circuit @ n qubits"
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=5)
+    p.add_argument("--warmup", type=int, default=2)
+    p.add_argument("--qubits", type=int, default=30)
+    p.add_argument("--depth", type=int, default=100)
+    p.add_argument("--seed", type=int, default=42)
+    p.add_argument("--mode", choices=["fused", "per-gate"], default="fused")
+    p.add_argument("--workload", choices=["hc", "ref", "1q"], default="hc",
+                   help="hc: W-HC random H+CNOT; ref: reference benchmark_scaling circuit; "
+                        "1q: 100 unfused H gates on targets i %% n")
+    p.add_argument("--cpu-budget", type=float, default=12.0,
+                   help="seconds of single-thread CPU oracle work for cpu_baseline (0 = skip)")
+    p.add_argument("--pmc-json", default=None,
+                   help="per-launch HBM traffic measured by rocprofv3 --pmc (see profiles/)")
+    return p.parse_args()
+
+
+def make_circuit(q, args):
+    n = args.qubits
+    if args.workload == "hc":
+        return q.createRandomHCCircuit(n, args.depth, args.seed), \
+            f"W-HC random H+CNOT depth-{args.depth} seed {args.seed}"
+    if args.workload == "ref":
+        return q.createScalingBenchmarkCircuit(n), "W-REF benchmark_scaling.cu:69-76 (100 H + 20 CNOT)"
+    c = q.Circuit(n)
+    for i in range(args.depth):
+        c.h(i % n)
+    return c, f"W-1Q {args.depth} H gates on targets i % n"
+
+
+def alg_bytes_of_circuit(circuit, n):
+    """Sum of per-gate algorithmic bytes — the 'effective' traffic of the circuit."""
+    N = float(1 << n)
+    total = 0.0
+    for g in circuit.getGates():
+        t = int(g.type)
+        if t in (0, 1, 3, 8, 9, 10):
+            total += 32 * N
+        elif t in (2, 4, 5, 6, 7, 11, 13, 14, 15):
+            total += 16 * N
+        else:  # CZ, Toffoli
+            total += 8 * N
+    return total
+
+
+def cpu_baseline(circuit, n, budget):
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import numpy_oracle as orc  # test infrastructure: the CPU baseline leg only
+    gates = orc.gates_of(circuit)
+    done, secs = orc.time_prefix(n, gates, budget)
+    cpu_model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    cpu_model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"value": done / secs if secs > 0 else None, "unit": "gates/s", "cores": 1,
+            "kind": "port",
+            "sample": f"first {done} gates of the same circuit at n={n}, single thread, "
+                      f"{secs:.1f} s ({cpu_model}; host has {os.cpu_count()} logical CPUs)"}
+
+
+def run_single(args):
+    import qsim_amd as q
+    n = args.qubits
+    circuit, wl = make_circuit(q, args)
+    mode = q.RunMode.Fused if args.mode == "fused" else q.RunMode.PerGate
+    if args.workload == "1q":
+        mode = q.RunMode.PerGate
+    sim = q.Simulator(n, mode=mode)
+    for _ in range(args.warmup):
+        sim.run(circuit)
+    sim.synchronize()
+    sim.state.profile(True)
+    sim.state.profileReset()
+    sim.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        sim.run(circuit)
+    sim.synchronize()
+    t1 = time.perf_counter()
+    stats = sim.state.profileStats()
+    sim.state.profile(False)
+    wall = t1 - t0
+    gates = circuit.getGateCount()
+    dom = max(stats, key=lambda s: s["ms"]) if stats else None
+    roof = None
+    if dom and dom["launches"]:
+        per_launch_bytes = dom["alg_bytes"] / dom["launches"]
+        avg_s = dom["ms"] / dom["launches"] / 1e3
+        achieved = per_launch_bytes / avg_s / 1e9
+        traffic = None
+        if args.pmc_json and os.path.exists(args.pmc_json):
+            with open(args.pmc_json) as f:
+                pmc = json.load(f)
+            traffic = pmc.get(dom["name"], {}).get("hbm_bytes_per_launch")
+        roof = {"bound": "hbm", "kernel": dom["name"], "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
+                "traffic": traffic, "alg_bytes_per_launch": per_launch_bytes,
+                "avg_launch_ms": round(dom["ms"] / dom["launches"], 4),
+                "launches": dom["launches"]}
+    eff = alg_bytes_of_circuit(circuit, n) * args.steps / wall / 1e9
+    out = {
+        "metric": METRIC, "value": round(gates * args.steps / wall, 2), "unit": "gates/s",
+        "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(wall / args.steps * 1e3, 3), "higher_is_better": True,
+        "scaling": "strong", "vs_baseline": None, "dtype": "c128 (complex<double>)",
+        "data": "synthetic",
+        "config": {"workload": wl, "qubits": n, "gates": gates, "mode": mode.name,
+                   "state_bytes": 16 << n, "parallelism": "single GPU"},
+        "roofline": roof,
+        "effective_GBps": round(eff, 1),
+        "kernels": stats,
+    }
+    if args.cpu_budget > 0:
+        out["cpu_baseline"] = cpu_baseline(circuit, n, args.cpu_budget)
+    else:
+        out["cpu_baseline"] = None
+    print(json.dumps(out))
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world > 1 or args.gpus > 1:
+        from qsim_amd import dist_bench  # sharded strong-scaling path (RCCL over xGMI)
+        dist_bench.run(args, METRIC, HBM_PEAK_GBPS)
+    else:
+        run_single(args)
+
+
+if __name__ == "__main__":
+    main()

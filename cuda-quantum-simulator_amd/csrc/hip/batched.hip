@@ -1,0 +1,356 @@
+// batched.hip — B independent trajectories of 2^n amplitudes (reference BatchedSimulator,
+// include/NoiseModel.cuh:231-297, src/NoiseModel.cu:653-972) with Monte-Carlo Pauli noise.
+//
+// Layout: trajectory-major [B][2^n] like the reference (d_states_, NoiseModel.cu:657-673), so
+// each gate is the single-state kernel with a batch dimension (launch_op(..., batch, ...)).
+//
+// Noise (deliberate redesign): the reference draws one curand number per amplitude
+// PAIR and keeps a 48-B curandState per pair (1.5 GiB at 16q x 1024).  Here each trajectory
+// draws once per channel per gate from a stateless counter hash keyed by (seed, step, channel,
+// trajectory); the Pauli picks of all channels of one gate are composed into one Pauli string
+// i^e X^x Z^z per trajectory, and only trajectories whose string is not the identity are
+// touched (one read+write of that trajectory).  This is the physical depolarizing channel on a
+// pure-state trajectory; statistics, not per-trajectory realizations, match the reference.
+// Channel types the reference batched mode ignores (F5: only Depolarizing) are Pauli-free here
+// too: BitFlip/PhaseFlip/BitPhaseFlip are applied (X/Z/Y), damping channels are ignored.
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <memory>
+#include <random>
+#include <string>
+#include <vector>
+
+#include "device_ops.hpp"
+#include "engine.hpp"
+#include "qsim_hip.h"
+
+using namespace qsim_hip;
+
+namespace qsim_hip {
+
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+    z += 0x9e3779b97f4a7c15ull;
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+    return z ^ (z >> 31);
+}
+// uniform double in [0,1) from 53 bits
+__device__ __forceinline__ double u01(uint64_t h) { return (double)(h >> 11) * 0x1.0p-53; }
+
+struct DevChannel {
+    int type;
+    int qubit;
+    double p;
+};
+
+// One thread per trajectory: compose this step's Pauli picks into (e, x, z).
+__global__ void k_pauli_draw(const DevChannel* ch, int nch, uint64_t seed, uint64_t step,
+                             int batch, uint64_t* xz, int* ephase) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= batch) return;
+    uint64_t x = 0, z = 0;
+    int e = 0;
+    for (int c = 0; c < nch; ++c) {
+        const uint64_t key = mix64(seed ^ mix64(step * 0x100000001b3ull + (uint64_t)c) ^
+                                   ((uint64_t)b << 20));
+        const double r1 = u01(mix64(key));
+        int pauli = 0;  // 1 X, 2 Y, 3 Z
+        const int t = ch[c].type;
+        if (r1 < ch[c].p) {
+            if (t == 0) {  // depolarizing: uniform X/Y/Z (reference thresholds 1/3, 2/3)
+                const double r2 = u01(mix64(key ^ 0x5bd1e995ull));
+                pauli = r2 < 1.0 / 3.0 ? 1 : (r2 < 2.0 / 3.0 ? 2 : 3);
+            } else if (t == 3) pauli = 1;       // bit flip
+            else if (t == 4) pauli = 3;         // phase flip
+            else if (t == 5) pauli = 2;         // bit-phase flip
+        }
+        if (!pauli) continue;
+        const uint64_t q = 1ull << ch[c].qubit;
+        if (pauli == 1) {
+            x ^= q;
+        } else if (pauli == 3) {
+            if (x & q) e += 2;
+            z ^= q;
+        } else {  // Y = i X Z
+            e += 1 + ((x & q) ? 2 : 0);
+            x ^= q;
+            z ^= q;
+        }
+    }
+    xz[2 * b] = x;
+    xz[2 * b + 1] = z;
+    ephase[b] = e & 3;
+}
+
+__device__ __forceinline__ double2 mul_ipow(double2 a, int e) {
+    switch (e & 3) {
+        case 1: return make_double2(-a.y, a.x);
+        case 2: return make_double2(-a.x, -a.y);
+        case 3: return make_double2(a.y, -a.x);
+        default: return a;
+    }
+}
+
+// new[j] = i^e (-1)^{popc(z & (j^x))} old[j^x]; pairs (j, j^x) with bit h of j == 0.
+__global__ __launch_bounds__(256) void k_pauli_apply(double2* st, int n, const uint64_t* xz,
+                                                     const int* ephase, uint64_t items_per_traj) {
+    const uint64_t item = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t b = item / items_per_traj;
+    const uint64_t k = item - b * items_per_traj;
+    const uint64_t x = xz[2 * b], z = xz[2 * b + 1];
+    const int e = ephase[b];
+    if (x == 0 && z == 0 && e == 0) return;
+    double2* s = st + (b << n);
+    if (x == 0) {  // diagonal: k enumerates all 2^n amplitudes (items_per_traj == 2^(n-1)): 2 each
+        for (int r = 0; r < 2; ++r) {
+            const uint64_t j = 2 * k + r;
+            const double2 a = s[j];
+            const int sign = __popcll(z & j) & 1;
+            double2 v = mul_ipow(a, e + 2 * sign);
+            s[j] = v;
+        }
+        return;
+    }
+    const int h = 63 - __clzll(x);
+    const uint64_t lo = k & ((1ull << h) - 1ull);
+    const uint64_t j = ((k ^ lo) << 1) | lo;  // bit h == 0
+    const uint64_t jp = j ^ x;
+    const double2 a = s[j], ap = s[jp];
+    // new[j] uses old[jp]; sign from z & (j ^ x) = z & jp
+    const double2 nj = mul_ipow(ap, e + 2 * (__popcll(z & jp) & 1));
+    const double2 njp = mul_ipow(a, e + 2 * (__popcll(z & j) & 1));
+    s[j] = nj;
+    s[jp] = njp;
+}
+
+}  // namespace qsim_hip
+
+struct qsim_batch {
+    int n = 0, batch = 0, device = 0;
+    double2* d = nullptr;
+    hipStream_t stream = nullptr;
+    uint64_t seed = 0, step = 0;
+    uint64_t* d_xz = nullptr;
+    int* d_e = nullptr;
+    DevChannel* d_ch = nullptr;
+    size_t ch_cap = 0;
+    Timer timer;
+    ~qsim_batch() {
+        if (stream) (void)hipStreamSynchronize(stream);
+        if (d) (void)hipFree(d);
+        if (d_xz) (void)hipFree(d_xz);
+        if (d_e) (void)hipFree(d_e);
+        if (d_ch) (void)hipFree(d_ch);
+        if (stream) (void)hipStreamDestroy(stream);
+    }
+};
+
+namespace {
+template <typename F>
+int bguard(F&& f) {
+    try {
+        f();
+        return QSIM_OK;
+    } catch (const Error& e) {
+        set_last_error(e.what());
+        return e.code;
+    } catch (const std::exception& e) {
+        set_last_error(e.what());
+        return QSIM_ERR_RUNTIME;
+    }
+}
+void need(const qsim_batch* b) {
+    if (!b) fail(QSIM_ERR_INVALID_ARGUMENT, "null batch handle");
+}
+}  // namespace
+
+extern "C" {
+
+int qsim_batch_create(int n_qubits, int batch_size, qsim_batch** out) {
+    return bguard([&] {
+        if (!out) fail(QSIM_ERR_INVALID_ARGUMENT, "null out");
+        *out = nullptr;
+        if (n_qubits < QSIM_MIN_QUBITS || n_qubits > QSIM_MAX_QUBITS_SINGLE)
+            fail(QSIM_ERR_INVALID_ARGUMENT, "Number of qubits must be between 1 and 30");
+        if (batch_size < 1) fail(QSIM_ERR_INVALID_ARGUMENT, "batch_size must be positive");
+        auto b = std::make_unique<qsim_batch>();
+        b->n = n_qubits;
+        b->batch = batch_size;
+        QSIM_HIPCHK(hipGetDevice(&b->device));
+        QSIM_HIPCHK(hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking));
+        b->timer.stream = b->stream;
+        QSIM_HIPCHK(hipMalloc((void**)&b->d, ((uint64_t)batch_size * sizeof(double2)) << n_qubits));
+        QSIM_HIPCHK(hipMalloc((void**)&b->d_xz, 2 * sizeof(uint64_t) * batch_size));
+        QSIM_HIPCHK(hipMalloc((void**)&b->d_e, sizeof(int) * batch_size));
+        b->seed = std::random_device{}();  // reference seeds from random_device (NoiseModel.cu:663)
+        launch_init_basis(b->d, n_qubits, batch_size, 0, b->stream);
+        QSIM_HIPCHK(hipStreamSynchronize(b->stream));
+        *out = b.release();
+    });
+}
+
+int qsim_batch_destroy(qsim_batch* b) {
+    return bguard([&] { delete b; });
+}
+
+int qsim_batch_reset(qsim_batch* b) {
+    return bguard([&] {
+        need(b);
+        launch_init_basis(b->d, b->n, b->batch, 0, b->stream);
+        QSIM_HIPCHK(hipStreamSynchronize(b->stream));
+    });
+}
+
+int qsim_batch_set_seed(qsim_batch* b, uint64_t seed) {
+    return bguard([&] {
+        need(b);
+        b->seed = seed;
+        b->step = 0;
+    });
+}
+
+int qsim_batch_run(qsim_batch* b, const qsim_gate* gates, size_t count,
+                   const qsim_noise_channel* channels, size_t n_channels, int flags) {
+    return bguard([&] {
+        need(b);
+        if (!gates && count) fail(QSIM_ERR_INVALID_ARGUMENT, "null gate list");
+        std::vector<DevChannel> ch;
+        for (size_t i = 0; i < n_channels; ++i) {
+            const auto& c = channels[i];
+            if (c.qubit < 0 || c.qubit >= b->n) fail(QSIM_ERR_OUT_OF_RANGE, "noise qubit out of range");
+            if (c.type == 0 || c.type == 3 || c.type == 4 || c.type == 5)
+                ch.push_back(DevChannel{c.type, c.qubit, c.probability});
+        }
+        if (ch.size() > b->ch_cap) {
+            if (b->d_ch) {
+                QSIM_HIPCHK(hipStreamSynchronize(b->stream));
+                QSIM_HIPCHK(hipFree(b->d_ch));
+            }
+            QSIM_HIPCHK(hipMalloc((void**)&b->d_ch, ch.size() * sizeof(DevChannel)));
+            b->ch_cap = ch.size();
+        }
+        if (!ch.empty())
+            QSIM_HIPCHK(hipMemcpyAsync(b->d_ch, ch.data(), ch.size() * sizeof(DevChannel),
+                                       hipMemcpyHostToDevice, b->stream));
+        std::vector<Op> ops;
+        for (size_t i = 0; i < count; ++i) {
+            const qsim_gate& g = gates[i];
+            if (flags & QSIM_BATCH_REFERENCE_GATESET) {
+                // src/NoiseModel.cu:742-763, 808-812, 821-825: only X/Y/Z/H and CNOT act.
+                const bool ok = g.type <= QSIM_GATE_H || g.type == QSIM_GATE_CNOT;
+                validate_gate(g, b->n);
+                ops.push_back(ok ? lower_gate(g, b->n) : Op{});
+                if (!ok) ops.back().kind = -1;
+            } else {
+                ops.push_back(lower_gate(g, b->n));
+            }
+        }
+        const uint64_t N = 1ull << b->n;
+        const uint64_t items_per_traj = N / 2 > 0 ? N / 2 : 1;
+        for (const Op& op : ops) {
+            if (op.kind >= 0) launch_op(b->d, b->n, (uint64_t)b->batch, op, b->stream, &b->timer);
+            if (!ch.empty()) {
+                {
+                    TimedLaunch tl(&b->timer, "pauli_draw", 0.0, b->stream);
+                    hipLaunchKernelGGL(k_pauli_draw, dim3((b->batch + 255) / 256), dim3(256), 0,
+                                       b->stream, b->d_ch, (int)ch.size(), b->seed, b->step,
+                                       b->batch, b->d_xz, b->d_e);
+                    QSIM_HIPCHK(hipGetLastError());
+                }
+                ++b->step;
+                const uint64_t total = items_per_traj * (uint64_t)b->batch;
+                TimedLaunch tl(&b->timer, "pauli_apply", 0.0, b->stream);
+                hipLaunchKernelGGL(k_pauli_apply, dim3((unsigned)((total + 255) / 256)), dim3(256),
+                                   0, b->stream, b->d, b->n, b->d_xz, b->d_e, items_per_traj);
+                QSIM_HIPCHK(hipGetLastError());
+            }
+        }
+    });
+}
+
+int qsim_batch_avg_probabilities(qsim_batch* b, double* dst) {
+    return bguard([&] {
+        need(b);
+        const uint64_t N = 1ull << b->n;
+        double* d_p = nullptr;
+        QSIM_HIPCHK(hipMallocAsync((void**)&d_p, N * sizeof(double), b->stream));
+        launch_avg_probabilities(b->d, b->n, (uint64_t)b->batch, d_p, b->stream);
+        QSIM_HIPCHK(hipMemcpyAsync(dst, d_p, N * sizeof(double), hipMemcpyDeviceToHost, b->stream));
+        QSIM_HIPCHK(hipFreeAsync(d_p, b->stream));
+        QSIM_HIPCHK(hipStreamSynchronize(b->stream));
+    });
+}
+
+int qsim_batch_traj_probabilities(qsim_batch* b, int traj, double* dst) {
+    return bguard([&] {
+        need(b);
+        if (traj < 0 || traj >= b->batch) fail(QSIM_ERR_OUT_OF_RANGE, "Invalid trajectory index");
+        const uint64_t N = 1ull << b->n;
+        double* d_p = nullptr;
+        QSIM_HIPCHK(hipMallocAsync((void**)&d_p, N * sizeof(double), b->stream));
+        launch_probabilities(b->d + (uint64_t)traj * N, N, d_p, b->stream);
+        QSIM_HIPCHK(hipMemcpyAsync(dst, d_p, N * sizeof(double), hipMemcpyDeviceToHost, b->stream));
+        QSIM_HIPCHK(hipFreeAsync(d_p, b->stream));
+        QSIM_HIPCHK(hipStreamSynchronize(b->stream));
+    });
+}
+
+int qsim_batch_traj_state(qsim_batch* b, int traj, double* dst) {
+    return bguard([&] {
+        need(b);
+        if (traj < 0 || traj >= b->batch) fail(QSIM_ERR_OUT_OF_RANGE, "Invalid trajectory index");
+        const uint64_t N = 1ull << b->n;
+        QSIM_HIPCHK(hipMemcpyAsync(dst, b->d + (uint64_t)traj * N, N * sizeof(double2),
+                                   hipMemcpyDeviceToHost, b->stream));
+        QSIM_HIPCHK(hipStreamSynchronize(b->stream));
+    });
+}
+
+int qsim_batch_device_ptr(qsim_batch* b, void** dptr) {
+    return bguard([&] {
+        need(b);
+        *dptr = b->d;
+    });
+}
+
+int qsim_batch_sync(qsim_batch* b) {
+    return bguard([&] {
+        need(b);
+        QSIM_HIPCHK(hipStreamSynchronize(b->stream));
+    });
+}
+
+int qsim_batch_profile(qsim_batch* b, int enable) {
+    return bguard([&] {
+        need(b);
+        b->timer.enabled = enable != 0;
+    });
+}
+
+int qsim_batch_profile_count(qsim_batch* b, int* n) {
+    return bguard([&] {
+        need(b);
+        b->timer.resolve();
+        *n = (int)b->timer.stats.size();
+    });
+}
+
+int qsim_batch_profile_get(qsim_batch* b, int i, char* name, size_t name_len, double* total_ms,
+                           int64_t* launches, double* alg_bytes) {
+    return bguard([&] {
+        need(b);
+        b->timer.resolve();
+        if (i < 0 || i >= (int)b->timer.stats.size()) fail(QSIM_ERR_OUT_OF_RANGE, "bad index");
+        const auto& st = b->timer.stats[i];
+        if (name && name_len) {
+            std::strncpy(name, st.name.c_str(), name_len - 1);
+            name[name_len - 1] = 0;
+        }
+        if (total_ms) *total_ms = st.ms;
+        if (launches) *launches = st.launches;
+        if (alg_bytes) *alg_bytes = st.bytes;
+    });
+}
+
+}  // extern "C"

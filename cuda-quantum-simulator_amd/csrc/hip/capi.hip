@@ -1,0 +1,504 @@
+// capi.hip — extern "C" implementation of include/qsim_hip.h for single-GPU states.
+//
+// Each qsim_state owns its device buffer (2^n x 16 B) and a non-blocking HIP stream; gate
+// application is asynchronous on that stream (as the reference's launches are on the legacy
+// stream, src/Simulator.cu:95-97) and every readout synchronizes it (src/StateVector.cu:204-233).
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "engine.hpp"
+#include "qsim_hip.h"
+
+using namespace qsim_hip;
+
+// ---------------------------------------------------------------------------------------
+// error plumbing
+// ---------------------------------------------------------------------------------------
+static thread_local std::string g_last_error;
+namespace qsim_hip {
+void set_last_error(const char* msg) { g_last_error = msg; }
+}  // namespace qsim_hip
+
+template <typename F>
+static int guarded(F&& f) {
+    try {
+        f();
+        return QSIM_OK;
+    } catch (const Error& e) {
+        g_last_error = e.what();
+        return e.code;
+    } catch (const std::bad_alloc&) {
+        g_last_error = "host allocation failed";
+        return QSIM_ERR_RUNTIME;
+    } catch (const std::exception& e) {
+        g_last_error = e.what();
+        return QSIM_ERR_RUNTIME;
+    }
+}
+#define QSIM_REQUIRE(cond, code, msg) \
+    do {                              \
+        if (!(cond)) fail(code, msg); \
+    } while (0)
+
+// ---------------------------------------------------------------------------------------
+// Timer
+// ---------------------------------------------------------------------------------------
+namespace qsim_hip {
+int Timer::slot_of(const char* name) {
+    for (size_t i = 0; i < stats.size(); ++i)
+        if (stats[i].name == name) return (int)i;
+    stats.push_back(Stat{name});
+    return (int)stats.size() - 1;
+}
+static hipEvent_t take_event(std::vector<hipEvent_t>& pool) {
+    if (!pool.empty()) {
+        hipEvent_t e = pool.back();
+        pool.pop_back();
+        return e;
+    }
+    hipEvent_t e;
+    QSIM_HIPCHK(hipEventCreate(&e));
+    return e;
+}
+void Timer::begin(const char* name, double, hipEvent_t* a_out, int* slot_out) {
+    *slot_out = slot_of(name);
+    *a_out = take_event(pool);
+    QSIM_HIPCHK(hipEventRecord(*a_out, stream));
+}
+void Timer::end(int slot, hipEvent_t a, double bytes) {
+    hipEvent_t b = take_event(pool);
+    QSIM_HIPCHK(hipEventRecord(b, stream));
+    pending.push_back(Pending{slot, a, b, bytes});
+}
+void Timer::resolve() {
+    for (auto& p : pending) {
+        QSIM_HIPCHK(hipEventSynchronize(p.b));
+        float ms = 0.f;
+        QSIM_HIPCHK(hipEventElapsedTime(&ms, p.a, p.b));
+        stats[p.slot].ms += ms;
+        stats[p.slot].launches += 1;
+        stats[p.slot].bytes += p.bytes;
+        pool.push_back(p.a);
+        pool.push_back(p.b);
+    }
+    pending.clear();
+}
+void Timer::reset() {
+    resolve();
+    stats.clear();
+}
+Timer::~Timer() {
+    for (auto& p : pending) {
+        (void)hipEventDestroy(p.a);
+        (void)hipEventDestroy(p.b);
+    }
+    for (auto e : pool) (void)hipEventDestroy(e);
+}
+TimedLaunch::TimedLaunch(Timer* t, const char* name, double b, hipStream_t s) : tm(t), bytes(b) {
+    if (tm && tm->enabled) {
+        tm->stream = s;
+        tm->begin(name, b, &a, &slot);
+    } else {
+        tm = nullptr;
+    }
+}
+TimedLaunch::~TimedLaunch() {
+    if (tm) {
+        try {
+            tm->end(slot, a, bytes);
+        } catch (...) {
+        }
+    }
+}
+}  // namespace qsim_hip
+
+// ---------------------------------------------------------------------------------------
+// state object
+// ---------------------------------------------------------------------------------------
+struct qsim_state {
+    int n = 0;
+    int device = 0;
+    double2* d = nullptr;
+    hipStream_t stream = nullptr;
+    double* d_partials = nullptr;
+    double* d_result = nullptr;
+    TileOp* d_ops = nullptr;
+    size_t d_ops_cap = 0;
+    Timer timer;
+    ~qsim_state() {
+        if (stream) (void)hipStreamSynchronize(stream);
+        if (d) (void)hipFree(d);
+        if (d_partials) (void)hipFree(d_partials);
+        if (d_result) (void)hipFree(d_result);
+        if (d_ops) (void)hipFree(d_ops);
+        if (stream) (void)hipStreamDestroy(stream);
+    }
+};
+
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != dev) QSIM_HIPCHK(hipSetDevice(dev));
+    }
+    ~DeviceGuard() {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
+static void check_state(const qsim_state* s) {
+    if (!s) fail(QSIM_ERR_INVALID_ARGUMENT, "null state handle");
+}
+
+static void upload_ops(qsim_state* s, const std::vector<TileOp>& ops) {
+    if (ops.empty()) return;
+    if (ops.size() > s->d_ops_cap) {
+        if (s->d_ops) {
+            QSIM_HIPCHK(hipStreamSynchronize(s->stream));
+            QSIM_HIPCHK(hipFree(s->d_ops));
+            s->d_ops = nullptr;
+        }
+        size_t cap = std::max<size_t>(ops.size(), 256);
+        QSIM_HIPCHK(hipMalloc((void**)&s->d_ops, cap * sizeof(TileOp)));
+        s->d_ops_cap = cap;
+    }
+    QSIM_HIPCHK(hipMemcpyAsync(s->d_ops, ops.data(), ops.size() * sizeof(TileOp),
+                               hipMemcpyHostToDevice, s->stream));
+}
+
+extern "C" {
+
+const char* qsim_last_error(void) { return g_last_error.c_str(); }
+int qsim_abi_version(void) { return QSIM_ABI_VERSION; }
+
+int qsim_device_count(int* count) {
+    return guarded([&] {
+        QSIM_REQUIRE(count, QSIM_ERR_INVALID_ARGUMENT, "null count");
+        int c = 0;
+        hipError_t e = hipGetDeviceCount(&c);
+        if (e != hipSuccess) c = 0;
+        *count = c;
+    });
+}
+
+int qsim_device_info(int device, char* name, size_t name_len, int* cu_count, size_t* total_mem) {
+    return guarded([&] {
+        hipDeviceProp_t p;
+        QSIM_HIPCHK(hipGetDeviceProperties(&p, device));
+        if (name && name_len) {
+            std::strncpy(name, p.name, name_len - 1);
+            name[name_len - 1] = 0;
+        }
+        if (cu_count) *cu_count = p.multiProcessorCount;
+        if (total_mem) *total_mem = p.totalGlobalMem;
+    });
+}
+
+int qsim_state_create_on(int device, int n_qubits, qsim_state** out) {
+    return guarded([&] {
+        QSIM_REQUIRE(out, QSIM_ERR_INVALID_ARGUMENT, "null out");
+        *out = nullptr;
+        // StateVector ctor validation (src/StateVector.cu:135-141, Constants.hpp:68-69)
+        if (n_qubits < QSIM_MIN_QUBITS || n_qubits > QSIM_MAX_QUBITS_SINGLE)
+            fail(QSIM_ERR_INVALID_ARGUMENT, "Number of qubits must be between " +
+                                                std::to_string(QSIM_MIN_QUBITS) + " and " +
+                                                std::to_string(QSIM_MAX_QUBITS_SINGLE));
+        DeviceGuard g(device);
+        auto s = std::make_unique<qsim_state>();
+        s->n = n_qubits;
+        s->device = device;
+        QSIM_HIPCHK(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
+        s->timer.stream = s->stream;
+        QSIM_HIPCHK(hipMalloc((void**)&s->d, (sizeof(double2)) << n_qubits));
+        QSIM_HIPCHK(hipMalloc((void**)&s->d_partials, 4096 * sizeof(double)));
+        QSIM_HIPCHK(hipMalloc((void**)&s->d_result, sizeof(double)));
+        launch_init_basis(s->d, s->n, 1, 0, s->stream);
+        QSIM_HIPCHK(hipStreamSynchronize(s->stream));
+        *out = s.release();
+    });
+}
+
+int qsim_state_create(int n_qubits, qsim_state** out) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+    return qsim_state_create_on(dev, n_qubits, out);
+}
+
+int qsim_state_destroy(qsim_state* s) {
+    return guarded([&] {
+        if (!s) return;
+        DeviceGuard g(s->device);
+        delete s;
+    });
+}
+
+int qsim_state_num_qubits(const qsim_state* s, int* n) {
+    return guarded([&] {
+        check_state(s);
+        *n = s->n;
+    });
+}
+
+int qsim_state_device_ptr(qsim_state* s, void** dptr) {
+    return guarded([&] {
+        check_state(s);
+        *dptr = s->d;
+    });
+}
+
+int qsim_state_stream(qsim_state* s, void** stream) {
+    return guarded([&] {
+        check_state(s);
+        *stream = (void*)s->stream;
+    });
+}
+
+int qsim_state_init_zero(qsim_state* s) {
+    return guarded([&] {
+        check_state(s);
+        DeviceGuard g(s->device);
+        launch_init_basis(s->d, s->n, 1, 0, s->stream);
+        QSIM_HIPCHK(hipStreamSynchronize(s->stream));
+    });
+}
+
+int qsim_state_init_basis(qsim_state* s, uint64_t idx) {
+    return guarded([&] {
+        check_state(s);
+        if (idx >= (1ull << s->n)) fail(QSIM_ERR_INVALID_ARGUMENT, "Basis index out of range");
+        DeviceGuard g(s->device);
+        launch_init_basis(s->d, s->n, 1, idx, s->stream);
+        QSIM_HIPCHK(hipStreamSynchronize(s->stream));
+    });
+}
+
+int qsim_state_sync(qsim_state* s) {
+    return guarded([&] {
+        check_state(s);
+        QSIM_HIPCHK(hipStreamSynchronize(s->stream));
+    });
+}
+
+int qsim_apply_gate(qsim_state* s, const qsim_gate* g) {
+    return guarded([&] {
+        check_state(s);
+        QSIM_REQUIRE(g, QSIM_ERR_INVALID_ARGUMENT, "null gate");
+        DeviceGuard dg(s->device);
+        const Op op = lower_gate(*g, s->n);
+        launch_op(s->d, s->n, 1, op, s->stream, &s->timer);
+    });
+}
+
+int qsim_run(qsim_state* s, const qsim_gate* gates, size_t count, int flags) {
+    return guarded([&] {
+        check_state(s);
+        QSIM_REQUIRE(gates || count == 0, QSIM_ERR_INVALID_ARGUMENT, "null gate list");
+        DeviceGuard dg(s->device);
+        std::vector<Op> ops;
+        ops.reserve(count);
+        for (size_t i = 0; i < count; ++i) {
+            ops.push_back(lower_gate(gates[i], s->n));
+            ops.back().src = (int)i;
+        }
+        if (flags & QSIM_RUN_FUSED) {
+            Plan plan = plan_fused(ops, s->n);
+            upload_ops(s, plan.ops);
+            launch_fused(s->d, s->n, 1, plan, s->d_ops, s->stream, &s->timer);
+        } else {
+            for (const Op& op : ops) launch_op(s->d, s->n, 1, op, s->stream, &s->timer);
+        }
+    });
+}
+
+int qsim_apply_matrix1q(qsim_state* s, int target, const double m[8], const int* controls,
+                        int n_controls) {
+    return guarded([&] {
+        check_state(s);
+        QSIM_REQUIRE(m, QSIM_ERR_INVALID_ARGUMENT, "null matrix");
+        if (target < 0 || target >= s->n)
+            fail(QSIM_ERR_OUT_OF_RANGE, "Qubit index " + std::to_string(target) + " out of range");
+        Op op;
+        op.kind = K_M1;
+        op.sub = S_GEN;
+        op.t0 = target;
+        for (int i = 0; i < 8; ++i) op.m[i] = m[i];
+        for (int i = 0; i < n_controls; ++i) {
+            const int c = controls[i];
+            if (c < 0 || c >= s->n)
+                fail(QSIM_ERR_OUT_OF_RANGE, "Qubit index " + std::to_string(c) + " out of range");
+            if (c == target || ((op.cmask >> c) & 1ull))
+                fail(QSIM_ERR_INVALID_ARGUMENT, "control qubits must be distinct from target");
+            op.cmask |= 1ull << c;
+        }
+        DeviceGuard dg(s->device);
+        launch_op(s->d, s->n, 1, op, s->stream, &s->timer);
+    });
+}
+
+int qsim_plan_fused(int n_qubits, const qsim_gate* gates, size_t count, int hmax, int32_t* order,
+                    int32_t* pass_of, int32_t* n_passes) {
+    return guarded([&] {
+        QSIM_REQUIRE(gates || count == 0, QSIM_ERR_INVALID_ARGUMENT, "null gate list");
+        if (n_qubits < QSIM_MIN_QUBITS || n_qubits > 40) fail(QSIM_ERR_INVALID_ARGUMENT, "bad qubit count");
+        if (hmax < 0 || hmax > kTileHMax) fail(QSIM_ERR_INVALID_ARGUMENT, "hmax out of range");
+        std::vector<Op> ops;
+        for (size_t i = 0; i < count; ++i) {
+            ops.push_back(lower_gate(gates[i], n_qubits));
+            ops.back().src = (int)i;
+        }
+        const Plan plan = plan_fused(ops, n_qubits, hmax);
+        size_t k = 0;
+        int32_t tile = 0;
+        for (const FusedPass& p : plan.passes) {
+            if (p.single >= 0) {
+                if (order) order[k] = plan.singles[p.single].src;
+                if (pass_of) pass_of[k] = -1;
+                ++k;
+                continue;
+            }
+            for (int o = p.op_begin; o < p.op_end; ++o, ++k) {
+                if (order) order[k] = plan.order[o];
+                if (pass_of) pass_of[k] = tile;
+            }
+            ++tile;
+        }
+        if (n_passes) *n_passes = tile;
+    });
+}
+
+int qsim_apply_gate_raw(void* dstate, int n_qubits, const qsim_gate* g, void* stream) {
+    return guarded([&] {
+        QSIM_REQUIRE(dstate && g, QSIM_ERR_INVALID_ARGUMENT, "null argument");
+        if (n_qubits < QSIM_MIN_QUBITS || n_qubits > 40)
+            fail(QSIM_ERR_INVALID_ARGUMENT, "bad qubit count");
+        const Op op = lower_gate(*g, n_qubits);
+        launch_op((double2*)dstate, n_qubits, 1, op, (hipStream_t)stream, nullptr);
+    });
+}
+
+int qsim_state_to_host(qsim_state* s, double* dst) {
+    return guarded([&] {
+        check_state(s);
+        QSIM_REQUIRE(dst, QSIM_ERR_INVALID_ARGUMENT, "null destination");
+        DeviceGuard dg(s->device);
+        QSIM_HIPCHK(hipMemcpyAsync(dst, s->d, sizeof(double2) << s->n, hipMemcpyDeviceToHost,
+                                   s->stream));
+        QSIM_HIPCHK(hipStreamSynchronize(s->stream));
+    });
+}
+
+int qsim_state_from_host(qsim_state* s, const double* src) {
+    return guarded([&] {
+        check_state(s);
+        QSIM_REQUIRE(src, QSIM_ERR_INVALID_ARGUMENT, "null source");
+        DeviceGuard dg(s->device);
+        QSIM_HIPCHK(hipMemcpyAsync(s->d, src, sizeof(double2) << s->n, hipMemcpyHostToDevice,
+                                   s->stream));
+        QSIM_HIPCHK(hipStreamSynchronize(s->stream));
+    });
+}
+
+int qsim_state_probabilities(qsim_state* s, double* dst) {
+    return guarded([&] {
+        check_state(s);
+        QSIM_REQUIRE(dst, QSIM_ERR_INVALID_ARGUMENT, "null destination");
+        DeviceGuard dg(s->device);
+        const uint64_t N = 1ull << s->n;
+        double* d_p = nullptr;
+        QSIM_HIPCHK(hipMallocAsync((void**)&d_p, N * sizeof(double), s->stream));
+        launch_probabilities(s->d, N, d_p, s->stream);
+        QSIM_HIPCHK(hipMemcpyAsync(dst, d_p, N * sizeof(double), hipMemcpyDeviceToHost, s->stream));
+        QSIM_HIPCHK(hipFreeAsync(d_p, s->stream));
+        QSIM_HIPCHK(hipStreamSynchronize(s->stream));
+    });
+}
+
+int qsim_state_total_probability(qsim_state* s, double* out) {
+    return guarded([&] {
+        check_state(s);
+        QSIM_REQUIRE(out, QSIM_ERR_INVALID_ARGUMENT, "null out");
+        DeviceGuard dg(s->device);
+        *out = reduce_norm(s->d, s->n, -1, s->d_partials, s->d_result, s->stream);
+    });
+}
+
+int qsim_state_prob_bit_zero(qsim_state* s, int bit, double* out) {
+    return guarded([&] {
+        check_state(s);
+        QSIM_REQUIRE(out, QSIM_ERR_INVALID_ARGUMENT, "null out");
+        if (bit < 0 || bit >= s->n) fail(QSIM_ERR_INVALID_ARGUMENT, "bit out of range");
+        DeviceGuard dg(s->device);
+        *out = reduce_norm(s->d, s->n, bit, s->d_partials, s->d_result, s->stream);
+    });
+}
+
+int qsim_state_collapse(qsim_state* s, int bit, int result, double scale) {
+    return guarded([&] {
+        check_state(s);
+        if (bit < 0 || bit >= s->n) fail(QSIM_ERR_INVALID_ARGUMENT, "bit out of range");
+        if (result != 0 && result != 1) fail(QSIM_ERR_INVALID_ARGUMENT, "result must be 0 or 1");
+        DeviceGuard dg(s->device);
+        launch_collapse(s->d, s->n, bit, result, scale, s->stream);
+        QSIM_HIPCHK(hipStreamSynchronize(s->stream));
+    });
+}
+
+int qsim_state_sample(qsim_state* s, const double* uniforms, int shots, int64_t* out) {
+    return guarded([&] {
+        check_state(s);
+        if (shots <= 0) fail(QSIM_ERR_INVALID_ARGUMENT, "n_shots must be positive");
+        QSIM_REQUIRE(uniforms && out, QSIM_ERR_INVALID_ARGUMENT, "null buffer");
+        DeviceGuard dg(s->device);
+        sample_indices(s->d, s->n, uniforms, shots, out, s->stream);
+    });
+}
+
+int qsim_state_profile(qsim_state* s, int enable) {
+    return guarded([&] {
+        check_state(s);
+        s->timer.enabled = enable != 0;
+        s->timer.stream = s->stream;
+    });
+}
+
+int qsim_state_profile_count(qsim_state* s, int* n) {
+    return guarded([&] {
+        check_state(s);
+        DeviceGuard dg(s->device);
+        s->timer.resolve();
+        *n = (int)s->timer.stats.size();
+    });
+}
+
+int qsim_state_profile_get(qsim_state* s, int i, char* name, size_t name_len, double* total_ms,
+                           int64_t* launches, double* alg_bytes) {
+    return guarded([&] {
+        check_state(s);
+        DeviceGuard dg(s->device);
+        s->timer.resolve();
+        if (i < 0 || i >= (int)s->timer.stats.size()) fail(QSIM_ERR_OUT_OF_RANGE, "bad index");
+        const auto& st = s->timer.stats[i];
+        if (name && name_len) {
+            std::strncpy(name, st.name.c_str(), name_len - 1);
+            name[name_len - 1] = 0;
+        }
+        if (total_ms) *total_ms = st.ms;
+        if (launches) *launches = st.launches;
+        if (alg_bytes) *alg_bytes = st.bytes;
+    });
+}
+
+int qsim_state_profile_reset(qsim_state* s) {
+    return guarded([&] {
+        check_state(s);
+        DeviceGuard dg(s->device);
+        s->timer.reset();
+    });
+}
+
+}  // extern "C"

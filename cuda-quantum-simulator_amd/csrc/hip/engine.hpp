@@ -1,0 +1,151 @@
+// engine.hpp — internal declarations shared by the HIP translation units of libqsim_hip.so.
+//
+// Nothing here crosses the C ABI (include/qsim_hip.h).  Host code lowers each reference
+// GateOp (include/Circuit.hpp:64-84) to an `Op`: a (multi-)controlled 2x2 unitary on one
+// target, a (multi-)controlled diagonal, or a SWAP.  The kernels only know those three kinds.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "qsim_hip.h"
+
+namespace qsim_hip {
+
+// ---------------------------------------------------------------------------------------
+// Errors (mapped to QSIM_ERR_* at the ABI boundary)
+// ---------------------------------------------------------------------------------------
+struct Error : std::runtime_error {
+    int code;
+    Error(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+[[noreturn]] inline void fail(int code, const std::string& m) { throw Error(code, m); }
+// Thread-local message returned by qsim_last_error() (capi.hip).
+void set_last_error(const char* msg);
+
+#define QSIM_HIPCHK(call)                                                                   \
+    do {                                                                                    \
+        hipError_t e_ = (call);                                                             \
+        if (e_ != hipSuccess)                                                               \
+            ::qsim_hip::fail(QSIM_ERR_DEVICE, std::string("HIP error: ") +                  \
+                                                  hipGetErrorString(e_) + " at " __FILE__ ":" + \
+                                                  std::to_string(__LINE__));                \
+    } while (0)
+
+// ---------------------------------------------------------------------------------------
+// Lowered operations
+// ---------------------------------------------------------------------------------------
+enum Kind : int { K_M1 = 0, K_DIAG = 1, K_SWAP = 2 };
+
+// Sub-kinds select exact reference arithmetic where the reference kernel has a closed form
+// (src/Gates.cu:31-175), so per-gate results are bitwise those formulas.
+enum Sub : int {
+    S_GEN = 0,  // general complex 2x2 / general diagonal
+    S_X = 1,    // swap                                   (Gates.cu:31-44)
+    S_Y = 2,    // (im1,-re1),(-im0,re0)                  (Gates.cu:46-63)
+    S_H = 3,    // (a0+-a1)*0.7071067811865476            (Gates.cu:79-104)
+    S_NEG = 4,  // d1 = -1   (Z, CZ)                      (Gates.cu:65-77, 283-296)
+    S_I = 5,    // d1 = +i   (S)                          (Gates.cu:106-119)
+    S_MI = 6,   // d1 = -i   (Sdag)                       (Gates.cu:143-155)
+    S_T = 7,    // d1 = (1+i)/sqrt2  as (re-im, re+im)*c  (Gates.cu:121-141)
+    S_TDG = 8   // d1 = (1-i)/sqrt2  as (re+im, im-re)*c  (Gates.cu:157-175)
+};
+
+constexpr double kInvSqrt2 = 0.7071067811865476;  // literal used by src/Gates.cu:88
+
+struct Op {
+    int kind = K_M1;
+    int sub = S_GEN;
+    int t0 = 0, t1 = -1;   // target (t1: second SWAP qubit)
+    uint64_t cmask = 0;    // control qubits, all must read 1
+    bool d0_one = false;   // DIAG: d0 == 1 exactly -> only the |1> half is touched
+    double m[8] = {0};     // M1: a,b,c,d ; DIAG: d0,d1 (re,im interleaved)
+    int src = -1;          // index of the circuit gate this op came from
+    int ncontrols() const { return __builtin_popcountll(cmask); }
+};
+
+// Lower one reference gate (validated) to an Op.  Throws Error on bad input.
+Op lower_gate(const qsim_gate& g, int n_qubits);
+// Validate a gate against n qubits with the reference's rules (src/Circuit.cpp:16-55).
+void validate_gate(const qsim_gate& g, int n_qubits);
+// Algorithmic HBM bytes of one op over `amps` amplitudes.
+double op_alg_bytes(const Op& op, double amps);
+const char* gate_name(int type);
+
+// ---------------------------------------------------------------------------------------
+// Kernel launch interface (gates.hip)
+// ---------------------------------------------------------------------------------------
+struct Timer;  // per-launch HIP-event attribution (capi.hip)
+
+// Apply one op to `batch` contiguous trajectories of 2^n amplitudes each.
+void launch_op(double2* st, int n, uint64_t batch, const Op& op, hipStream_t s, Timer* tm);
+
+// Fused tile passes (fused.hip).
+struct FusedPass {
+    int single = -1;       // >= 0: not a tile pass but one per-gate op, Plan::singles[single]
+    int h = 0;             // number of high tile qubits (tile = 64 << h amplitudes)
+    int hpos[8] = {0};     // ascending physical qubit positions of the high tile bits (>= 6)
+    int op_begin = 0, op_end = 0;  // range in the pass-op buffer
+};
+struct TileOp {            // an Op re-expressed in tile-index bits
+    int kind, sub, b0, b1;
+    uint32_t cmask;
+    int d0_one;
+    double m[8];
+};
+struct Plan {
+    std::vector<FusedPass> passes;
+    std::vector<TileOp> ops;
+    std::vector<int> order;  // source gate index of each entry of `ops` (execution order)
+    std::vector<Op> singles;  // ops run by the per-gate kernels (gate wider than the tile, n < 6)
+    size_t fused_gate_count = 0;
+    size_t tile_passes = 0;
+};
+constexpr int kTileHMax = 6;  // 64 << 6 = 4096 amplitudes = 64 KiB of LDS per workgroup
+Plan plan_fused(const std::vector<Op>& ops, int n, int hmax = kTileHMax);
+void launch_fused(double2* st, int n, uint64_t batch, const Plan& plan, const TileOp* d_ops,
+                  hipStream_t s, Timer* tm);
+
+// Reductions / readout helpers (reduce.hip)
+void launch_init_basis(double2* st, int n, uint64_t batch, uint64_t basis, hipStream_t s);
+void launch_probabilities(const double2* st, uint64_t count, double* out, hipStream_t s);
+// sum over |a_i|^2 for i with ((i >> bit) & 1) == 0 (bit < 0: all), deterministic 2-pass.
+double reduce_norm(const double2* st, int n, int bit, double* d_partials, double* d_result,
+                   hipStream_t s);
+void launch_collapse(double2* st, int n, int bit, int result, double scale, hipStream_t s);
+void sample_indices(const double2* st, int n, const double* uniforms, int shots, int64_t* out,
+                    hipStream_t s);
+// Average of |a|^2 over `batch` trajectories into out[2^n] (device).
+void launch_avg_probabilities(const double2* st, int n, uint64_t batch, double* out,
+                              hipStream_t s);
+
+// ---------------------------------------------------------------------------------------
+// Timing (capi.hip): per-launch HIP events grouped by kernel name.
+// ---------------------------------------------------------------------------------------
+struct Timer {
+    struct Pending { int slot; hipEvent_t a, b; double bytes; };
+    struct Stat { std::string name; double ms = 0; int64_t launches = 0; double bytes = 0; };
+    bool enabled = false;
+    std::vector<Stat> stats;
+    std::vector<Pending> pending;
+    std::vector<hipEvent_t> pool;
+    hipStream_t stream = nullptr;
+    int slot_of(const char* name);
+    void begin(const char* name, double bytes, hipEvent_t* a_out, int* slot_out);
+    void end(int slot, hipEvent_t a, double bytes);
+    void resolve();   // synchronizes on outstanding events
+    void reset();
+    ~Timer();
+};
+// RAII scope used around each launch.
+struct TimedLaunch {
+    Timer* tm; int slot = -1; hipEvent_t a = nullptr; double bytes;
+    TimedLaunch(Timer* t, const char* name, double b, hipStream_t s);
+    ~TimedLaunch();
+};
+
+}  // namespace qsim_hip

@@ -1,0 +1,133 @@
+// NoiseModel.cpp — noise-channel container (reference src/NoiseModel.cu:24-101) and the
+// BatchedSimulator front end (src/NoiseModel.cu:653-972) over the qsim_batch C ABI.
+#include "qsim/NoiseModel.hpp"
+
+#include <numeric>
+#include <stdexcept>
+
+#include "abi_util.hpp"
+
+namespace qsim {
+
+using detail::check;
+
+// ---- NoiseModel: the per-qubit forms store one single-qubit channel per listed qubit; the
+// "global" forms store an empty qubit list (which the Monte-Carlo simulators apply to no qubit).
+void NoiseModel::addPerQubit(NoiseType t, const std::vector<int>& qubits, double p) {
+    for (int q : qubits) channels_.emplace_back(t, std::vector<int>{q}, p);
+}
+void NoiseModel::addDepolarizing(const std::vector<int>& q, double p) { addPerQubit(NoiseType::Depolarizing, q, p); }
+void NoiseModel::addAmplitudeDamping(const std::vector<int>& q, double g) { addPerQubit(NoiseType::AmplitudeDamping, q, g); }
+void NoiseModel::addPhaseDamping(const std::vector<int>& q, double g) { addPerQubit(NoiseType::PhaseDamping, q, g); }
+void NoiseModel::addBitFlip(const std::vector<int>& q, double p) { addPerQubit(NoiseType::BitFlip, q, p); }
+void NoiseModel::addPhaseFlip(const std::vector<int>& q, double p) { addPerQubit(NoiseType::PhaseFlip, q, p); }
+void NoiseModel::addBitPhaseFlip(const std::vector<int>& q, double p) { addPerQubit(NoiseType::BitPhaseFlip, q, p); }
+
+void NoiseModel::addDepolarizing(double p) { channels_.emplace_back(NoiseType::Depolarizing, std::vector<int>{}, p); }
+void NoiseModel::addAmplitudeDamping(double g) { channels_.emplace_back(NoiseType::AmplitudeDamping, std::vector<int>{}, g); }
+void NoiseModel::addPhaseDamping(double g) { channels_.emplace_back(NoiseType::PhaseDamping, std::vector<int>{}, g); }
+void NoiseModel::addBitFlip(double p) { channels_.emplace_back(NoiseType::BitFlip, std::vector<int>{}, p); }
+void NoiseModel::addPhaseFlip(double p) { channels_.emplace_back(NoiseType::PhaseFlip, std::vector<int>{}, p); }
+void NoiseModel::addBitPhaseFlip(double p) { channels_.emplace_back(NoiseType::BitPhaseFlip, std::vector<int>{}, p); }
+
+static std::vector<int> allQubits(int n) {
+    std::vector<int> v(n);
+    std::iota(v.begin(), v.end(), 0);
+    return v;
+}
+void NoiseModel::addDepolarizingAll(int n, double p) { addDepolarizing(allQubits(n), p); }
+void NoiseModel::addAmplitudeDampingAll(int n, double g) { addAmplitudeDamping(allQubits(n), g); }
+void NoiseModel::addPhaseDampingAll(int n, double g) { addPhaseDamping(allQubits(n), g); }
+
+// ---- BatchedSimulator
+BatchedSimulator::BatchedSimulator(int num_qubits, int batch_size)
+    : num_qubits_(num_qubits), batch_size_(batch_size), rng_(std::random_device{}()) {
+    check(qsim_batch_create(num_qubits, batch_size, &h_));
+}
+
+BatchedSimulator::BatchedSimulator(int num_qubits, int batch_size, const NoiseModel& noise_model)
+    : BatchedSimulator(num_qubits, batch_size) {
+    noise_model_ = noise_model;
+}
+
+BatchedSimulator::~BatchedSimulator() {
+    if (h_) qsim_batch_destroy(h_);
+}
+
+BatchedSimulator::BatchedSimulator(BatchedSimulator&& o) noexcept
+    : num_qubits_(o.num_qubits_), batch_size_(o.batch_size_), h_(o.h_),
+      noise_model_(std::move(o.noise_model_)), gate_set_(o.gate_set_), rng_(o.rng_) {
+    o.h_ = nullptr;
+}
+
+BatchedSimulator& BatchedSimulator::operator=(BatchedSimulator&& o) noexcept {
+    if (this != &o) {
+        if (h_) qsim_batch_destroy(h_);
+        num_qubits_ = o.num_qubits_;
+        batch_size_ = o.batch_size_;
+        h_ = o.h_;
+        noise_model_ = std::move(o.noise_model_);
+        gate_set_ = o.gate_set_;
+        rng_ = o.rng_;
+        o.h_ = nullptr;
+    }
+    return *this;
+}
+
+void BatchedSimulator::setSeed(unsigned int seed) {
+    rng_.seed(seed);
+    check(qsim_batch_set_seed(h_, seed));
+}
+
+void BatchedSimulator::reset() { check(qsim_batch_reset(h_)); }
+
+void BatchedSimulator::run(const Circuit& circuit) {
+    if (circuit.getNumQubits() != num_qubits_)
+        throw std::invalid_argument("Circuit qubit count doesn't match simulator");
+    const std::vector<qsim_gate> gates = detail::toAbi(circuit);
+    std::vector<qsim_noise_channel> ch;
+    for (const NoiseChannel& c : noise_model_.getChannels())
+        for (int q : c.qubits) ch.push_back(qsim_noise_channel{static_cast<int>(c.type), q, c.probability});
+    check(qsim_batch_run(h_, gates.data(), gates.size(), ch.data(), ch.size(),
+                         gate_set_ == BatchedGateSet::Reference ? QSIM_BATCH_REFERENCE_GATESET
+                                                                : QSIM_BATCH_FULL_GATESET));
+}
+
+std::vector<double> BatchedSimulator::getAverageProbabilities() const {
+    std::vector<double> p(size_t(1) << num_qubits_);
+    check(qsim_batch_avg_probabilities(h_, p.data()));
+    return p;
+}
+
+std::vector<double> BatchedSimulator::getProbabilities(int t) const {
+    if (t < 0 || t >= batch_size_) throw std::out_of_range("Invalid trajectory index");
+    std::vector<double> p(size_t(1) << num_qubits_);
+    check(qsim_batch_traj_probabilities(h_, t, p.data()));
+    return p;
+}
+
+std::vector<std::vector<int>> BatchedSimulator::sample(int n_shots) {
+    if (n_shots < 0) throw std::invalid_argument("n_shots must be non-negative");
+    std::vector<std::vector<int>> out(n_shots, std::vector<int>(batch_size_));
+    std::uniform_real_distribution<double> dist(0.0, 1.0);
+    for (int t = 0; t < batch_size_; ++t) {
+        const std::vector<double> p = getProbabilities(t);
+        std::vector<double> cdf(p.size());
+        std::partial_sum(p.begin(), p.end(), cdf.begin());
+        for (int s = 0; s < n_shots; ++s) {
+            const double r = dist(rng_);
+            out[s][t] = (int)(std::lower_bound(cdf.begin(), cdf.end(), r) - cdf.begin());
+        }
+    }
+    return out;
+}
+
+std::vector<int> BatchedSimulator::getHistogram(int n_shots) {
+    std::vector<int> hist(size_t(1) << num_qubits_, 0);
+    for (const auto& shot : sample(n_shots))
+        for (int o : shot)
+            if (o < (int)hist.size()) ++hist[o];
+    return hist;
+}
+
+}  // namespace qsim

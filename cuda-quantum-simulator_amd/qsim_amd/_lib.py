@@ -1,0 +1,143 @@
+"""ctypes bindings of the C ABI (include/qsim_hip.h, include/qsim_circuits.h).
+
+The HIP engine (lib/libqsim_hip.so) is REQUIRED: there is no CPU fallback anywhere in this
+package.  If the shared object is missing or cannot be loaded, import fails loudly.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import (POINTER, Structure, c_char_p, c_double, c_int, c_int32, c_int64,
+                    c_size_t, c_uint, c_uint64, c_void_p)
+
+PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_DIR = os.path.join(PKG_ROOT, "lib")
+HIP_LIB_PATH = os.path.join(LIB_DIR, "libqsim_hip.so")
+API_LIB_PATH = os.path.join(LIB_DIR, "libqsim.so")
+
+QSIM_OK = 0
+QSIM_ERR_INVALID_ARGUMENT = 1
+QSIM_ERR_OUT_OF_RANGE = 2
+QSIM_ERR_RUNTIME = 3
+QSIM_ERR_DEVICE = 4
+
+QSIM_RUN_PER_GATE = 0
+QSIM_RUN_FUSED = 1
+QSIM_BATCH_FULL_GATESET = 0
+QSIM_BATCH_REFERENCE_GATESET = 1
+
+QSIM_CIRCUIT_BELL = 0
+QSIM_CIRCUIT_GHZ = 1
+QSIM_CIRCUIT_RANDOM = 2
+QSIM_CIRCUIT_RANDOM_HC = 3
+QSIM_CIRCUIT_SCALING = 4
+
+
+class qsim_gate(Structure):
+    _fields_ = [("type", c_int32), ("nqubits", c_int32), ("qubits", c_int32 * 3),
+                ("_pad", c_int32), ("parameter", c_double)]
+
+
+class qsim_noise_channel(Structure):
+    _fields_ = [("type", c_int32), ("qubit", c_int32), ("probability", c_double)]
+
+
+def _load(path: str) -> ctypes.CDLL:
+    if not os.path.exists(path):
+        raise ImportError(
+            f"qsim_amd: native library {path} is missing; build it with "
+            f"`python -c 'import __graft_entry__ as g; g.build()'` (no CPU fallback exists)")
+    return ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+
+
+hip = _load(HIP_LIB_PATH)
+api = _load(API_LIB_PATH)
+
+_P = c_void_p
+
+
+def _sig(lib, name, argtypes, restype=c_int):
+    f = getattr(lib, name)
+    f.argtypes = argtypes
+    f.restype = restype
+    return f
+
+
+# ---- engine (libqsim_hip.so)
+_sig(hip, "qsim_last_error", [], c_char_p)
+_sig(hip, "qsim_abi_version", [])
+_sig(hip, "qsim_device_count", [POINTER(c_int)])
+_sig(hip, "qsim_device_info", [c_int, c_char_p, c_size_t, POINTER(c_int), POINTER(c_size_t)])
+_sig(hip, "qsim_state_create", [c_int, POINTER(_P)])
+_sig(hip, "qsim_state_create_on", [c_int, c_int, POINTER(_P)])
+_sig(hip, "qsim_state_destroy", [_P])
+_sig(hip, "qsim_state_num_qubits", [_P, POINTER(c_int)])
+_sig(hip, "qsim_state_device_ptr", [_P, POINTER(_P)])
+_sig(hip, "qsim_state_stream", [_P, POINTER(_P)])
+_sig(hip, "qsim_state_init_zero", [_P])
+_sig(hip, "qsim_state_init_basis", [_P, c_uint64])
+_sig(hip, "qsim_state_sync", [_P])
+_sig(hip, "qsim_apply_gate", [_P, POINTER(qsim_gate)])
+_sig(hip, "qsim_run", [_P, POINTER(qsim_gate), c_size_t, c_int])
+_sig(hip, "qsim_apply_matrix1q", [_P, c_int, POINTER(c_double), POINTER(c_int), c_int])
+_sig(hip, "qsim_apply_gate_raw", [_P, c_int, POINTER(qsim_gate), _P])
+_sig(hip, "qsim_plan_fused", [c_int, POINTER(qsim_gate), c_size_t, c_int, _P, _P,
+                              POINTER(c_int32)])
+_sig(hip, "qsim_state_to_host", [_P, _P])
+_sig(hip, "qsim_state_from_host", [_P, _P])
+_sig(hip, "qsim_state_probabilities", [_P, _P])
+_sig(hip, "qsim_state_total_probability", [_P, POINTER(c_double)])
+_sig(hip, "qsim_state_prob_bit_zero", [_P, c_int, POINTER(c_double)])
+_sig(hip, "qsim_state_collapse", [_P, c_int, c_int, c_double])
+_sig(hip, "qsim_state_sample", [_P, _P, c_int, _P])
+_sig(hip, "qsim_state_profile", [_P, c_int])
+_sig(hip, "qsim_state_profile_count", [_P, POINTER(c_int)])
+_sig(hip, "qsim_state_profile_get", [_P, c_int, c_char_p, c_size_t, POINTER(c_double),
+                                     POINTER(c_int64), POINTER(c_double)])
+_sig(hip, "qsim_state_profile_reset", [_P])
+_sig(hip, "qsim_batch_create", [c_int, c_int, POINTER(_P)])
+_sig(hip, "qsim_batch_destroy", [_P])
+_sig(hip, "qsim_batch_reset", [_P])
+_sig(hip, "qsim_batch_set_seed", [_P, c_uint64])
+_sig(hip, "qsim_batch_run", [_P, POINTER(qsim_gate), c_size_t, POINTER(qsim_noise_channel),
+                             c_size_t, c_int])
+_sig(hip, "qsim_batch_avg_probabilities", [_P, _P])
+_sig(hip, "qsim_batch_traj_probabilities", [_P, c_int, _P])
+_sig(hip, "qsim_batch_traj_state", [_P, c_int, _P])
+_sig(hip, "qsim_batch_device_ptr", [_P, POINTER(_P)])
+_sig(hip, "qsim_batch_sync", [_P])
+_sig(hip, "qsim_batch_profile", [_P, c_int])
+_sig(hip, "qsim_batch_profile_count", [_P, POINTER(c_int)])
+_sig(hip, "qsim_batch_profile_get", [_P, c_int, c_char_p, c_size_t, POINTER(c_double),
+                                     POINTER(c_int64), POINTER(c_double)])
+
+# ---- C++ API library (libqsim.so): circuit factories
+_sig(api, "qsim_circuit_make", [c_int, c_int, c_int, c_uint, POINTER(qsim_gate), c_size_t,
+                                POINTER(c_size_t)])
+_sig(api, "qsim_circuit_depth", [c_int, POINTER(qsim_gate), c_size_t, POINTER(c_size_t)])
+_sig(api, "qsim_circuits_last_error", [], c_char_p)
+
+
+def raise_for(rc: int, msg_fn=None) -> None:
+    """Map a QSIM_ERR_* code to the reference's exception classes (Python analogues)."""
+    if rc == QSIM_OK:
+        return
+    msg = (msg_fn or hip.qsim_last_error)()
+    msg = msg.decode() if isinstance(msg, bytes) else str(msg)
+    if rc == QSIM_ERR_INVALID_ARGUMENT:
+        raise ValueError(msg)            # std::invalid_argument
+    if rc == QSIM_ERR_OUT_OF_RANGE:
+        raise IndexError(msg)            # std::out_of_range
+    raise RuntimeError(msg)              # std::runtime_error (incl. device errors)
+
+
+def check(rc: int) -> None:
+    raise_for(rc)
+
+
+def check_circ(rc: int) -> None:
+    raise_for(rc, api.qsim_circuits_last_error)
+
+
+def loaded_paths():
+    return [HIP_LIB_PATH, API_LIB_PATH]

@@ -1,0 +1,175 @@
+/*
+ * qsim_hip.h — C ABI of the MI355X (gfx950) state-vector engine.
+ *
+ * This is the drop-in boundary between host code (the C++17 API in
+ * include/qsim/ headers, the Python ctypes mirror, or any FFI) and the
+ * hand-written HIP kernels.  Plain C types only: opaque handles, pointers,
+ * sizes, int status codes.  No HIP, torch or C++ types cross it.
+ *
+ * Amplitude layout: 2^n interleaved {double re, double im} (16 B each),
+ * index bit q == qubit q (LSB-first; reference src/Gates.cu:19-25 and
+ * tests/test_gates.cu:258-273 pin this convention).
+ *
+ * Every entry point returns QSIM_OK (0) or a QSIM_ERR_* code; the message of
+ * the last failure on the calling thread is in qsim_last_error().
+ *
+ * Reference interfaces replaced (file:line in rylanmalarchick/cuda-quantum-simulator):
+ *   StateVector ctor/alloc/init      include/StateVector.cuh:66-86, src/StateVector.cu:130-202
+ *   Gates.cuh __global__ kernels     include/Gates.cuh:58-101 (launched per gate)
+ *   Simulator::run / applyGate       include/Simulator.hpp:53-85, src/Simulator.cu:28-154
+ *   toHost / getProbabilities        src/StateVector.cu:204-233
+ *   measure (prob + collapse)        src/StateVector.cu:260-314
+ *   sample                           src/Simulator.cu:164-185, src/StateVector.cu:316-342
+ *   OptimizedGates applyGate1Q_opt   include/OptimizedGates.cuh:91-93
+ *   BatchedSimulator                 include/NoiseModel.cuh:231-297, src/NoiseModel.cu:653-972
+ */
+#ifndef QSIM_HIP_H
+#define QSIM_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define QSIM_ABI_VERSION 1
+
+/* ---- status codes (mapped to the reference's exception types by the C++ layer) ---- */
+enum {
+    QSIM_OK = 0,
+    QSIM_ERR_INVALID_ARGUMENT = 1, /* std::invalid_argument (src/StateVector.cu:135-141, :261-266) */
+    QSIM_ERR_OUT_OF_RANGE = 2,     /* std::out_of_range (src/Circuit.cpp:26-31, src/NoiseModel.cu:917-919) */
+    QSIM_ERR_RUNTIME = 3,          /* std::runtime_error (zero-probability measure, unknown gate) */
+    QSIM_ERR_DEVICE = 4            /* std::runtime_error from a HIP/RCCL failure (CUDA_CHECK analogue) */
+};
+
+/* ---- gate types: numbering == reference enum class GateType (include/Circuit.hpp:42-59) ---- */
+enum {
+    QSIM_GATE_X = 0, QSIM_GATE_Y = 1, QSIM_GATE_Z = 2, QSIM_GATE_H = 3,
+    QSIM_GATE_S = 4, QSIM_GATE_T = 5, QSIM_GATE_SDAG = 6, QSIM_GATE_TDAG = 7,
+    QSIM_GATE_RX = 8, QSIM_GATE_RY = 9, QSIM_GATE_RZ = 10,
+    QSIM_GATE_CNOT = 11, QSIM_GATE_CZ = 12, QSIM_GATE_CRY = 13, QSIM_GATE_CRZ = 14,
+    QSIM_GATE_SWAP = 15, QSIM_GATE_TOFFOLI = 16,
+    QSIM_GATE_COUNT = 17
+};
+
+/* One circuit operation, same meaning as the reference GateOp (include/Circuit.hpp:64-84):
+ * qubits = [target] | [control, target] | [q1, q2] (SWAP) | [c1, c2, target]. */
+typedef struct qsim_gate {
+    int32_t type;      /* QSIM_GATE_* */
+    int32_t nqubits;   /* 1, 2 or 3 */
+    int32_t qubits[3];
+    int32_t _pad;
+    double  parameter; /* angle in radians for Rx/Ry/Rz/CRY/CRZ, else ignored */
+} qsim_gate;
+
+/* Execution flags for qsim_run / qsim_batch_run. */
+enum {
+    QSIM_RUN_PER_GATE = 0,   /* one kernel launch per gate (reference Simulator::run shape) */
+    QSIM_RUN_FUSED = 1       /* host planner groups gates into LDS-tiled fused passes */
+};
+
+typedef struct qsim_state qsim_state; /* one 2^n state vector on one GPU + its HIP stream */
+typedef struct qsim_batch qsim_batch; /* B trajectories of 2^n amplitudes (BatchedSimulator) */
+
+/* ---- library ---- */
+const char* qsim_last_error(void);
+int qsim_abi_version(void);
+int qsim_device_count(int* count);
+/* Name/bandwidth facts of the current device (for bench reports). name_len includes NUL. */
+int qsim_device_info(int device, char* name, size_t name_len, int* cu_count, size_t* total_mem);
+
+/* ---- state vector lifecycle (StateVector.cuh:66-86) ---- */
+/* 1 <= n_qubits <= QSIM_MAX_QUBITS_SINGLE (30, Constants.hpp:68), else QSIM_ERR_INVALID_ARGUMENT.
+ * The new state is |0...0> (src/StateVector.cu:130-143). */
+int qsim_state_create(int n_qubits, qsim_state** out);
+int qsim_state_create_on(int device, int n_qubits, qsim_state** out);
+int qsim_state_destroy(qsim_state* s);
+int qsim_state_num_qubits(const qsim_state* s, int* n);
+/* Raw device address of amplitude 0 (StateVector::devicePtr, StateVector.cuh:89-90). */
+int qsim_state_device_ptr(qsim_state* s, void** dptr);
+/* hipStream_t of the state, as an opaque pointer. */
+int qsim_state_stream(qsim_state* s, void** stream);
+int qsim_state_init_zero(qsim_state* s);                      /* initializeZero */
+int qsim_state_init_basis(qsim_state* s, uint64_t basis_idx);  /* initializeBasis; >= 2^n -> INVALID_ARGUMENT */
+int qsim_state_sync(qsim_state* s);
+
+/* ---- gate application ---- */
+/* Validate + apply one gate (Simulator::applyGate, src/Simulator.cu:38-46).  Asynchronous. */
+int qsim_apply_gate(qsim_state* s, const qsim_gate* g);
+/* Whole circuit (Simulator::run, src/Simulator.cu:28-36).  flags = QSIM_RUN_*.  Asynchronous. */
+int qsim_run(qsim_state* s, const qsim_gate* gates, size_t count, int flags);
+/* General 2x2 unitary [[a,b],[c,d]] on `target`, m = {a.re,a.im,b.re,b.im,c.re,c.im,d.re,d.im}
+ * (applyGate1Q_opt, include/OptimizedGates.cuh:91-93), optionally controlled on `controls`. */
+int qsim_apply_matrix1q(qsim_state* s, int target, const double m[8],
+                        const int* controls, int n_controls);
+/* Host-only introspection of the fused-pass planner (no device needed).  Writes, for each gate
+ * in execution order, its index in `gates` (order[count]) and its pass number (pass_of[count],
+ * -1 for gates executed per-gate), and the number of passes.  Gates are only reordered past
+ * gates on disjoint qubits. */
+int qsim_plan_fused(int n_qubits, const qsim_gate* gates, size_t count, int hmax,
+                    int32_t* order, int32_t* pass_of, int32_t* n_passes);
+/* Kernel-level entry on a raw device pointer (the reference's Gates.cuh kernels, launched by
+ * tests/test_statevector.cu:151-159).  stream may be NULL (the null stream). */
+int qsim_apply_gate_raw(void* dstate, int n_qubits, const qsim_gate* g, void* stream);
+
+/* ---- readout (each synchronizes the state's stream) ---- */
+int qsim_state_to_host(qsim_state* s, double* dst);            /* 2*2^n doubles */
+int qsim_state_from_host(qsim_state* s, const double* src);    /* 2*2^n doubles */
+int qsim_state_probabilities(qsim_state* s, double* dst);      /* 2^n doubles, |a_i|^2 */
+int qsim_state_total_probability(qsim_state* s, double* out);  /* device wave64 reduction */
+/* P(index bit `bit` == 0), device reduction (qubitProbabilityKernel src/StateVector.cu:83-99
+ * + host sum :280-287).  `bit` is an index bit: the C++ layer maps the reference's
+ * big-endian measure(q) to bit n-1-q. */
+int qsim_state_prob_bit_zero(qsim_state* s, int bit, double* out);
+/* Zero amplitudes whose `bit` != result, scale the rest (collapseStateKernel :105-124). */
+int qsim_state_collapse(qsim_state* s, int bit, int result, double scale);
+/* Draw `shots` basis indices from |a|^2 with uniforms u[i] in [0,1) supplied by the caller
+ * (host RNG keeps the reference's mt19937 stream): device CDF + binary search. */
+int qsim_state_sample(qsim_state* s, const double* uniforms, int shots, int64_t* out);
+
+/* ---- timing (bench / profiling) ---- */
+/* Enable per-launch HIP-event timing on the state's stream; kernels are attributed by name. */
+int qsim_state_profile(qsim_state* s, int enable);
+/* Number of distinct kernel names timed so far, and per-name stats (ms totals, launch counts). */
+int qsim_state_profile_count(qsim_state* s, int* n);
+int qsim_state_profile_get(qsim_state* s, int i, char* name, size_t name_len,
+                           double* total_ms, int64_t* launches, double* alg_bytes);
+int qsim_state_profile_reset(qsim_state* s);
+
+/* ---- batched trajectories (BatchedSimulator, include/NoiseModel.cuh:231-297) ---- */
+/* Noise channel on one qubit, NoiseType numbering == reference enum (NoiseModel.cuh:49-56). */
+typedef struct qsim_noise_channel {
+    int32_t type;   /* 0 Depolarizing, 1 AmplitudeDamping, 2 PhaseDamping, 3 BitFlip, 4 PhaseFlip, 5 BitPhaseFlip */
+    int32_t qubit;
+    double  probability;
+} qsim_noise_channel;
+
+int qsim_batch_create(int n_qubits, int batch_size, qsim_batch** out);
+int qsim_batch_destroy(qsim_batch* b);
+int qsim_batch_reset(qsim_batch* b);
+int qsim_batch_set_seed(qsim_batch* b, uint64_t seed);
+/* Apply the circuit to every trajectory; after each gate apply every channel (reference
+ * BatchedSimulator::run, src/NoiseModel.cu:815-831).  Gate semantics follow
+ * src/NoiseModel.cu:717-801 when flags has QSIM_BATCH_REFERENCE_GATESET, else the full gate set. */
+enum { QSIM_BATCH_FULL_GATESET = 0, QSIM_BATCH_REFERENCE_GATESET = 1 };
+int qsim_batch_run(qsim_batch* b, const qsim_gate* gates, size_t count,
+                   const qsim_noise_channel* channels, size_t n_channels, int flags);
+int qsim_batch_avg_probabilities(qsim_batch* b, double* dst);           /* 2^n */
+int qsim_batch_traj_probabilities(qsim_batch* b, int traj, double* dst);  /* 2^n */
+int qsim_batch_traj_state(qsim_batch* b, int traj, double* dst);          /* 2*2^n */
+int qsim_batch_device_ptr(qsim_batch* b, void** dptr);
+int qsim_batch_sync(qsim_batch* b);
+int qsim_batch_profile(qsim_batch* b, int enable);
+int qsim_batch_profile_count(qsim_batch* b, int* n);
+int qsim_batch_profile_get(qsim_batch* b, int i, char* name, size_t name_len,
+                           double* total_ms, int64_t* launches, double* alg_bytes);
+
+#define QSIM_MAX_QUBITS_SINGLE 30
+#define QSIM_MIN_QUBITS 1
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* QSIM_HIP_H */

@@ -1,0 +1,179 @@
+"""PARITY ORACLE (test infrastructure only) — independent numpy formulation + ctypes access to the
+C++ CPUSimulator restatement (cpu_simulator.hpp).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import this module, and
+only as the checker / timed CPU baseline.  The product never imports it.
+
+Two implementations, written differently on purpose:
+  * `run_numpy`: each gate is a small unitary contracted into the state viewed as a rank-n tensor
+    (np.tensordot over the gate's axes).  Gate matrices come from their textbook definitions
+    (Nielsen & Chuang ch.4); qubit q is index bit q (reference SURVEY F1), i.e. tensor axis n-1-q.
+    CRY/CRZ/Toffoli follow the reference GPU kernels src/Gates.cu:322-410.
+  * `run_cpu`: the C++ restatement of the reference CPUSimulator (src/Simulator.cu:191-345),
+    loaded from oracle/build/libqsim_oracle.so.
+The two are cross-checked in tests/test_oracle.py and both against the reference's known-answer
+vectors in tests/golden/.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Iterable, Sequence, Tuple
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ORACLE_LIB = os.path.join(HERE, "build", "libqsim_oracle.so")
+
+INV_SQRT2 = 0.70710678118654752440
+
+# (type, qubits, parameter) tuples; type numbering == reference GateType.
+Gate = Tuple[int, Sequence[int], float]
+
+
+def _mat1(t: int, th: float) -> np.ndarray:
+    c, s = np.cos(th / 2.0), np.sin(th / 2.0)
+    r = INV_SQRT2
+    return {
+        0: np.array([[0, 1], [1, 0]], complex),
+        1: np.array([[0, -1j], [1j, 0]], complex),
+        2: np.array([[1, 0], [0, -1]], complex),
+        3: np.array([[r, r], [r, -r]], complex),
+        4: np.array([[1, 0], [0, 1j]], complex),
+        5: np.array([[1, 0], [0, r + 1j * r]], complex),
+        6: np.array([[1, 0], [0, -1j]], complex),
+        7: np.array([[1, 0], [0, r - 1j * r]], complex),
+        8: np.array([[c, -1j * s], [-1j * s, c]], complex),
+        9: np.array([[c, -s], [s, c]], complex),
+        10: np.array([[c - 1j * s, 0], [0, c + 1j * s]], complex),
+    }[t]
+
+
+def _controlled(u: np.ndarray, ncontrols: int) -> np.ndarray:
+    """Matrix on (controls..., target) with controls as the most significant tensor axes."""
+    d = 2 ** (ncontrols + 1)
+    m = np.eye(d, dtype=complex)
+    m[d - 2:, d - 2:] = u
+    return m
+
+
+def gate_matrix(t: int, qubits: Sequence[int], th: float):
+    """Return (matrix, qubit order) where the matrix acts on tensor axes in that order
+    (first listed qubit = most significant axis of the small matrix)."""
+    if t <= 10:
+        return _mat1(t, th), [qubits[0]]
+    if t == 11:  # CNOT(control, target)
+        return _controlled(_mat1(0, 0.0), 1), [qubits[0], qubits[1]]
+    if t == 12:  # CZ
+        return _controlled(_mat1(2, 0.0), 1), [qubits[0], qubits[1]]
+    if t == 13:  # CRY
+        return _controlled(_mat1(9, th), 1), [qubits[0], qubits[1]]
+    if t == 14:  # CRZ
+        return _controlled(_mat1(10, th), 1), [qubits[0], qubits[1]]
+    if t == 15:  # SWAP
+        m = np.eye(4, dtype=complex)[[0, 2, 1, 3]]
+        return m, [qubits[0], qubits[1]]
+    if t == 16:  # Toffoli(c1, c2, target)
+        return _controlled(_mat1(0, 0.0), 2), [qubits[0], qubits[1], qubits[2]]
+    raise ValueError(f"unknown gate type {t}")
+
+
+def apply_numpy(state: np.ndarray, n: int, gate: Gate) -> np.ndarray:
+    t, qubits, th = gate
+    m, order = gate_matrix(t, list(qubits), th)
+    k = len(order)
+    psi = state.reshape((2,) * n)
+    axes = [n - 1 - q for q in order]
+    mt = m.reshape((2,) * (2 * k))
+    out = np.tensordot(mt, psi, axes=(list(range(k, 2 * k)), axes))
+    # tensordot puts the gate's output axes first; move them back to their positions
+    out = np.moveaxis(out, list(range(k)), axes)
+    return out.reshape(-1)
+
+
+def zero_state(n: int) -> np.ndarray:
+    s = np.zeros(1 << n, complex)
+    s[0] = 1.0
+    return s
+
+
+def run_numpy(n: int, gates: Iterable[Gate], state: np.ndarray | None = None) -> np.ndarray:
+    s = zero_state(n) if state is None else np.array(state, dtype=complex)
+    for g in gates:
+        s = apply_numpy(s, n, g)
+    return s
+
+
+def gates_of(circuit) -> list:
+    """(type, qubits, parameter) tuples from a qsim_amd.Circuit (or any getGates() provider)."""
+    return [(int(g.type), list(g.qubits), float(g.parameter)) for g in circuit.getGates()]
+
+
+# ---- C++ restatement of CPUSimulator -----------------------------------------------------
+class _Gate(ctypes.Structure):
+    _fields_ = [("type", ctypes.c_int32), ("nqubits", ctypes.c_int32),
+                ("qubits", ctypes.c_int32 * 3), ("_pad", ctypes.c_int32),
+                ("parameter", ctypes.c_double)]
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(ORACLE_LIB):
+            raise RuntimeError(f"oracle library missing: {ORACLE_LIB} (run make -C oracle)")
+        _lib = ctypes.CDLL(ORACLE_LIB)
+        _lib.qsim_oracle_run.argtypes = [ctypes.c_int, ctypes.POINTER(_Gate), ctypes.c_size_t,
+                                         ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+        _lib.qsim_oracle_sample.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                            ctypes.c_int, ctypes.c_void_p]
+        _lib.qsim_oracle_time_prefix.argtypes = [ctypes.c_int, ctypes.POINTER(_Gate),
+                                                 ctypes.c_size_t, ctypes.c_double,
+                                                 ctypes.POINTER(ctypes.c_size_t),
+                                                 ctypes.POINTER(ctypes.c_double)]
+    return _lib
+
+
+def _to_abi(gates: Sequence[Gate]):
+    arr = (_Gate * max(1, len(gates)))()
+    for i, (t, qs, th) in enumerate(gates):
+        arr[i].type = int(t)
+        arr[i].nqubits = len(qs)
+        for j, q in enumerate(qs):
+            arr[i].qubits[j] = int(q)
+        arr[i].parameter = float(th)
+    return arr
+
+
+def run_cpu(n: int, gates: Sequence[Gate], state: np.ndarray | None = None,
+            strict_cpu: bool = False) -> np.ndarray:
+    """C++ CPUSimulator restatement. strict_cpu=True keeps the reference's CRY/CRZ/CCX no-ops (F4)."""
+    gates = list(gates)
+    out = np.zeros(1 << n, complex) if state is None else np.array(state, dtype=complex)
+    rc = lib().qsim_oracle_run(n, _to_abi(gates), len(gates), 1 if strict_cpu else 0,
+                               0 if state is None else 1, out.ctypes.data_as(ctypes.c_void_p))
+    if rc != 0:
+        raise ValueError("oracle rejected input")
+    return out
+
+
+def sample_cpu(n: int, state: np.ndarray, uniforms: np.ndarray) -> np.ndarray:
+    st = np.ascontiguousarray(state, dtype=complex)
+    u = np.ascontiguousarray(uniforms, dtype=np.float64)
+    out = np.empty(u.size, dtype=np.int64)
+    lib().qsim_oracle_sample(n, st.ctypes.data_as(ctypes.c_void_p),
+                             u.ctypes.data_as(ctypes.c_void_p), int(u.size),
+                             out.ctypes.data_as(ctypes.c_void_p))
+    return out
+
+
+def time_prefix(n: int, gates: Sequence[Gate], budget_s: float):
+    """Single-threaded CPU baseline: gates of `gates` applied in order until budget_s elapses."""
+    gates = list(gates)
+    done = ctypes.c_size_t(0)
+    secs = ctypes.c_double(0.0)
+    lib().qsim_oracle_time_prefix(n, _to_abi(gates), len(gates), budget_s, ctypes.byref(done),
+                                  ctypes.byref(secs))
+    return done.value, secs.value
