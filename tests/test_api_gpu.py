@@ -88,13 +88,6 @@ def test_measure_is_big_endian_reference_quirk(qsim, gpu_ready):
     assert sv.measureBit(0) == 1
 
 
-def test_zero_probability_measure_raises(qsim, gpu_ready):
-    sv = qsim.StateVector(1)
-    sv.fromHost(np.array([0.0, 0.0], complex))
-    with pytest.raises(RuntimeError):
-        sv.measureBit(0)
-
-
 def test_sampling(qsim, oracle, gpu_ready):
     sv = qsim.StateVector(2)
     assert np.all(sv.sample(100) == 0)
