@@ -98,6 +98,31 @@ Timer::~Timer() {
     }
     for (auto e : pool) (void)hipEventDestroy(e);
 }
+void DevBuf::upload(const void* src, size_t bytes, hipStream_t s) {
+    if (bytes == 0) return;
+    if (shadow.size() == bytes && std::memcmp(shadow.data(), src, bytes) == 0) return;
+    if (copied) QSIM_HIPCHK(hipEventSynchronize(copied));  // previous copy done reading shadow
+    if (bytes > cap) {
+        if (ptr) {
+            QSIM_HIPCHK(hipStreamSynchronize(s));
+            QSIM_HIPCHK(hipFree(ptr));
+            ptr = nullptr;
+        }
+        cap = std::max<size_t>(bytes, 16384);
+        QSIM_HIPCHK(hipMalloc(&ptr, cap));
+    }
+    shadow.assign((const unsigned char*)src, (const unsigned char*)src + bytes);
+    QSIM_HIPCHK(hipMemcpyAsync(ptr, shadow.data(), bytes, hipMemcpyHostToDevice, s));
+    if (!copied) QSIM_HIPCHK(hipEventCreateWithFlags(&copied, hipEventDisableTiming));
+    QSIM_HIPCHK(hipEventRecord(copied, s));
+}
+DevBuf::~DevBuf() {
+    if (copied) {
+        (void)hipEventSynchronize(copied);
+        (void)hipEventDestroy(copied);
+    }
+    if (ptr) (void)hipFree(ptr);
+}
 TimedLaunch::TimedLaunch(Timer* t, const char* name, double b, hipStream_t s) : tm(t), bytes(b) {
     if (tm && tm->enabled) {
         tm->stream = s;
@@ -126,15 +151,13 @@ struct qsim_state {
     hipStream_t stream = nullptr;
     double* d_partials = nullptr;
     double* d_result = nullptr;
-    TileOp* d_ops = nullptr;
-    size_t d_ops_cap = 0;
+    DevBuf ops, stages;  // fused-plan descriptors, re-uploaded only when the plan changes
     Timer timer;
     ~qsim_state() {
         if (stream) (void)hipStreamSynchronize(stream);
         if (d) (void)hipFree(d);
         if (d_partials) (void)hipFree(d_partials);
         if (d_result) (void)hipFree(d_result);
-        if (d_ops) (void)hipFree(d_ops);
         if (stream) (void)hipStreamDestroy(stream);
     }
 };
@@ -155,20 +178,12 @@ static void check_state(const qsim_state* s) {
     if (!s) fail(QSIM_ERR_INVALID_ARGUMENT, "null state handle");
 }
 
-static void upload_ops(qsim_state* s, const std::vector<TileOp>& ops) {
-    if (ops.empty()) return;
-    if (ops.size() > s->d_ops_cap) {
-        if (s->d_ops) {
-            QSIM_HIPCHK(hipStreamSynchronize(s->stream));
-            QSIM_HIPCHK(hipFree(s->d_ops));
-            s->d_ops = nullptr;
-        }
-        size_t cap = std::max<size_t>(ops.size(), 256);
-        QSIM_HIPCHK(hipMalloc((void**)&s->d_ops, cap * sizeof(TileOp)));
-        s->d_ops_cap = cap;
-    }
-    QSIM_HIPCHK(hipMemcpyAsync(s->d_ops, ops.data(), ops.size() * sizeof(TileOp),
-                               hipMemcpyHostToDevice, s->stream));
+static void run_fused(qsim_state* s, const std::vector<Op>& ops) {
+    Plan plan = plan_fused(ops, s->n);
+    s->ops.upload(plan.ops.data(), plan.ops.size() * sizeof(TileOp), s->stream);
+    s->stages.upload(plan.stages.data(), plan.stages.size() * sizeof(Stage), s->stream);
+    launch_fused(s->d, s->n, 1, plan, (const TileOp*)s->ops.ptr, (const Stage*)s->stages.ptr,
+                 s->stream, &s->timer);
 }
 
 extern "C" {
@@ -306,9 +321,7 @@ int qsim_run(qsim_state* s, const qsim_gate* gates, size_t count, int flags) {
             ops.back().src = (int)i;
         }
         if (flags & QSIM_RUN_FUSED) {
-            Plan plan = plan_fused(ops, s->n);
-            upload_ops(s, plan.ops);
-            launch_fused(s->d, s->n, 1, plan, s->d_ops, s->stream, &s->timer);
+            run_fused(s, ops);
         } else {
             for (const Op& op : ops) launch_op(s->d, s->n, 1, op, s->stream, &s->timer);
         }
@@ -361,9 +374,17 @@ int qsim_plan_fused(int n_qubits, const qsim_gate* gates, size_t count, int hmax
                 ++k;
                 continue;
             }
-            for (int o = p.op_begin; o < p.op_end; ++o, ++k) {
+            auto emit = [&](int o) {
+                if (plan.order[o] < 0) return;  // 2nd/3rd controlled-X of a lowered SWAP
                 if (order) order[k] = plan.order[o];
                 if (pass_of) pass_of[k] = tile;
+                ++k;
+            };
+            if (p.stage_end > p.stage_begin) {
+                for (int s = p.stage_begin; s < p.stage_end; ++s)
+                    for (int o = plan.stages[s].op_begin; o < plan.stages[s].op_end; ++o) emit(o);
+            } else {
+                for (int o = p.op_begin; o < p.op_end; ++o) emit(o);
             }
             ++tile;
         }

@@ -89,18 +89,31 @@ struct FusedPass {
     int single = -1;       // >= 0: not a tile pass but one per-gate op, Plan::singles[single]
     int h = 0;             // number of high tile qubits (tile = 64 << h amplitudes)
     int hpos[8] = {0};     // ascending physical qubit positions of the high tile bits (>= 6)
-    int op_begin = 0, op_end = 0;  // range in the pass-op buffer
+    int op_begin = 0, op_end = 0;  // range in the pass-op buffer (unstaged kernel)
+    int stage_begin = 0, stage_end = 0;  // range in Plan::stages (staged kernel, h >= 4)
 };
 struct TileOp {            // an Op re-expressed in tile-index bits
     int kind, sub, b0, b1;
     uint32_t cmask;
     int d0_one;
+    int p0;                // staged kernel: register-bit position of the target (-1: thread bit)
+    uint32_t cm_reg;       // staged kernel: controls among the stage bits, in register-bit space
+    uint32_t cm_thr;       // staged kernel: controls among the other tile bits (tile space)
+    int _pad;
     double m[8];
+};
+// A stage of a staged tile pass: every thread holds the 2^rb amplitudes spanned by `fix` (the
+// stage's tile bits) in registers; ops in [op_begin, op_end) act on them with no LDS traffic.
+struct Stage {
+    uint32_t offs[16];     // tile-index offset of register r (spread of r over fix[])
+    int fix[4];            // ascending stage tile bits
+    int op_begin, op_end;
 };
 struct Plan {
     std::vector<FusedPass> passes;
     std::vector<TileOp> ops;
     std::vector<int> order;  // source gate index of each entry of `ops` (execution order)
+    std::vector<Stage> stages;
     std::vector<Op> singles;  // ops run by the per-gate kernels (gate wider than the tile, n < 6)
     size_t fused_gate_count = 0;
     size_t tile_passes = 0;
@@ -108,7 +121,7 @@ struct Plan {
 constexpr int kTileHMax = 6;  // 64 << 6 = 4096 amplitudes = 64 KiB of LDS per workgroup
 Plan plan_fused(const std::vector<Op>& ops, int n, int hmax = kTileHMax);
 void launch_fused(double2* st, int n, uint64_t batch, const Plan& plan, const TileOp* d_ops,
-                  hipStream_t s, Timer* tm);
+                  const Stage* d_stages, hipStream_t s, Timer* tm);
 
 // Reductions / readout helpers (reduce.hip)
 void launch_init_basis(double2* st, int n, uint64_t batch, uint64_t basis, hipStream_t s);
@@ -141,6 +154,18 @@ struct Timer {
     void reset();
     ~Timer();
 };
+// Device copy of a small host descriptor array (fused plans).  Uploads only when the bytes
+// change (a re-run of the same circuit re-uses the resident plan); the host shadow stays alive
+// until the async copy that reads it has completed.
+struct DevBuf {
+    void* ptr = nullptr;
+    size_t cap = 0;
+    std::vector<unsigned char> shadow;
+    hipEvent_t copied = nullptr;
+    void upload(const void* src, size_t bytes, hipStream_t s);
+    ~DevBuf();
+};
+
 // RAII scope used around each launch.
 struct TimedLaunch {
     Timer* tm; int slot = -1; hipEvent_t a = nullptr; double bytes;

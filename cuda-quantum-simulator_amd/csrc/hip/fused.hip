@@ -7,14 +7,17 @@
 // applies every planned gate whose qubits lie inside the tile, and writes it back.  HBM traffic
 // per pass is 32 B x 2^n, independent of how many gates the pass absorbs.
 //
-// The host planner walks the circuit in order and moves a gate into the current pass when its
-// qubits fit the tile and it shares no qubit with an earlier gate that was deferred (gates on
-// disjoint qubits commute exactly, so the product is unchanged).  Semantics of each gate are
-// the per-gate kernels' (device_ops.hpp), i.e. src/Gates.cu:31-410.
+// Inside a pass the gates are grouped into register stages (h >= 4): each thread pulls the
+// 2^(h-2) amplitudes spanned by the stage's target bits from LDS into registers, applies every
+// gate of the stage there (diagonal gates need no target bit at all), and writes them back — one
+// LDS round trip and one barrier per stage instead of per gate.
+//
+// Planner rule (both levels): a gate moves into the current pass/stage when its qubits fit and
+// it shares no qubit with an earlier gate that was deferred (gates on disjoint qubits commute
+// exactly).  Gate semantics are the per-gate kernels' (device_ops.hpp), i.e. src/Gates.cu.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
-#include <set>
 
 #include "device_ops.hpp"
 #include "engine.hpp"
@@ -28,6 +31,95 @@ static uint64_t op_qubits(const Op& op) {
     uint64_t m = op.cmask | (1ull << op.t0);
     if (op.kind == K_SWAP) m |= 1ull << op.t1;
     return m;
+}
+
+static TileOp make_tile_op(int kind, int sub, int b0, int b1, uint32_t cm, int d0_one,
+                           const double* m) {
+    TileOp t{};
+    t.kind = kind;
+    t.sub = sub;
+    t.b0 = b0;
+    t.b1 = b1;
+    t.cmask = cm;
+    t.d0_one = d0_one;
+    t.p0 = -1;
+    for (int i = 0; i < 8; ++i) t.m[i] = m ? m[i] : 0.0;
+    return t;
+}
+
+// Group one pass's ops (tile bits) into register stages of at most `rb` target bits.
+static void plan_stages(std::vector<TileOp>& pass_ops, std::vector<int>& pass_src, int tile_bits,
+                        int rb, Plan& plan, FusedPass& p) {
+    // SWAP -> three controlled-X on the register bits (exact data movement).
+    std::vector<TileOp> ops;
+    std::vector<int> src;
+    static const double xm[8] = {0, 0, 1, 0, 1, 0, 0, 0};
+    for (size_t i = 0; i < pass_ops.size(); ++i) {
+        const TileOp& t = pass_ops[i];
+        if (t.kind == K_SWAP) {
+            const uint32_t a = 1u << t.b0, b = 1u << t.b1;
+            ops.push_back(make_tile_op(K_M1, S_X, t.b1, -1, t.cmask | a, 0, xm));
+            ops.push_back(make_tile_op(K_M1, S_X, t.b0, -1, t.cmask | b, 0, xm));
+            ops.push_back(make_tile_op(K_M1, S_X, t.b1, -1, t.cmask | a, 0, xm));
+            src.push_back(pass_src[i]);  // the gate is reported once (introspection skips -1)
+            src.push_back(-1);
+            src.push_back(-1);
+        } else {
+            ops.push_back(t);
+            src.push_back(pass_src[i]);
+        }
+    }
+    p.stage_begin = (int)plan.stages.size();
+    std::vector<int> rem(ops.size());
+    for (size_t i = 0; i < rem.size(); ++i) rem[i] = (int)i;
+    while (!rem.empty()) {
+        uint32_t sbits = 0, blocked = 0;
+        std::vector<int> in, deferred;
+        for (int i : rem) {
+            const TileOp& t = ops[i];
+            const uint32_t need = t.kind == K_M1 ? (1u << t.b0) : 0u;
+            const uint32_t touch = t.cmask | (1u << t.b0);
+            if ((touch & blocked) == 0 && __builtin_popcount(sbits | need) <= rb) {
+                sbits |= need;
+                in.push_back(i);
+            } else {
+                deferred.push_back(i);
+                blocked |= touch;
+            }
+        }
+        // pad with the highest unused tile bits (threads then walk consecutive LDS slots)
+        for (int b = tile_bits - 1; b >= 0 && __builtin_popcount(sbits) < rb; --b) sbits |= 1u << b;
+        Stage st{};
+        int k = 0;
+        int pos_of[32];
+        for (int b = 0; b < tile_bits; ++b)
+            if ((sbits >> b) & 1u) {
+                st.fix[k] = b;
+                pos_of[b] = k;
+                ++k;
+            }
+        for (int r = 0; r < (1 << rb); ++r) {
+            uint32_t o = 0;
+            for (int i = 0; i < rb; ++i)
+                if ((r >> i) & 1) o |= 1u << st.fix[i];
+            st.offs[r] = o;
+        }
+        st.op_begin = (int)plan.ops.size();
+        for (int i : in) {
+            TileOp t = ops[i];
+            t.p0 = ((sbits >> t.b0) & 1u) ? pos_of[t.b0] : -1;  // M1 targets are always stage bits
+            t.cm_reg = 0;
+            for (int b = 0; b < tile_bits; ++b)
+                if (((t.cmask & sbits) >> b) & 1u) t.cm_reg |= 1u << pos_of[b];
+            t.cm_thr = t.cmask & ~sbits;
+            plan.ops.push_back(t);
+            plan.order.push_back(src[i]);
+        }
+        st.op_end = (int)plan.ops.size();
+        plan.stages.push_back(st);
+        rem.swap(deferred);
+    }
+    p.stage_end = (int)plan.stages.size();
 }
 
 Plan plan_fused(const std::vector<Op>& ops, int n, int hmax) {
@@ -79,23 +171,27 @@ Plan plan_fused(const std::vector<Op>& ops, int n, int hmax) {
                 bit_of[q] = 6 + k;
                 ++k;
             }
-        p.op_begin = (int)plan.ops.size();
+        std::vector<TileOp> tops;
+        std::vector<int> tsrc;
         for (const Op& op : in_pass) {
-            TileOp t{};
-            t.kind = op.kind;
-            t.sub = op.sub;
-            t.b0 = bit_of[op.t0];
-            t.b1 = op.kind == K_SWAP ? bit_of[op.t1] : -1;
-            if (t.kind == K_SWAP && t.b0 > t.b1) std::swap(t.b0, t.b1);
-            t.cmask = 0;
+            uint32_t cm = 0;
             for (int q = 0; q < n; ++q)
-                if ((op.cmask >> q) & 1ull) t.cmask |= 1u << bit_of[q];
-            t.d0_one = op.d0_one ? 1 : 0;
-            for (int i = 0; i < 8; ++i) t.m[i] = op.m[i];
-            plan.ops.push_back(t);
-            plan.order.push_back(op.src);
+                if ((op.cmask >> q) & 1ull) cm |= 1u << bit_of[q];
+            int b0 = bit_of[op.t0], b1 = op.kind == K_SWAP ? bit_of[op.t1] : -1;
+            if (op.kind == K_SWAP && b0 > b1) std::swap(b0, b1);
+            tops.push_back(make_tile_op(op.kind, op.sub, b0, b1, cm, op.d0_one ? 1 : 0, op.m));
+            tsrc.push_back(op.src);
         }
-        p.op_end = (int)plan.ops.size();
+        if (heff >= 4) {
+            plan_stages(tops, tsrc, 6 + heff, heff - 2, plan, p);
+        } else {
+            p.op_begin = (int)plan.ops.size();
+            for (size_t i = 0; i < tops.size(); ++i) {
+                plan.ops.push_back(tops[i]);
+                plan.order.push_back(tsrc[i]);
+            }
+            p.op_end = (int)plan.ops.size();
+        }
         plan.fused_gate_count += in_pass.size();
         plan.tile_passes += 1;
         plan.passes.push_back(p);
@@ -110,10 +206,12 @@ Plan plan_fused(const std::vector<Op>& ops, int n, int hmax) {
 struct FArgs {
     double2* st;
     const TileOp* ops;
+    const Stage* stages;
     uint64_t stride;     // 2^n
     uint64_t tpt_mask;   // tiles per trajectory - 1
     int log_tpt;
     int op_begin, op_end;
+    int stage_begin, stage_end;
     int hpos[8];
 };
 
@@ -140,31 +238,65 @@ __device__ __forceinline__ uint32_t ins0(uint32_t p, int b) {
     return ((p ^ lo) << 1) | lo;
 }
 
+// LDS slot of tile element j.  A ds_read/write_b128 bank row is 256 B = 16 amplitudes, so the
+// bank of an access is its low 4 index bits.  XOR-ing them with bits 4..7 keeps both access
+// families conflict-free: the coalesced HBM phases (consecutive threads = consecutive j) and
+// register stages whose bits include tile bits 0..3 (consecutive threads then stride 2^k
+// amplitudes, which without the swizzle all land in one 16-B bank slot).
+__device__ __forceinline__ uint32_t sw(uint32_t j) { return j ^ ((j >> 4) & 15u); }
+
+// HBM <-> LDS halves shared by both tile kernels: element j = r*256 + tid, low 6 bits are lanes.
+template <int H>
+__device__ __forceinline__ void tile_load(const FArgs& a, uint64_t base, double2* tile) {
+    constexpr int T = 64 << H;
+    constexpr int R = T >= 256 ? T / 256 : 1;
+    const int tid = threadIdx.x;
+    if constexpr (T >= 256) {  // every thread owns R elements: no guards (keeps v[] in VGPRs)
+        double2 v[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const uint32_t j = (uint32_t)(r * 256 + tid);
+            v[r] = a.st[base | (j & 63u) | spread<H>(j >> 6, a.hpos)];
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r) tile[sw(r * 256 + tid)] = v[r];
+    } else if (tid < T) {
+        const uint32_t j = (uint32_t)tid;
+        tile[sw(j)] = a.st[base | (j & 63u) | spread<H>(j >> 6, a.hpos)];
+    }
+}
+
+template <int H>
+__device__ __forceinline__ void tile_store(const FArgs& a, uint64_t base, const double2* tile) {
+    constexpr int T = 64 << H;
+    constexpr int R = T >= 256 ? T / 256 : 1;
+    const int tid = threadIdx.x;
+    if constexpr (T >= 256) {
+        double2 v[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) v[r] = tile[sw(r * 256 + tid)];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const uint32_t j = (uint32_t)(r * 256 + tid);
+            a.st[base | (j & 63u) | spread<H>(j >> 6, a.hpos)] = v[r];
+        }
+    } else if (tid < T) {
+        const uint32_t j = (uint32_t)tid;
+        a.st[base | (j & 63u) | spread<H>(j >> 6, a.hpos)] = tile[sw(j)];
+    }
+}
+
+// Unstaged kernel (h < 4): one LDS sweep + barrier per gate.
 template <int H>
 __global__ __launch_bounds__(256) void k_fused_tile(FArgs a) {
-    constexpr int T = 64 << H;                 // amplitudes per tile
-    constexpr int R = T >= 256 ? T / 256 : 1;  // loads per thread
+    constexpr int T = 64 << H;
     __shared__ double2 tile[T];
     const int tid = threadIdx.x;
     const uint64_t tile_id = blockIdx.x;
-    const uint64_t traj = tile_id >> a.log_tpt;
     const uint64_t base =
-        traj * a.stride + deposit_h<H>((tile_id & a.tpt_mask) << 6, a.hpos);
-
-    // HBM -> LDS: element j = r*256 + tid; low 6 bits are lanes (1 KiB runs).
-    double2 v[R];
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-        const uint32_t j = (uint32_t)(r * 256 + tid);
-        if (j < (uint32_t)T) v[r] = a.st[base | (j & 63u) | spread<H>(j >> 6, a.hpos)];
-    }
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-        const uint32_t j = (uint32_t)(r * 256 + tid);
-        if (j < (uint32_t)T) tile[j] = v[r];
-    }
+        (tile_id >> a.log_tpt) * a.stride + deposit_h<H>((tile_id & a.tpt_mask) << 6, a.hpos);
+    tile_load<H>(a, base, tile);
     __syncthreads();
-
     for (int o = a.op_begin; o < a.op_end; ++o) {
         const TileOp& op = a.ops[o];
         const int kind = op.kind, sub = op.sub, b0 = op.b0;
@@ -175,24 +307,23 @@ __global__ __launch_bounds__(256) void k_fused_tile(FArgs a) {
             for (uint32_t p = tid; p < (uint32_t)T / 2; p += 256) {
                 const uint32_t j0 = ins0(p, b0), j1 = j0 | (1u << b0);
                 if ((j0 & cm) == cm) {
-                    double2 x0 = tile[j0], x1 = tile[j1];
+                    double2 x0 = tile[sw(j0)], x1 = tile[sw(j1)];
                     m1_pair(sub, m0, m1, m2, m3, x0, x1);
-                    tile[j0] = x0;
-                    tile[j1] = x1;
+                    tile[sw(j0)] = x0;
+                    tile[sw(j1)] = x1;
                 }
             }
         } else if (kind == K_DIAG) {
             const double2 d0 = make_double2(op.m[0], op.m[1]), d1 = make_double2(op.m[2], op.m[3]);
-            const int d0_one = op.d0_one;
-            if (d0_one) {  // only the target==1 half, enumerated directly
+            if (op.d0_one) {  // only the target==1 half, enumerated directly
                 for (uint32_t p = tid; p < (uint32_t)T / 2; p += 256) {
                     const uint32_t j = ins0(p, b0) | (1u << b0);
-                    if ((j & cm) == cm) tile[j] = diag1(sub, d1, tile[j]);
+                    if ((j & cm) == cm) tile[sw(j)] = diag1(sub, d1, tile[sw(j)]);
                 }
             } else {
                 for (uint32_t j = tid; j < (uint32_t)T; j += 256)
                     if ((j & cm) == cm)
-                        tile[j] = diag_apply(sub, 0, d0, d1, (j >> b0) & 1u, tile[j]);
+                        tile[sw(j)] = diag_apply(sub, 0, d0, d1, (j >> b0) & 1u, tile[sw(j)]);
             }
         } else {  // K_SWAP, b0 < b1
             const int b1 = op.b1;
@@ -200,24 +331,140 @@ __global__ __launch_bounds__(256) void k_fused_tile(FArgs a) {
                 const uint32_t j = ins0(ins0(p, b0), b1);
                 const uint32_t ja = j | (1u << b1), jb = j | (1u << b0);
                 if ((j & cm) == cm) {
-                    const double2 xa = tile[ja], xb = tile[jb];
-                    tile[ja] = xb;
-                    tile[jb] = xa;
+                    const double2 xa = tile[sw(ja)], xb = tile[sw(jb)];
+                    tile[sw(ja)] = xb;
+                    tile[sw(jb)] = xa;
                 }
             }
         }
         __syncthreads();
     }
+    tile_store<H>(a, base, tile);
+}
 
+// Register-stage ops.  The target register bit P and the gate sub-kind are compile-time (one
+// dispatch per op, none per pair); controls become per-pair selects, never branches.
+template <int SUB>
+__device__ __forceinline__ void pair_t(double2 m0, double2 m1, double2 m2, double2 m3,
+                                       double2& a0, double2& a1) {
+    m1_pair(SUB, m0, m1, m2, m3, a0, a1);  // SUB folds to one arm after inlining
+}
+
+__device__ __forceinline__ double2 sel(bool c, double2 a, double2 b) {
+    return make_double2(c ? a.x : b.x, c ? a.y : b.y);
+}
+
+// Controls: register-bit controls (cm_reg) skip whole pairs by a scalar test on the
+// compile-time register index; thread-bit controls (cm_thr) are one per-thread select.
+template <int RB, int P, int SUB>
+__device__ __forceinline__ void stage_m1(double2 (&v)[1 << RB], uint32_t jb, const TileOp& op) {
+    const uint32_t cr = op.cm_reg, ct = op.cm_thr;
+    const double2 m0 = make_double2(op.m[0], op.m[1]), m1 = make_double2(op.m[2], op.m[3]);
+    const double2 m2 = make_double2(op.m[4], op.m[5]), m3 = make_double2(op.m[6], op.m[7]);
+    const bool thr_ok = (jb & ct) == ct;
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
-        const uint32_t j = (uint32_t)(r * 256 + tid);
-        if (j < (uint32_t)T) a.st[base | (j & 63u) | spread<H>(j >> 6, a.hpos)] = tile[j];
+    for (int r = 0; r < (1 << RB); ++r) {
+        if (r & (1 << P)) continue;
+        if (((uint32_t)r & cr) != cr) continue;  // uniform
+        double2 x0 = v[r], x1 = v[r | (1 << P)];
+        pair_t<SUB>(m0, m1, m2, m3, x0, x1);
+        if (ct) {
+            x0 = sel(thr_ok, x0, v[r]);
+            x1 = sel(thr_ok, x1, v[r | (1 << P)]);
+        }
+        v[r] = x0;
+        v[r | (1 << P)] = x1;
     }
 }
 
+template <int RB, int P>
+__device__ __forceinline__ void stage_m1_sub(double2 (&v)[1 << RB], uint32_t jb, const TileOp& op) {
+    switch (op.sub) {
+        case S_X: stage_m1<RB, P, S_X>(v, jb, op); break;
+        case S_H: stage_m1<RB, P, S_H>(v, jb, op); break;
+        case S_Y: stage_m1<RB, P, S_Y>(v, jb, op); break;
+        default: stage_m1<RB, P, S_GEN>(v, jb, op); break;
+    }
+}
+
+template <int RB, int SUB>
+__device__ __forceinline__ void stage_diag(double2 (&v)[1 << RB], uint32_t jb, const TileOp& op) {
+    const uint32_t cr = op.cm_reg, ct = op.cm_thr;
+    const int p0 = op.p0, d0_one = op.d0_one;
+    const double2 d0 = make_double2(op.m[0], op.m[1]), d1 = make_double2(op.m[2], op.m[3]);
+    const bool thr_ok = (jb & ct) == ct;
+    const int tbit = (int)((jb >> op.b0) & 1u);  // target bit when it is a thread bit
+#pragma unroll
+    for (int r = 0; r < (1 << RB); ++r) {
+        if (((uint32_t)r & cr) != cr) continue;  // uniform
+        if (p0 >= 0) {  // target is register bit p0: the arm is uniform per r
+            if ((r >> p0) & 1) {
+                v[r] = sel(thr_ok, diag1(SUB, d1, v[r]), v[r]);
+            } else if (!d0_one) {
+                v[r] = sel(thr_ok, cmul(d0, v[r]), v[r]);
+            }
+        } else {
+            const double2 nv = tbit ? diag1(SUB, d1, v[r]) : (d0_one ? v[r] : cmul(d0, v[r]));
+            v[r] = sel(thr_ok, nv, v[r]);
+        }
+    }
+}
+
+template <int RB>
+__device__ __forceinline__ void stage_op(double2 (&v)[1 << RB], uint32_t jb, const TileOp& op) {
+    if (op.kind == K_M1) {
+        switch (op.p0) {
+            case 0: stage_m1_sub<RB, 0>(v, jb, op); break;
+            case 1: stage_m1_sub<RB, 1>(v, jb, op); break;
+            case 2: if constexpr (RB > 2) stage_m1_sub<RB, 2>(v, jb, op); break;
+            case 3: if constexpr (RB > 3) stage_m1_sub<RB, 3>(v, jb, op); break;
+            default: break;
+        }
+    } else {  // K_DIAG (SWAPs were lowered to controlled-X by the planner)
+        switch (op.sub) {
+            case S_NEG: stage_diag<RB, S_NEG>(v, jb, op); break;
+            case S_I: stage_diag<RB, S_I>(v, jb, op); break;
+            case S_MI: stage_diag<RB, S_MI>(v, jb, op); break;
+            case S_T: stage_diag<RB, S_T>(v, jb, op); break;
+            case S_TDG: stage_diag<RB, S_TDG>(v, jb, op); break;
+            default: stage_diag<RB, S_GEN>(v, jb, op); break;
+        }
+    }
+}
+
+template <int H>
+__global__ __launch_bounds__(256, 2) void k_fused_staged(FArgs a) {  // 2 WGs/CU (LDS-bound)
+    constexpr int T = 64 << H;
+    constexpr int RB = H - 2;
+    constexpr int R = 1 << RB;
+    __shared__ double2 tile[T];
+    const int tid = threadIdx.x;
+    const uint64_t tile_id = blockIdx.x;
+    const uint64_t base =
+        (tile_id >> a.log_tpt) * a.stride + deposit_h<H>((tile_id & a.tpt_mask) << 6, a.hpos);
+    tile_load<H>(a, base, tile);
+    __syncthreads();
+    for (int s = a.stage_begin; s < a.stage_end; ++s) {
+        const Stage& st = a.stages[s];
+        uint32_t offs[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) offs[r] = st.offs[r];
+        uint32_t jb = (uint32_t)tid;  // thread index spread over the non-stage tile bits
+#pragma unroll
+        for (int i = 0; i < RB; ++i) jb = ins0(jb, st.fix[i]);
+        double2 v[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) v[r] = tile[sw(jb | offs[r])];
+        for (int o = st.op_begin; o < st.op_end; ++o) stage_op<RB>(v, jb, a.ops[o]);
+#pragma unroll
+        for (int r = 0; r < R; ++r) tile[sw(jb | offs[r])] = v[r];
+        __syncthreads();
+    }
+    tile_store<H>(a, base, tile);
+}
+
 void launch_fused(double2* st, int n, uint64_t batch, const Plan& plan, const TileOp* d_ops,
-                  hipStream_t s, Timer* tm) {
+                  const Stage* d_stages, hipStream_t s, Timer* tm) {
     const double pass_bytes = 32.0 * (double)(1ull << n) * (double)batch;
     for (const FusedPass& p : plan.passes) {
         if (p.single >= 0) {
@@ -227,9 +474,12 @@ void launch_fused(double2* st, int n, uint64_t batch, const Plan& plan, const Ti
         FArgs a{};
         a.st = st;
         a.ops = d_ops;
+        a.stages = d_stages;
         a.stride = 1ull << n;
         a.op_begin = p.op_begin;
         a.op_end = p.op_end;
+        a.stage_begin = p.stage_begin;
+        a.stage_end = p.stage_end;
         for (int i = 0; i < 8; ++i) a.hpos[i] = p.hpos[i];
         const int lt = n - 6 - p.h;
         a.log_tpt = lt;
@@ -237,16 +487,19 @@ void launch_fused(double2* st, int n, uint64_t batch, const Plan& plan, const Ti
         const uint64_t blocks = batch << lt;
         TimedLaunch tl(tm, "fused_tile", pass_bytes, s);
         switch (p.h) {
-#define QSIM_FUSED_CASE(HH) \
+#define QSIM_TILE_CASE(HH) \
     case HH: hipLaunchKernelGGL(k_fused_tile<HH>, dim3((unsigned)blocks), dim3(256), 0, s, a); break;
-            QSIM_FUSED_CASE(0)
-            QSIM_FUSED_CASE(1)
-            QSIM_FUSED_CASE(2)
-            QSIM_FUSED_CASE(3)
-            QSIM_FUSED_CASE(4)
-            QSIM_FUSED_CASE(5)
-            QSIM_FUSED_CASE(6)
-#undef QSIM_FUSED_CASE
+#define QSIM_STAGED_CASE(HH) \
+    case HH: hipLaunchKernelGGL(k_fused_staged<HH>, dim3((unsigned)blocks), dim3(256), 0, s, a); break;
+            QSIM_TILE_CASE(0)
+            QSIM_TILE_CASE(1)
+            QSIM_TILE_CASE(2)
+            QSIM_TILE_CASE(3)
+            QSIM_STAGED_CASE(4)
+            QSIM_STAGED_CASE(5)
+            QSIM_STAGED_CASE(6)
+#undef QSIM_TILE_CASE
+#undef QSIM_STAGED_CASE
             default: fail(QSIM_ERR_RUNTIME, "unsupported tile height");
         }
         QSIM_HIPCHK(hipGetLastError());
