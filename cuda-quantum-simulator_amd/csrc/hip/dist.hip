@@ -1,0 +1,662 @@
+// dist.hip — state vector sharded over the GPUs of one node, one process per GPU, RCCL over xGMI.
+//
+// The reference is single-GPU (README.md:361-367); SURVEY §8(e) specifies this extension.
+//
+// Layout: W = 2^g ranks, L = n - g local qubits.  Rank r owns the 2^L amplitudes whose top g
+// PHYSICAL index bits equal r.  Every rank keeps the same logical->physical qubit map `perm`:
+//   * SWAP gates only exchange two map entries (zero data movement);
+//   * controls on global (rank) bits are resolved per rank (the op is dropped on ranks whose bit
+//     is 0, the control is dropped on the others); a diagonal gate whose target is global becomes a
+//     uniform phase on the rank's shard;
+//   * a gate whose TARGET is global needs data from another rank: before it, the planner remaps
+//     qubits — the g logical qubits whose next use as a target lies furthest ahead become global —
+//     and executes the remap as one all-to-all: pack (gather the 2^k - 1 outgoing chunks by their
+//     local bits) -> grouped ncclSend/ncclRecv with the 2^k - 1 peers -> unpack.  With k = g all
+//     W - 1 xGMI links of every GPU carry 1/W of its shard concurrently.
+// Local work between remaps is the single-GPU engine (fused tile passes) on the 2^L shard.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "device_ops.hpp"
+#include "engine.hpp"
+#include "qsim_hip.h"
+
+using namespace qsim_hip;
+
+namespace qsim_hip {
+
+struct DStep {
+    int kind = 0;  // 0 ops, 1 exchange
+    int k = 0;
+    int gpos[8] = {0}, lpos[8] = {0};
+    std::vector<Op> ops;
+};
+
+// Logical target that must be local for gate g (2x2 ops), or -1 (diagonal, SWAP).
+static int needs_local(const qsim_gate& g) {
+    switch (g.type) {
+        case QSIM_GATE_X: case QSIM_GATE_Y: case QSIM_GATE_H: case QSIM_GATE_RX: case QSIM_GATE_RY:
+            return g.qubits[0];
+        case QSIM_GATE_CNOT: case QSIM_GATE_CRY:
+            return g.qubits[1];
+        case QSIM_GATE_TOFFOLI:
+            return g.qubits[2];
+        default:
+            return -1;
+    }
+}
+
+static std::vector<DStep> plan_dist(const qsim_gate* gates, size_t count, int n, int g, int rank,
+                                    std::vector<int>& perm) {
+    const int L = n - g;
+    auto rank_bit = [&](int p) { return (rank >> (p - L)) & 1; };
+    std::vector<DStep> steps;
+    DStep cur;
+    auto flush = [&]() {
+        if (!cur.ops.empty()) steps.push_back(cur);
+        cur = DStep();
+    };
+    for (size_t i = 0; i < count; ++i) validate_gate(gates[i], n);
+    for (size_t i = 0; i < count; ++i) {
+        const qsim_gate& gt = gates[i];
+        if (gt.type == QSIM_GATE_SWAP) {  // relabel only
+            std::swap(perm[gt.qubits[0]], perm[gt.qubits[1]]);
+            continue;
+        }
+        const int tq = needs_local(gt);
+        if (tq >= 0 && perm[tq] >= L) {
+            flush();
+            // desired global set: the g logical qubits whose next target use is furthest away
+            const size_t INF = count + 1;
+            std::vector<size_t> next(n, INF);
+            for (size_t j = count; j-- > i;) {
+                const int q = needs_local(gates[j]);
+                if (q >= 0) next[q] = j;
+            }
+            std::vector<int> order(n);
+            for (int q = 0; q < n; ++q) order[q] = q;
+            std::stable_sort(order.begin(), order.end(), [&](int a, int b) {
+                if (next[a] != next[b]) return next[a] > next[b];
+                const bool ga = perm[a] >= L, gb = perm[b] >= L;
+                if (ga != gb) return ga;          // keep current globals (no movement)
+                return perm[a] > perm[b];         // prefer high local positions (coalesced pack)
+            });
+            std::vector<char> want(n, 0);
+            for (int j = 0; j < g; ++j) want[order[j]] = 1;
+            std::vector<int> out, in;
+            for (int q = 0; q < n; ++q) {
+                if (perm[q] >= L && !want[q]) out.push_back(q);
+                if (perm[q] < L && want[q]) in.push_back(q);
+            }
+            DStep ex;
+            ex.kind = 1;
+            ex.k = (int)out.size();
+            for (int j = 0; j < ex.k; ++j) {
+                ex.gpos[j] = perm[out[j]];
+                ex.lpos[j] = perm[in[j]];
+                perm[out[j]] = ex.lpos[j];
+                perm[in[j]] = ex.gpos[j];
+            }
+            steps.push_back(ex);
+        }
+        qsim_gate pg = gt;
+        for (int j = 0; j < gt.nqubits; ++j) pg.qubits[j] = perm[gt.qubits[j]];
+        Op op = lower_gate(pg, n);
+        op.src = (int)i;
+        bool skip = false;
+        for (int c = L; c < n; ++c)
+            if ((op.cmask >> c) & 1ull) {
+                if (!rank_bit(c)) skip = true;
+                op.cmask &= ~(1ull << c);
+            }
+        if (skip) continue;
+        if (op.kind == K_DIAG && op.t0 >= L) {
+            const int b = rank_bit(op.t0);
+            if (!b && op.d0_one) continue;  // factor 1 on this rank
+            const double fr = b ? op.m[2] : op.m[0], fi = b ? op.m[3] : op.m[1];
+            int t = 0;
+            while (t < L - 1 && ((op.cmask >> t) & 1ull)) ++t;
+            op.t0 = t;
+            op.sub = S_GEN;
+            op.d0_one = false;
+            op.m[0] = op.m[2] = fr;
+            op.m[1] = op.m[3] = fi;
+        }
+        if (op.t0 >= L || (op.kind == K_SWAP && op.t1 >= L))
+            fail(QSIM_ERR_RUNTIME, "distributed planner left a global target");
+        cur.ops.push_back(op);
+    }
+    flush();
+    return steps;
+}
+
+// ---- exchange kernels ---------------------------------------------------------------------
+struct XArgs {
+    double2* st;
+    double2* buf;
+    uint64_t chunk;     // 2^(L-k) amplitudes
+    int chunk_log;
+    int k;
+    int my_c;
+    int sorted[8];      // ascending lpos
+    int lpos[8];        // chunk bit j <-> lpos[j]
+};
+
+__device__ __forceinline__ uint64_t xlocal(const XArgs& a, uint64_t e) {
+    const uint64_t c = e >> a.chunk_log;
+    uint64_t off = e & (a.chunk - 1);
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+        if (j < a.k) {
+            const uint64_t lo = off & ((1ull << a.sorted[j]) - 1ull);
+            off = ((off ^ lo) << 1) | lo;
+        }
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+        if (j < a.k) off |= ((c >> j) & 1ull) << a.lpos[j];
+    return off;
+}
+
+template <bool PACK>
+__global__ __launch_bounds__(256) void k_exchange_copy(XArgs a, uint64_t total) {
+    const uint64_t step = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += step) {
+        if ((int)(e >> a.chunk_log) == a.my_c) continue;
+        const uint64_t i = xlocal(a, e);
+        if (PACK) a.buf[e] = a.st[i];
+        else a.st[i] = a.buf[e];
+    }
+}
+
+}  // namespace qsim_hip
+
+#define QSIM_NCCLCHK(call)                                                              \
+    do {                                                                                \
+        ncclResult_t r_ = (call);                                                       \
+        if (r_ != ncclSuccess)                                                          \
+            fail(QSIM_ERR_DEVICE, std::string("RCCL error: ") + ncclGetErrorString(r_)); \
+    } while (0)
+
+// One rank's share: its amplitudes and the exchange staging buffers.
+struct Shard {
+    int rank = 0;
+    double2* d = nullptr;
+    double2* sendbuf = nullptr;
+    double2* recvbuf = nullptr;
+};
+
+// Real mode: one shard per process, peers reached through an RCCL communicator.
+// Virtual mode (qsim_dist_create_virtual): all W shards in this process on one GPU, exchanged by
+// device copies — the same planner, per-rank lowering and pack/unpack kernels, no RCCL.
+struct qsim_dist {
+    int n = 0, g = 0, L = 0, world = 1, device = 0;
+    bool virt = false;
+    std::vector<Shard> shards;
+    double* d_partials = nullptr;
+    double* d_result = nullptr;
+    hipStream_t stream = nullptr;
+    ncclComm_t comm = nullptr;
+    std::vector<int> perm;
+    DevBuf ops, stages;
+    Timer timer;
+    ~qsim_dist() {
+        (void)hipSetDevice(device);
+        if (stream) (void)hipStreamSynchronize(stream);
+        if (comm) (void)ncclCommDestroy(comm);
+        for (Shard& s : shards)
+            for (void* p : {(void*)s.d, (void*)s.sendbuf, (void*)s.recvbuf})
+                if (p) (void)hipFree(p);
+        if (d_partials) (void)hipFree(d_partials);
+        if (d_result) (void)hipFree(d_result);
+        if (stream) (void)hipStreamDestroy(stream);
+    }
+};
+
+namespace {
+template <typename F>
+int dguard(F&& f) {
+    try {
+        f();
+        return QSIM_OK;
+    } catch (const Error& e) {
+        set_last_error(e.what());
+        return e.code;
+    } catch (const std::exception& e) {
+        set_last_error(e.what());
+        return QSIM_ERR_RUNTIME;
+    }
+}
+void need(const qsim_dist* d) {
+    if (!d) fail(QSIM_ERR_INVALID_ARGUMENT, "null dist handle");
+}
+int log2_exact(int w) {
+    if (w < 1) fail(QSIM_ERR_INVALID_ARGUMENT, "world size must be positive");
+    int g = 0;
+    while ((1 << g) < w) ++g;
+    if ((1 << g) != w) fail(QSIM_ERR_INVALID_ARGUMENT, "world size must be a power of two");
+    return g;
+}
+void check_sizes(int n, int g) {
+    if (n < QSIM_MIN_QUBITS || n > QSIM_MAX_QUBITS_DIST)
+        fail(QSIM_ERR_INVALID_ARGUMENT, "Number of qubits out of range");
+    if (n - g < std::max(1, g))
+        fail(QSIM_ERR_INVALID_ARGUMENT, "too few qubits per rank for this world size");
+}
+void alloc_shards(qsim_dist* d, const std::vector<int>& ranks) {
+    const size_t bytes = sizeof(double2) << d->L;
+    for (int r : ranks) {
+        Shard s;
+        s.rank = r;
+        QSIM_HIPCHK(hipMalloc((void**)&s.d, bytes));
+        if (d->world > 1) {
+            QSIM_HIPCHK(hipMalloc((void**)&s.sendbuf, bytes));
+            QSIM_HIPCHK(hipMalloc((void**)&s.recvbuf, bytes));
+        }
+        d->shards.push_back(s);
+    }
+    QSIM_HIPCHK(hipMalloc((void**)&d->d_partials, 4096 * sizeof(double)));
+    QSIM_HIPCHK(hipMalloc((void**)&d->d_result, sizeof(double)));
+}
+void init_zero(qsim_dist* d) {
+    for (int q = 0; q < d->n; ++q) d->perm[q] = q;
+    for (Shard& s : d->shards) launch_init_basis(s.d, d->L, 1, s.rank == 0 ? 0 : ~0ull, d->stream);
+    QSIM_HIPCHK(hipStreamSynchronize(d->stream));
+}
+
+struct XPlan {
+    XArgs a;
+    int peer_of[256];
+};
+XPlan xplan(const qsim_dist* d, const Shard& sh, const DStep& ex) {
+    XPlan x{};
+    XArgs& a = x.a;
+    a.st = sh.d;
+    a.k = ex.k;
+    a.chunk_log = d->L - ex.k;
+    a.chunk = 1ull << a.chunk_log;
+    for (int j = 0; j < ex.k; ++j) {
+        a.lpos[j] = ex.lpos[j];
+        a.sorted[j] = ex.lpos[j];
+        a.my_c |= ((sh.rank >> (ex.gpos[j] - d->L)) & 1) << j;
+    }
+    std::sort(a.sorted, a.sorted + ex.k);
+    for (int c = 0; c < (1 << ex.k); ++c) {
+        int peer = sh.rank;
+        for (int j = 0; j < ex.k; ++j) {
+            const int b = ex.gpos[j] - d->L;
+            peer = (peer & ~(1 << b)) | (((c >> j) & 1) << b);
+        }
+        x.peer_of[c] = peer;
+    }
+    return x;
+}
+void copy_kernel(bool pack, XArgs a, uint64_t total, hipStream_t s) {
+    const unsigned blocks = (unsigned)std::min<uint64_t>((total + 255) / 256, 256 * 64);
+    if (pack) hipLaunchKernelGGL(k_exchange_copy<true>, dim3(blocks), dim3(256), 0, s, a, total);
+    else hipLaunchKernelGGL(k_exchange_copy<false>, dim3(blocks), dim3(256), 0, s, a, total);
+    QSIM_HIPCHK(hipGetLastError());
+}
+// Qubit remap: rank r sends its amplitudes with local bits lpos == c to the rank whose bits at
+// gpos are c, and stores what that rank sends at local bits == c (the swap of the two qubit
+// sets, SURVEY §8(e) "global<->local qubit swap by all-to-all").
+void exchange(qsim_dist* d, const DStep& ex) {
+    if (ex.k == 0) return;
+    const uint64_t total = 1ull << d->L;
+    const uint64_t chunk = total >> ex.k;
+    const double bytes = 2.0 * 16.0 * (double)(total - chunk) * (double)d->shards.size();
+    TimedLaunch tl(&d->timer, "alltoall_remap", bytes, d->stream);
+    std::vector<XPlan> xs;
+    for (Shard& sh : d->shards) {
+        xs.push_back(xplan(d, sh, ex));
+        XArgs a = xs.back().a;
+        a.buf = sh.sendbuf;
+        copy_kernel(true, a, total, d->stream);
+    }
+    if (!d->virt) {
+        const Shard& sh = d->shards[0];
+        const XPlan& x = xs[0];
+        QSIM_NCCLCHK(ncclGroupStart());
+        for (int c = 0; c < (1 << ex.k); ++c) {
+            if (c == x.a.my_c) continue;
+            const size_t cnt = (size_t)chunk * 2;
+            QSIM_NCCLCHK(ncclSend(sh.sendbuf + (uint64_t)c * chunk, cnt, ncclDouble, x.peer_of[c], d->comm, d->stream));
+            QSIM_NCCLCHK(ncclRecv(sh.recvbuf + (uint64_t)c * chunk, cnt, ncclDouble, x.peer_of[c], d->comm, d->stream));
+        }
+        QSIM_NCCLCHK(ncclGroupEnd());
+    } else {  // shard r's chunk c goes to shard peer(c), into that shard's slot my_c(r)
+        for (size_t i = 0; i < d->shards.size(); ++i) {
+            const XPlan& x = xs[i];
+            for (int c = 0; c < (1 << ex.k); ++c) {
+                if (c == x.a.my_c) continue;
+                Shard& dst = d->shards[x.peer_of[c]];
+                QSIM_HIPCHK(hipMemcpyAsync(dst.recvbuf + (uint64_t)x.a.my_c * chunk,
+                                           d->shards[i].sendbuf + (uint64_t)c * chunk,
+                                           chunk * sizeof(double2), hipMemcpyDeviceToDevice, d->stream));
+            }
+        }
+    }
+    for (size_t i = 0; i < d->shards.size(); ++i) {
+        XArgs a = xs[i].a;
+        a.buf = d->shards[i].recvbuf;
+        copy_kernel(false, a, total, d->stream);
+    }
+}
+double allreduce_sum(qsim_dist* d, double local) {
+    if (d->virt) return local;
+    QSIM_HIPCHK(hipMemcpyAsync(d->d_result, &local, sizeof(double), hipMemcpyHostToDevice, d->stream));
+    QSIM_NCCLCHK(ncclAllReduce(d->d_result, d->d_result, 1, ncclDouble, ncclSum, d->comm, d->stream));
+    double out = 0.0;
+    QSIM_HIPCHK(hipMemcpyAsync(&out, d->d_result, sizeof(double), hipMemcpyDeviceToHost, d->stream));
+    QSIM_HIPCHK(hipStreamSynchronize(d->stream));
+    return out;
+}
+void run_local(qsim_dist* d, Shard& sh, const std::vector<Op>& ops, int flags) {
+    if (flags & QSIM_RUN_FUSED) {
+        Plan plan = plan_fused(ops, d->L);
+        d->ops.upload(plan.ops.data(), plan.ops.size() * sizeof(TileOp), d->stream);
+        d->stages.upload(plan.stages.data(), plan.stages.size() * sizeof(Stage), d->stream);
+        launch_fused(sh.d, d->L, 1, plan, (const TileOp*)d->ops.ptr, (const Stage*)d->stages.ptr,
+                     d->stream, &d->timer);
+    } else {
+        for (const Op& op : ops) launch_op(sh.d, d->L, 1, op, d->stream, &d->timer);
+    }
+}
+}  // namespace
+
+extern "C" {
+
+int qsim_dist_unique_id(void* id_out) {
+    return dguard([&] {
+        if (!id_out) fail(QSIM_ERR_INVALID_ARGUMENT, "null id buffer");
+        static_assert(sizeof(ncclUniqueId) <= QSIM_DIST_UNIQUE_ID_BYTES, "unique id size");
+        ncclUniqueId id;
+        QSIM_NCCLCHK(ncclGetUniqueId(&id));
+        std::memset(id_out, 0, QSIM_DIST_UNIQUE_ID_BYTES);
+        std::memcpy(id_out, &id, sizeof(id));
+    });
+}
+
+int qsim_dist_create(int n_qubits, int rank, int world, const void* unique_id, int device,
+                     qsim_dist** out) {
+    return dguard([&] {
+        if (!out || !unique_id) fail(QSIM_ERR_INVALID_ARGUMENT, "null argument");
+        *out = nullptr;
+        const int g = log2_exact(world);
+        if (rank < 0 || rank >= world) fail(QSIM_ERR_INVALID_ARGUMENT, "rank out of range");
+        check_sizes(n_qubits, g);
+        auto d = std::make_unique<qsim_dist>();
+        d->n = n_qubits;
+        d->g = g;
+        d->L = n_qubits - g;
+        d->world = world;
+        d->device = device;
+        d->perm.resize(n_qubits);
+        QSIM_HIPCHK(hipSetDevice(device));
+        QSIM_HIPCHK(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
+        d->timer.stream = d->stream;
+        alloc_shards(d.get(), {rank});
+        ncclUniqueId id;
+        std::memcpy(&id, unique_id, sizeof(id));
+        QSIM_NCCLCHK(ncclCommInitRank(&d->comm, world, id, rank));
+        init_zero(d.get());
+        *out = d.release();
+    });
+}
+
+int qsim_dist_create_virtual(int n_qubits, int world, int device, qsim_dist** out) {
+    return dguard([&] {
+        if (!out) fail(QSIM_ERR_INVALID_ARGUMENT, "null argument");
+        *out = nullptr;
+        const int g = log2_exact(world);
+        check_sizes(n_qubits, g);
+        auto d = std::make_unique<qsim_dist>();
+        d->n = n_qubits;
+        d->g = g;
+        d->L = n_qubits - g;
+        d->world = world;
+        d->device = device;
+        d->virt = true;
+        d->perm.resize(n_qubits);
+        QSIM_HIPCHK(hipSetDevice(device));
+        QSIM_HIPCHK(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
+        d->timer.stream = d->stream;
+        std::vector<int> ranks(world);
+        for (int r = 0; r < world; ++r) ranks[r] = r;
+        alloc_shards(d.get(), ranks);
+        init_zero(d.get());
+        *out = d.release();
+    });
+}
+
+int qsim_dist_destroy(qsim_dist* d) {
+    return dguard([&] { delete d; });
+}
+
+int qsim_dist_reset(qsim_dist* d) {
+    return dguard([&] {
+        need(d);
+        QSIM_HIPCHK(hipSetDevice(d->device));
+        init_zero(d);
+    });
+}
+
+int qsim_dist_run(qsim_dist* d, const qsim_gate* gates, size_t count, int flags) {
+    return dguard([&] {
+        need(d);
+        if (!gates && count) fail(QSIM_ERR_INVALID_ARGUMENT, "null gate list");
+        QSIM_HIPCHK(hipSetDevice(d->device));
+        // Plan per shard (ranks differ only in which global controls/phases apply).
+        std::vector<std::vector<DStep>> plans;
+        std::vector<int> perm_after;
+        for (const Shard& sh : d->shards) {
+            std::vector<int> perm = d->perm;
+            plans.push_back(plan_dist(gates, count, d->n, d->g, sh.rank, perm));
+            perm_after = perm;
+        }
+        // Every rank's plan has the same exchange skeleton: walk the steps in lockstep.
+        std::vector<size_t> pos(d->shards.size(), 0);
+        for (;;) {
+            bool any = false;
+            for (size_t i = 0; i < d->shards.size(); ++i)  // local ops up to the next exchange
+                while (pos[i] < plans[i].size() && plans[i][pos[i]].kind == 0) {
+                    run_local(d, d->shards[i], plans[i][pos[i]].ops, flags);
+                    ++pos[i];
+                    any = true;
+                }
+            bool ex = pos[0] < plans[0].size();
+            for (size_t i = 1; i < d->shards.size(); ++i)
+                if ((pos[i] < plans[i].size()) != ex) fail(QSIM_ERR_RUNTIME, "exchange skeleton mismatch");
+            if (!ex) break;
+            exchange(d, plans[0][pos[0]]);
+            for (size_t i = 0; i < d->shards.size(); ++i) ++pos[i];
+            any = true;
+            if (!any) break;
+        }
+        d->perm = perm_after;
+    });
+}
+
+int qsim_dist_sync(qsim_dist* d) {
+    return dguard([&] {
+        need(d);
+        QSIM_HIPCHK(hipSetDevice(d->device));
+        QSIM_HIPCHK(hipStreamSynchronize(d->stream));
+    });
+}
+
+int qsim_dist_perm(qsim_dist* d, int32_t* perm) {
+    return dguard([&] {
+        need(d);
+        for (int q = 0; q < d->n; ++q) perm[q] = d->perm[q];
+    });
+}
+
+int qsim_dist_local_state(qsim_dist* d, double* dst) {
+    return dguard([&] {
+        need(d);
+        QSIM_HIPCHK(hipSetDevice(d->device));
+        const size_t bytes = sizeof(double2) << d->L;
+        for (size_t i = 0; i < d->shards.size(); ++i)  // virtual mode: all shards, rank order
+            QSIM_HIPCHK(hipMemcpyAsync((char*)dst + i * bytes, d->shards[i].d, bytes,
+                                       hipMemcpyDeviceToHost, d->stream));
+        QSIM_HIPCHK(hipStreamSynchronize(d->stream));
+    });
+}
+
+int qsim_dist_gather_state(qsim_dist* d, double* dst) {
+    return dguard([&] {
+        need(d);
+        QSIM_HIPCHK(hipSetDevice(d->device));
+        const uint64_t shard = 1ull << d->L;
+        const bool root = d->virt || d->shards[0].rank == 0;
+        double2* all = nullptr;
+        if (root) QSIM_HIPCHK(hipMalloc((void**)&all, (sizeof(double2) << d->n)));
+        if (d->virt) {
+            for (const Shard& s : d->shards)
+                QSIM_HIPCHK(hipMemcpyAsync(all + s.rank * shard, s.d, sizeof(double2) * shard,
+                                           hipMemcpyDeviceToDevice, d->stream));
+        } else {
+            QSIM_NCCLCHK(ncclGroupStart());
+            if (root) {
+                QSIM_HIPCHK(hipMemcpyAsync(all, d->shards[0].d, sizeof(double2) * shard,
+                                           hipMemcpyDeviceToDevice, d->stream));
+                for (int r = 1; r < d->world; ++r)
+                    QSIM_NCCLCHK(ncclRecv(all + r * shard, shard * 2, ncclDouble, r, d->comm, d->stream));
+            } else {
+                QSIM_NCCLCHK(ncclSend(d->shards[0].d, shard * 2, ncclDouble, 0, d->comm, d->stream));
+            }
+            QSIM_NCCLCHK(ncclGroupEnd());
+        }
+        QSIM_HIPCHK(hipStreamSynchronize(d->stream));
+        if (root) {
+            std::vector<double2> phys(1ull << d->n);
+            QSIM_HIPCHK(hipMemcpy(phys.data(), all, sizeof(double2) << d->n, hipMemcpyDeviceToHost));
+            QSIM_HIPCHK(hipFree(all));
+            if (dst) {
+                for (uint64_t i = 0; i < (1ull << d->n); ++i) {  // logical index -> physical
+                    uint64_t p = 0;
+                    for (int q = 0; q < d->n; ++q) p |= ((i >> q) & 1ull) << d->perm[q];
+                    dst[2 * i] = phys[p].x;
+                    dst[2 * i + 1] = phys[p].y;
+                }
+            }
+        }
+    });
+}
+
+int qsim_dist_total_probability(qsim_dist* d, double* out) {
+    return dguard([&] {
+        need(d);
+        QSIM_HIPCHK(hipSetDevice(d->device));
+        double local = 0.0;
+        for (const Shard& s : d->shards)
+            local += reduce_norm(s.d, d->L, -1, d->d_partials, d->d_result, d->stream);
+        *out = allreduce_sum(d, local);
+    });
+}
+
+int qsim_dist_prob_bit_zero(qsim_dist* d, int q, double* out) {
+    return dguard([&] {
+        need(d);
+        if (q < 0 || q >= d->n) fail(QSIM_ERR_INVALID_ARGUMENT, "bit out of range");
+        QSIM_HIPCHK(hipSetDevice(d->device));
+        const int p = d->perm[q];
+        double local = 0.0;
+        for (const Shard& s : d->shards) {
+            if (p < d->L) local += reduce_norm(s.d, d->L, p, d->d_partials, d->d_result, d->stream);
+            else if (!((s.rank >> (p - d->L)) & 1))
+                local += reduce_norm(s.d, d->L, -1, d->d_partials, d->d_result, d->stream);
+        }
+        *out = allreduce_sum(d, local);
+    });
+}
+
+int qsim_dist_profile(qsim_dist* d, int enable) {
+    return dguard([&] {
+        need(d);
+        d->timer.enabled = enable != 0;
+    });
+}
+
+int qsim_dist_profile_count(qsim_dist* d, int* n) {
+    return dguard([&] {
+        need(d);
+        QSIM_HIPCHK(hipSetDevice(d->device));
+        d->timer.resolve();
+        *n = (int)d->timer.stats.size();
+    });
+}
+
+int qsim_dist_profile_get(qsim_dist* d, int i, char* name, size_t name_len, double* total_ms,
+                          int64_t* launches, double* alg_bytes) {
+    return dguard([&] {
+        need(d);
+        QSIM_HIPCHK(hipSetDevice(d->device));
+        d->timer.resolve();
+        if (i < 0 || i >= (int)d->timer.stats.size()) fail(QSIM_ERR_OUT_OF_RANGE, "bad index");
+        const auto& st = d->timer.stats[i];
+        if (name && name_len) {
+            std::strncpy(name, st.name.c_str(), name_len - 1);
+            name[name_len - 1] = 0;
+        }
+        if (total_ms) *total_ms = st.ms;
+        if (launches) *launches = st.launches;
+        if (alg_bytes) *alg_bytes = st.bytes;
+    });
+}
+
+int qsim_dist_plan(int n, int world, int rank, const qsim_gate* gates, size_t count,
+                   int32_t* perm_inout, qsim_dist_step* steps, size_t step_cap, size_t* n_steps,
+                   qsim_op* ops, size_t op_cap, size_t* n_ops) {
+    return dguard([&] {
+        const int g = log2_exact(world);
+        check_sizes(n, g);
+        if (rank < 0 || rank >= world) fail(QSIM_ERR_INVALID_ARGUMENT, "rank out of range");
+        std::vector<int> perm(n);
+        for (int q = 0; q < n; ++q) perm[q] = perm_inout ? perm_inout[q] : q;
+        const std::vector<DStep> st = plan_dist(gates, count, n, g, rank, perm);
+        size_t si = 0, oi = 0;
+        for (const DStep& s : st) {
+            if (si < step_cap) {
+                qsim_dist_step& o = steps[si];
+                std::memset(&o, 0, sizeof(o));
+                o.kind = s.kind;
+                o.k = s.k;
+                o.op_begin = (int32_t)oi;
+                o.op_end = (int32_t)(oi + s.ops.size());
+                for (int j = 0; j < 8; ++j) {
+                    o.gpos[j] = s.gpos[j];
+                    o.lpos[j] = s.lpos[j];
+                }
+            }
+            for (const Op& op : s.ops) {
+                if (oi < op_cap) {
+                    qsim_op& r = ops[oi];
+                    r.kind = op.kind;
+                    r.sub = op.sub;
+                    r.t0 = op.t0;
+                    r.t1 = op.t1;
+                    r.cmask = op.cmask;
+                    r.d0_one = op.d0_one ? 1 : 0;
+                    r.src = op.src;
+                    for (int j = 0; j < 8; ++j) r.m[j] = op.m[j];
+                }
+                ++oi;
+            }
+            ++si;
+        }
+        if (n_steps) *n_steps = si;
+        if (n_ops) *n_ops = oi;
+        if (perm_inout)
+            for (int q = 0; q < n; ++q) perm_inout[q] = perm[q];
+    });
+}
+
+}  // extern "C"

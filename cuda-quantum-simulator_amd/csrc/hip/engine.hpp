@@ -91,6 +91,7 @@ struct FusedPass {
     int hpos[8] = {0};     // ascending physical qubit positions of the high tile bits (>= 6)
     int op_begin = 0, op_end = 0;  // range in the pass-op buffer (unstaged kernel)
     int stage_begin = 0, stage_end = 0;  // range in Plan::stages (staged kernel, h >= 4)
+    int hu_count = 0;      // unnormalized H butterflies in the pass: store scales by 2^(-k/2)
 };
 struct TileOp {            // an Op re-expressed in tile-index bits
     int kind, sub, b0, b1;

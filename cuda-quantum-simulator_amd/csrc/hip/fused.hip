@@ -18,6 +18,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 
 #include "device_ops.hpp"
 #include "engine.hpp"
@@ -70,6 +71,13 @@ static void plan_stages(std::vector<TileOp>& pass_ops, std::vector<int>& pass_sr
         }
     }
     p.stage_begin = (int)plan.stages.size();
+    p.hu_count = 0;
+    for (TileOp& t : ops) {
+        if (t.kind == K_M1 && t.sub == S_H) {
+            if (t.cmask == 0) ++p.hu_count;  // unnormalized butterfly in the staged kernel
+            else t.sub = S_GEN;              // (no controlled H in the gate set; keep it exact)
+        }
+    }
     std::vector<int> rem(ops.size());
     for (size_t i = 0; i < rem.size(); ++i) rem[i] = (int)i;
     while (!rem.empty()) {
@@ -213,6 +221,7 @@ struct FArgs {
     int op_begin, op_end;
     int stage_begin, stage_end;
     int hpos[8];
+    double scale;        // applied at the store: (1/sqrt2)^(unnormalized H butterflies)
 };
 
 template <int H>
@@ -275,6 +284,10 @@ __device__ __forceinline__ void tile_store(const FArgs& a, uint64_t base, const 
         double2 v[R];
 #pragma unroll
         for (int r = 0; r < R; ++r) v[r] = tile[sw(r * 256 + tid)];
+        if (a.scale != 1.0) {  // uniform
+#pragma unroll
+            for (int r = 0; r < R; ++r) v[r] = make_double2(v[r].x * a.scale, v[r].y * a.scale);
+        }
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             const uint32_t j = (uint32_t)(r * 256 + tid);
@@ -356,7 +369,14 @@ __device__ __forceinline__ double2 sel(bool c, double2 a, double2 b) {
 
 // Controls: register-bit controls (cm_reg) skip whole pairs by a scalar test on the
 // compile-time register index; thread-bit controls (cm_thr) are one per-thread select.
-template <int RB, int P, int SUB>
+// FP64 issue (16 lanes/clk/SIMD on gfx950) and instruction-cache footprint both matter here, so
+// the interpreter has exactly three 2x2 arms per target register bit P — swap (X, CNOT, CCX, the
+// SWAP lowering: selects only), the unnormalized Hadamard butterfly (a0+a1, a0-a1: 4 DP adds per
+// pair; the (1/sqrt2)^k of a pass is applied once when the tile is stored) and the general
+// complex 2x2 — and two diagonal arms (negate: Z/CZ; general phase).
+enum StageArm : int { A_SWAP = 0, A_HU = 1, A_GEN = 2 };
+
+template <int RB, int P, int ARM>
 __device__ __forceinline__ void stage_m1(double2 (&v)[1 << RB], uint32_t jb, const TileOp& op) {
     const uint32_t cr = op.cm_reg, ct = op.cm_thr;
     const double2 m0 = make_double2(op.m[0], op.m[1]), m1 = make_double2(op.m[2], op.m[3]);
@@ -366,69 +386,71 @@ __device__ __forceinline__ void stage_m1(double2 (&v)[1 << RB], uint32_t jb, con
     for (int r = 0; r < (1 << RB); ++r) {
         if (r & (1 << P)) continue;
         if (((uint32_t)r & cr) != cr) continue;  // uniform
-        double2 x0 = v[r], x1 = v[r | (1 << P)];
-        pair_t<SUB>(m0, m1, m2, m3, x0, x1);
-        if (ct) {
-            x0 = sel(thr_ok, x0, v[r]);
-            x1 = sel(thr_ok, x1, v[r | (1 << P)]);
+        const double2 a0 = v[r], a1 = v[r | (1 << P)];
+        double2 x0, x1;
+        if constexpr (ARM == A_SWAP) {
+            x0 = a1;
+            x1 = a0;
+        } else if constexpr (ARM == A_HU) {
+            x0 = make_double2(a0.x + a1.x, a0.y + a1.y);
+            x1 = make_double2(a0.x - a1.x, a0.y - a1.y);
+        } else {
+            x0 = cadd(cmul(m0, a0), cmul(m1, a1));
+            x1 = cadd(cmul(m2, a0), cmul(m3, a1));
+        }
+        if (ct) {  // uniform: only thread-bit-controlled ops pay for the select
+            x0 = sel(thr_ok, x0, a0);
+            x1 = sel(thr_ok, x1, a1);
         }
         v[r] = x0;
         v[r | (1 << P)] = x1;
     }
 }
 
-template <int RB, int P>
-__device__ __forceinline__ void stage_m1_sub(double2 (&v)[1 << RB], uint32_t jb, const TileOp& op) {
-    switch (op.sub) {
-        case S_X: stage_m1<RB, P, S_X>(v, jb, op); break;
-        case S_H: stage_m1<RB, P, S_H>(v, jb, op); break;
-        case S_Y: stage_m1<RB, P, S_Y>(v, jb, op); break;
-        default: stage_m1<RB, P, S_GEN>(v, jb, op); break;
-    }
-}
-
-template <int RB, int SUB>
+template <int RB, bool NEG>
 __device__ __forceinline__ void stage_diag(double2 (&v)[1 << RB], uint32_t jb, const TileOp& op) {
     const uint32_t cr = op.cm_reg, ct = op.cm_thr;
     const int p0 = op.p0, d0_one = op.d0_one;
     const double2 d0 = make_double2(op.m[0], op.m[1]), d1 = make_double2(op.m[2], op.m[3]);
     const bool thr_ok = (jb & ct) == ct;
-    const int tbit = (int)((jb >> op.b0) & 1u);  // target bit when it is a thread bit
+    const bool tbit = ((jb >> op.b0) & 1u) != 0;  // target bit when it is a thread bit
 #pragma unroll
     for (int r = 0; r < (1 << RB); ++r) {
         if (((uint32_t)r & cr) != cr) continue;  // uniform
-        if (p0 >= 0) {  // target is register bit p0: the arm is uniform per r
-            if ((r >> p0) & 1) {
-                v[r] = sel(thr_ok, diag1(SUB, d1, v[r]), v[r]);
-            } else if (!d0_one) {
-                v[r] = sel(thr_ok, cmul(d0, v[r]), v[r]);
-            }
+        if (p0 >= 0 && !((r >> p0) & 1) && d0_one) continue;  // uniform: |0> side untouched
+        const bool bit = p0 >= 0 ? (((r >> p0) & 1) != 0) : tbit;
+        const bool ok = thr_ok && (bit || !d0_one);
+        if constexpr (NEG) {  // d1 = -1, d0 = 1
+            v[r] = sel(ok, make_double2(-v[r].x, -v[r].y), v[r]);
         } else {
-            const double2 nv = tbit ? diag1(SUB, d1, v[r]) : (d0_one ? v[r] : cmul(d0, v[r]));
-            v[r] = sel(thr_ok, nv, v[r]);
+            const double2 f = make_double2(bit ? d1.x : d0.x, bit ? d1.y : d0.y);
+            v[r] = sel(ok, cmul(f, v[r]), v[r]);
         }
+    }
+}
+
+template <int RB, int P>
+__device__ __forceinline__ void stage_m1_arm(double2 (&v)[1 << RB], uint32_t jb, const TileOp& op) {
+    switch (op.sub) {
+        case S_X: stage_m1<RB, P, A_SWAP>(v, jb, op); break;
+        case S_H: stage_m1<RB, P, A_HU>(v, jb, op); break;
+        default: stage_m1<RB, P, A_GEN>(v, jb, op); break;
     }
 }
 
 template <int RB>
 __device__ __forceinline__ void stage_op(double2 (&v)[1 << RB], uint32_t jb, const TileOp& op) {
-    if (op.kind == K_M1) {
-        switch (op.p0) {
-            case 0: stage_m1_sub<RB, 0>(v, jb, op); break;
-            case 1: stage_m1_sub<RB, 1>(v, jb, op); break;
-            case 2: if constexpr (RB > 2) stage_m1_sub<RB, 2>(v, jb, op); break;
-            case 3: if constexpr (RB > 3) stage_m1_sub<RB, 3>(v, jb, op); break;
-            default: break;
-        }
-    } else {  // K_DIAG (SWAPs were lowered to controlled-X by the planner)
-        switch (op.sub) {
-            case S_NEG: stage_diag<RB, S_NEG>(v, jb, op); break;
-            case S_I: stage_diag<RB, S_I>(v, jb, op); break;
-            case S_MI: stage_diag<RB, S_MI>(v, jb, op); break;
-            case S_T: stage_diag<RB, S_T>(v, jb, op); break;
-            case S_TDG: stage_diag<RB, S_TDG>(v, jb, op); break;
-            default: stage_diag<RB, S_GEN>(v, jb, op); break;
-        }
+    if (op.kind == K_DIAG) {  // SWAPs were lowered to controlled-X by the planner
+        if (op.sub == S_NEG) stage_diag<RB, true>(v, jb, op);
+        else stage_diag<RB, false>(v, jb, op);
+        return;
+    }
+    switch (op.p0) {
+        case 0: stage_m1_arm<RB, 0>(v, jb, op); break;
+        case 1: stage_m1_arm<RB, 1>(v, jb, op); break;
+        case 2: if constexpr (RB > 2) stage_m1_arm<RB, 2>(v, jb, op); break;
+        case 3: if constexpr (RB > 3) stage_m1_arm<RB, 3>(v, jb, op); break;
+        default: break;
     }
 }
 
@@ -480,6 +502,8 @@ void launch_fused(double2* st, int n, uint64_t batch, const Plan& plan, const Ti
         a.op_end = p.op_end;
         a.stage_begin = p.stage_begin;
         a.stage_end = p.stage_end;
+        // (1/sqrt2)^k: exact power of two for even k, one rounding for odd k
+        a.scale = std::ldexp(1.0, -(p.hu_count / 2)) * ((p.hu_count & 1) ? kInvSqrt2 : 1.0);
         for (int i = 0; i < 8; ++i) a.hpos[i] = p.hpos[i];
         const int lt = n - 6 - p.h;
         a.log_tpt = lt;

@@ -111,6 +111,38 @@ _sig(hip, "qsim_batch_profile_count", [_P, POINTER(c_int)])
 _sig(hip, "qsim_batch_profile_get", [_P, c_int, c_char_p, c_size_t, POINTER(c_double),
                                      POINTER(c_int64), POINTER(c_double)])
 
+# ---- multi-GPU (sharded) state
+class qsim_op(Structure):
+    _fields_ = [("kind", c_int32), ("sub", c_int32), ("t0", c_int32), ("t1", c_int32),
+                ("cmask", c_uint64), ("d0_one", c_int32), ("src", c_int32),
+                ("m", c_double * 8)]
+
+
+class qsim_dist_step(Structure):
+    _fields_ = [("kind", c_int32), ("k", c_int32), ("op_begin", c_int32), ("op_end", c_int32),
+                ("gpos", c_int32 * 8), ("lpos", c_int32 * 8)]
+
+
+_sig(hip, "qsim_dist_unique_id", [_P])
+_sig(hip, "qsim_dist_create", [c_int, c_int, c_int, _P, c_int, POINTER(_P)])
+_sig(hip, "qsim_dist_create_virtual", [c_int, c_int, c_int, POINTER(_P)])
+_sig(hip, "qsim_dist_destroy", [_P])
+_sig(hip, "qsim_dist_run", [_P, POINTER(qsim_gate), c_size_t, c_int])
+_sig(hip, "qsim_dist_sync", [_P])
+_sig(hip, "qsim_dist_reset", [_P])
+_sig(hip, "qsim_dist_perm", [_P, POINTER(c_int32)])
+_sig(hip, "qsim_dist_local_state", [_P, _P])
+_sig(hip, "qsim_dist_gather_state", [_P, _P])
+_sig(hip, "qsim_dist_total_probability", [_P, POINTER(c_double)])
+_sig(hip, "qsim_dist_prob_bit_zero", [_P, c_int, POINTER(c_double)])
+_sig(hip, "qsim_dist_profile", [_P, c_int])
+_sig(hip, "qsim_dist_profile_count", [_P, POINTER(c_int)])
+_sig(hip, "qsim_dist_profile_get", [_P, c_int, c_char_p, c_size_t, POINTER(c_double),
+                                    POINTER(c_int64), POINTER(c_double)])
+_sig(hip, "qsim_dist_plan", [c_int, c_int, c_int, POINTER(qsim_gate), c_size_t, POINTER(c_int32),
+                             POINTER(qsim_dist_step), c_size_t, POINTER(c_size_t),
+                             POINTER(qsim_op), c_size_t, POINTER(c_size_t)])
+
 # ---- C++ API library (libqsim.so): circuit factories
 _sig(api, "qsim_circuit_make", [c_int, c_int, c_int, c_uint, POINTER(qsim_gate), c_size_t,
                                 POINTER(c_size_t)])

@@ -1,0 +1,143 @@
+"""Sharded multi-GPU state (qsim_dist_* of include/qsim_hip.h).
+
+One process per GPU: `DistributedSimulator(n, rank, world, unique_id, device)`; rank 0 creates the
+RCCL unique id with `unique_id()` and the launcher (torch.distributed over gloo, see
+dist_bench.py) broadcasts it.  `DistributedSimulator.virtual(n, world)` keeps all `world` shards in
+one process on one GPU (exchanges by device copies) — the same planner and kernels, used to test
+the sharded path on a single GPU.  `plan()` exposes the host planner (no GPU needed).
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import List, Optional, Tuple
+
+import numpy as np
+
+from . import _lib
+from .circuit import Circuit
+
+_c = ctypes
+UNIQUE_ID_BYTES = 128
+
+
+def unique_id() -> bytes:
+    buf = _c.create_string_buffer(UNIQUE_ID_BYTES)
+    _lib.check(_lib.hip.qsim_dist_unique_id(buf))
+    return buf.raw
+
+
+class DistributedSimulator:
+    def __init__(self, num_qubits: int, rank: int = 0, world: int = 1,
+                 uid: Optional[bytes] = None, device: int = 0, _virtual: bool = False):
+        self._h = _c.c_void_p()
+        self._n, self._world, self._rank = num_qubits, world, rank
+        self._virtual = _virtual
+        if _virtual:
+            _lib.check(_lib.hip.qsim_dist_create_virtual(num_qubits, world, device,
+                                                         _c.byref(self._h)))
+        else:
+            if uid is None:
+                if world != 1:
+                    raise ValueError("a unique id from rank 0 is required for world > 1")
+                uid = unique_id()
+            buf = _c.create_string_buffer(uid, UNIQUE_ID_BYTES)
+            _lib.check(_lib.hip.qsim_dist_create(num_qubits, rank, world, buf, device,
+                                                 _c.byref(self._h)))
+
+    @classmethod
+    def virtual(cls, num_qubits: int, world: int, device: int = 0) -> "DistributedSimulator":
+        return cls(num_qubits, 0, world, None, device, _virtual=True)
+
+    def __del__(self):
+        self.close()
+
+    def close(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            _lib.hip.qsim_dist_destroy(h)
+            self._h = _c.c_void_p()
+
+    def getNumQubits(self) -> int: return self._n
+    def getWorldSize(self) -> int: return self._world
+
+    def run(self, circuit: Circuit, fused: bool = True) -> None:
+        if circuit.getNumQubits() != self._n:
+            raise ValueError("Circuit qubit count doesn't match simulator")
+        arr, cnt = circuit.to_abi()
+        _lib.check(_lib.hip.qsim_dist_run(self._h, arr, cnt,
+                                          _lib.QSIM_RUN_FUSED if fused else _lib.QSIM_RUN_PER_GATE))
+
+    def synchronize(self) -> None: _lib.check(_lib.hip.qsim_dist_sync(self._h))
+    def reset(self) -> None: _lib.check(_lib.hip.qsim_dist_reset(self._h))
+
+    def perm(self) -> List[int]:
+        p = (_c.c_int32 * self._n)()
+        _lib.check(_lib.hip.qsim_dist_perm(self._h, p))
+        return list(p)
+
+    def getStateVector(self) -> Optional[np.ndarray]:
+        """Full logical-order state on rank 0 (collective); None on other ranks."""
+        out = np.empty(1 << self._n, dtype=np.complex128)
+        root = self._virtual or self._rank == 0
+        _lib.check(_lib.hip.qsim_dist_gather_state(self._h, out.ctypes.data_as(_c.c_void_p)
+                                                   if root else None))
+        return out if root else None
+
+    def localState(self) -> np.ndarray:
+        shards = self._world if self._virtual else 1
+        out = np.empty(shards << (self._n - (self._world.bit_length() - 1)), dtype=np.complex128)
+        _lib.check(_lib.hip.qsim_dist_local_state(self._h, out.ctypes.data_as(_c.c_void_p)))
+        return out
+
+    def getTotalProbability(self) -> float:
+        t = _c.c_double()
+        _lib.check(_lib.hip.qsim_dist_total_probability(self._h, _c.byref(t)))
+        return t.value
+
+    def probBitZero(self, q: int) -> float:
+        t = _c.c_double()
+        _lib.check(_lib.hip.qsim_dist_prob_bit_zero(self._h, q, _c.byref(t)))
+        return t.value
+
+    def profile(self, enable: bool = True) -> None:
+        _lib.check(_lib.hip.qsim_dist_profile(self._h, 1 if enable else 0))
+
+    def profileStats(self):
+        n = _c.c_int(0)
+        _lib.check(_lib.hip.qsim_dist_profile_count(self._h, _c.byref(n)))
+        out = []
+        for i in range(n.value):
+            name = _c.create_string_buffer(64)
+            ms, cnt, by = _c.c_double(), _c.c_int64(), _c.c_double()
+            _lib.check(_lib.hip.qsim_dist_profile_get(self._h, i, name, 64, _c.byref(ms),
+                                                      _c.byref(cnt), _c.byref(by)))
+            out.append({"name": name.value.decode(), "ms": ms.value, "launches": cnt.value,
+                        "alg_bytes": by.value})
+        return out
+
+
+def plan(circuit: Circuit, world: int, rank: int, perm: Optional[List[int]] = None):
+    """Host planner output for `rank`: (steps, ops, perm_after).  steps are dicts
+    {kind: 'ops'|'exchange', ...}; ops are dicts with the lowered op fields."""
+    n = circuit.getNumQubits()
+    arr, cnt = circuit.to_abi()
+    p = (_c.c_int32 * n)(*(perm if perm is not None else range(n)))
+    ns, no = _c.c_size_t(0), _c.c_size_t(0)
+    _lib.check(_lib.hip.qsim_dist_plan(n, world, rank, arr, cnt, None, None, 0, _c.byref(ns),
+                                       None, 0, _c.byref(no)))
+    steps = (_lib.qsim_dist_step * max(1, ns.value))()
+    ops = (_lib.qsim_op * max(1, no.value))()
+    _lib.check(_lib.hip.qsim_dist_plan(n, world, rank, arr, cnt, p, steps, ns.value, _c.byref(ns),
+                                       ops, no.value, _c.byref(no)))
+    out_ops = [{"kind": o.kind, "sub": o.sub, "t0": o.t0, "t1": o.t1, "cmask": o.cmask,
+                "d0_one": o.d0_one, "src": o.src,
+                "m": [complex(o.m[2 * i], o.m[2 * i + 1]) for i in range(4)]}
+               for o in ops[:no.value]]
+    out_steps = []
+    for s in steps[:ns.value]:
+        if s.kind == 1:
+            out_steps.append({"kind": "exchange", "k": s.k, "gpos": list(s.gpos[:s.k]),
+                              "lpos": list(s.lpos[:s.k])})
+        else:
+            out_steps.append({"kind": "ops", "ops": out_ops[s.op_begin:s.op_end]})
+    return out_steps, list(p)

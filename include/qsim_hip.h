@@ -166,6 +166,58 @@ int qsim_batch_profile_count(qsim_batch* b, int* n);
 int qsim_batch_profile_get(qsim_batch* b, int i, char* name, size_t name_len,
                            double* total_ms, int64_t* launches, double* alg_bytes);
 
+/* ---- multi-GPU: state sharded by its high physical qubits, one process per GPU, RCCL ----
+ * (the reference is single-GPU, README.md:361-367).  World size W = 2^g ranks;
+ * rank r holds the 2^(n-g) amplitudes whose top g PHYSICAL index bits equal r.  A logical->
+ * physical qubit map is kept on every rank: SWAP gates only relabel it, gates whose target sits
+ * on a global (rank) bit trigger an all-to-all qubit remap over RCCL. */
+typedef struct qsim_dist qsim_dist;
+#define QSIM_DIST_UNIQUE_ID_BYTES 128
+#define QSIM_MAX_QUBITS_DIST 36
+/* Lowered operation record (host planner output, see qsim_dist_plan). kind: 0 controlled 2x2
+ * (m = a,b,c,d), 1 controlled diagonal (m = d0,d1), 2 swap(t0,t1); qubits are PHYSICAL local
+ * positions of the rank the plan was made for. */
+typedef struct qsim_op {
+    int32_t kind, sub, t0, t1;
+    uint64_t cmask;
+    int32_t d0_one, src;
+    double m[8];
+} qsim_op;
+/* One plan step: kind 0 = ops[op_begin, op_end) on the local shard; kind 1 = exchange that
+ * swaps global physical positions gpos[i] with local positions lpos[i], i < k. */
+typedef struct qsim_dist_step {
+    int32_t kind, k;
+    int32_t op_begin, op_end;
+    int32_t gpos[8], lpos[8];
+} qsim_dist_step;
+
+int qsim_dist_unique_id(void* id_out);  /* ncclGetUniqueId, on rank 0 */
+int qsim_dist_create(int n_qubits, int rank, int world, const void* unique_id, int device,
+                     qsim_dist** out);
+/* Virtual ranks: all `world` shards in this process on one GPU, exchanged by device copies
+ * (same planner and pack/unpack kernels, no RCCL) — for testing the sharded path on one GPU. */
+int qsim_dist_create_virtual(int n_qubits, int world, int device, qsim_dist** out);
+int qsim_dist_destroy(qsim_dist* d);
+int qsim_dist_run(qsim_dist* d, const qsim_gate* gates, size_t count, int flags);
+int qsim_dist_sync(qsim_dist* d);
+int qsim_dist_reset(qsim_dist* d);                         /* |0..0>, identity qubit map */
+int qsim_dist_perm(qsim_dist* d, int32_t* perm);            /* logical -> physical, n entries */
+/* This rank's 2*2^(n-g) doubles (virtual mode: all shards in rank order, 2*2^n doubles). */
+int qsim_dist_local_state(qsim_dist* d, double* dst);
+/* Full state in LOGICAL index order on rank 0 (collective; dst may be NULL on other ranks). */
+int qsim_dist_gather_state(qsim_dist* d, double* dst);
+int qsim_dist_total_probability(qsim_dist* d, double* out); /* collective */
+int qsim_dist_prob_bit_zero(qsim_dist* d, int logical_bit, double* out);  /* collective */
+int qsim_dist_profile(qsim_dist* d, int enable);
+int qsim_dist_profile_count(qsim_dist* d, int* n);
+int qsim_dist_profile_get(qsim_dist* d, int i, char* name, size_t name_len, double* total_ms,
+                          int64_t* launches, double* alg_bytes);
+/* Host-only planner (no GPU, no RCCL): the exact step list qsim_dist_run executes on `rank`
+ * starting from qubit map perm_inout (updated).  Call with caps = 0 to size the output. */
+int qsim_dist_plan(int n_qubits, int world, int rank, const qsim_gate* gates, size_t count,
+                   int32_t* perm_inout, qsim_dist_step* steps, size_t step_cap, size_t* n_steps,
+                   qsim_op* ops, size_t op_cap, size_t* n_ops);
+
 #define QSIM_MAX_QUBITS_SINGLE 30
 #define QSIM_MIN_QUBITS 1
 

@@ -1,0 +1,114 @@
+"""CPU, multi-process (gloo): the sharded path's planner + exchange logic against the oracle.
+
+world_size 2 and 4 ranks run as separate processes (torch.multiprocessing, gloo over 127.0.0.1);
+each executes its own host plan (qsim_amd.dist.plan, the exact step list qsim_dist_run launches)
+on a numpy shard, performing every qubit remap as real isend/irecv exchanges.  Rank 0 gathers the
+shards, undoes the logical->physical map and compares with the CPUSimulator restatement at 1e-12.
+"""
+import math
+import os
+import socket
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+
+def free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def circuits(qsim, n):
+    out = [qsim.createRandomHCCircuit(n, 60, 42), qsim.createRandomCircuit(n, 80, 3)]
+    rng = np.random.default_rng(n)
+    c = qsim.Circuit(n)
+    for _ in range(90):
+        t = int(rng.integers(0, 17))
+        ar = 1 if t <= 10 else (2 if t <= 15 else 3)
+        qs = [int(x) for x in rng.choice(n, size=ar, replace=False)]
+        c.append(qsim.GateOp(t, qs, float(rng.uniform(0, 2 * math.pi))))
+    out.append(c)
+    return out
+
+
+def worker(rank, world, port, n, result_q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for p in (os.path.join(root, "cuda-quantum-simulator_amd"), os.path.join(root, "tests")):
+        sys.path.insert(0, p)
+    import torch.distributed as dist
+    import qsim_amd
+    import dist_exec
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        for ci, c in enumerate(circuits(qsim_amd, n)):
+            shard, perm = dist_exec.run_rank(n, world, rank, c, dist)
+            gathered = [torch.empty(2 * shard.size, dtype=torch.float64) for _ in range(world)] \
+                if rank == 0 else None
+            dist.gather(torch.from_numpy(shard.view(np.float64).copy()), gathered, dst=0)
+            if rank == 0:
+                full = dist_exec.assemble([g.numpy().view(np.complex128) for g in gathered], perm, n)
+                result_q.put((ci, full))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n", [(2, 7), (4, 8), (2, 10)])
+def test_sharded_plan_matches_oracle_gloo(qsim, oracle, world, n):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=worker, args=(r, world, port, n, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = {}
+    try:
+        for _ in range(3):
+            ci, full = q.get(timeout=240)
+            got[ci] = full
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    for p in procs:
+        assert p.exitcode == 0
+    for ci, c in enumerate(circuits(qsim, n)):
+        ref = oracle.run_cpu(n, oracle.gates_of(c))
+        assert np.max(np.abs(got[ci] - ref)) < 1e-12, ci
+
+
+def test_plan_structure(qsim):
+    """SWAPs never move data; exchanges only when a target sits on a rank bit; all ranks share
+    the exchange skeleton."""
+    import qsim_amd.dist as qd
+    n, world = 10, 8
+    c = qsim.Circuit(n)
+    c.swap(0, 9).swap(1, 8).h(9).cnot(9, 2).cz(8, 7).crz(7, 9, 0.4).h(7).toffoli(9, 8, 1)
+    skel = None
+    for r in range(world):
+        steps, perm = qd.plan(c, world, r)
+        kinds = [s["kind"] for s in steps]
+        ex = [(s["k"], s["gpos"], s["lpos"]) for s in steps if s["kind"] == "exchange"]
+        skel = skel or (kinds.count("exchange"), ex)
+        assert (kinds.count("exchange"), ex) == skel
+        assert sorted(perm) == list(range(n))
+        for s in steps:
+            if s["kind"] == "ops":
+                for op in s["ops"]:
+                    assert op["t0"] < n - 3 and (op["kind"] != 2 or op["t1"] < n - 3)
+                    assert op["cmask"] < (1 << (n - 3))
+
+
+def test_plan_w_hc_30q_exchange_count(qsim):
+    import qsim_amd.dist as qd
+    c = qsim.createRandomHCCircuit(30, 100, 42)
+    steps, _ = qd.plan(c, 8, 0)
+    n_ex = sum(s["kind"] == "exchange" for s in steps)
+    assert 1 <= n_ex <= 12
