@@ -376,7 +376,11 @@ __device__ __forceinline__ double2 sel(bool c, double2 a, double2 b) {
 // complex 2x2 — and two diagonal arms (negate: Z/CZ; general phase).
 enum StageArm : int { A_SWAP = 0, A_HU = 1, A_GEN = 2 };
 
-template <int RB, int P, int ARM>
+// No per-pair branches: a branch around one pair makes the compiler merge two versions of the
+// register array (v_mov copies of every live amplitude).  Controls are therefore either absent
+// (PRED = false, pure arithmetic) or folded — register-bit part as a uniform scalar condition,
+// thread-bit part as a per-lane one — into one select per dword.
+template <int RB, int P, int ARM, bool PRED>
 __device__ __forceinline__ void stage_m1(double2 (&v)[1 << RB], uint32_t jb, const TileOp& op) {
     const uint32_t cr = op.cm_reg, ct = op.cm_thr;
     const double2 m0 = make_double2(op.m[0], op.m[1]), m1 = make_double2(op.m[2], op.m[3]);
@@ -384,8 +388,7 @@ __device__ __forceinline__ void stage_m1(double2 (&v)[1 << RB], uint32_t jb, con
     const bool thr_ok = (jb & ct) == ct;
 #pragma unroll
     for (int r = 0; r < (1 << RB); ++r) {
-        if (r & (1 << P)) continue;
-        if (((uint32_t)r & cr) != cr) continue;  // uniform
+        if (r & (1 << P)) continue;  // compile time
         const double2 a0 = v[r], a1 = v[r | (1 << P)];
         double2 x0, x1;
         if constexpr (ARM == A_SWAP) {
@@ -398,9 +401,10 @@ __device__ __forceinline__ void stage_m1(double2 (&v)[1 << RB], uint32_t jb, con
             x0 = cadd(cmul(m0, a0), cmul(m1, a1));
             x1 = cadd(cmul(m2, a0), cmul(m3, a1));
         }
-        if (ct) {  // uniform: only thread-bit-controlled ops pay for the select
-            x0 = sel(thr_ok, x0, a0);
-            x1 = sel(thr_ok, x1, a1);
+        if constexpr (PRED) {
+            const bool ok = (((uint32_t)r & cr) == cr) && thr_ok;
+            x0 = sel(ok, x0, a0);
+            x1 = sel(ok, x1, a1);
         }
         v[r] = x0;
         v[r | (1 << P)] = x1;
@@ -416,10 +420,8 @@ __device__ __forceinline__ void stage_diag(double2 (&v)[1 << RB], uint32_t jb, c
     const bool tbit = ((jb >> op.b0) & 1u) != 0;  // target bit when it is a thread bit
 #pragma unroll
     for (int r = 0; r < (1 << RB); ++r) {
-        if (((uint32_t)r & cr) != cr) continue;  // uniform
-        if (p0 >= 0 && !((r >> p0) & 1) && d0_one) continue;  // uniform: |0> side untouched
         const bool bit = p0 >= 0 ? (((r >> p0) & 1) != 0) : tbit;
-        const bool ok = thr_ok && (bit || !d0_one);
+        const bool ok = (((uint32_t)r & cr) == cr) && thr_ok && (bit || !d0_one);
         if constexpr (NEG) {  // d1 = -1, d0 = 1
             v[r] = sel(ok, make_double2(-v[r].x, -v[r].y), v[r]);
         } else {
@@ -431,10 +433,19 @@ __device__ __forceinline__ void stage_diag(double2 (&v)[1 << RB], uint32_t jb, c
 
 template <int RB, int P>
 __device__ __forceinline__ void stage_m1_arm(double2 (&v)[1 << RB], uint32_t jb, const TileOp& op) {
+    const bool pred = (op.cm_reg | op.cm_thr) != 0;
     switch (op.sub) {
-        case S_X: stage_m1<RB, P, A_SWAP>(v, jb, op); break;
-        case S_H: stage_m1<RB, P, A_HU>(v, jb, op); break;
-        default: stage_m1<RB, P, A_GEN>(v, jb, op); break;
+        case S_X:
+            if (pred) stage_m1<RB, P, A_SWAP, true>(v, jb, op);
+            else stage_m1<RB, P, A_SWAP, false>(v, jb, op);
+            break;
+        case S_H:  // never controlled (no CH in the gate set; the planner re-labels it S_GEN)
+            stage_m1<RB, P, A_HU, false>(v, jb, op);
+            break;
+        default:
+            if (pred) stage_m1<RB, P, A_GEN, true>(v, jb, op);
+            else stage_m1<RB, P, A_GEN, false>(v, jb, op);
+            break;
     }
 }
 
