@@ -81,6 +81,30 @@ __device__ __forceinline__ double2 diag_apply(int sub, int d0_one, double2 d0, d
     return d0_one ? a : cmul(d0, a);
 }
 
+// Streaming HBM access: in a per-gate kernel or a fused pass every amplitude is read and written
+// exactly once, so the non-temporal forms (no cache retention) are selectable per launch.
+typedef double dv2 __attribute__((ext_vector_type(2)));
+template <bool NT>
+__device__ __forceinline__ double2 ld(const double2* p) {
+    if constexpr (NT) {
+        const dv2 t = __builtin_nontemporal_load(reinterpret_cast<const dv2*>(p));
+        return make_double2(t.x, t.y);
+    } else {
+        return *p;
+    }
+}
+template <bool NT>
+__device__ __forceinline__ void st(double2* p, double2 v) {
+    if constexpr (NT) {
+        dv2 t;
+        t.x = v.x;
+        t.y = v.y;
+        __builtin_nontemporal_store(t, reinterpret_cast<dv2*>(p));
+    } else {
+        *p = v;
+    }
+}
+
 // 64-bit-lane shuffle of a complex amplitude (two ds_bpermute per double).
 __device__ __forceinline__ double2 shfl_xor2(double2 v, int mask) {
     return make_double2(__shfl_xor(v.x, mask), __shfl_xor(v.y, mask));

@@ -21,6 +21,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <string>
 
 #include "device_ops.hpp"
@@ -159,36 +160,38 @@ __device__ __forceinline__ uint64_t item_base(const GArgs& a, uint64_t item, int
 }
 
 // Slice mode: target >= 6, each wave-item is 64 pairs (two 1 KiB runs).
-template <int U>
+template <int U, bool NT>
 __global__ __launch_bounds__(256) void k_m1_slice(GArgs a) {
     const int lane = threadIdx.x & 63;
     const uint64_t first = (uint64_t)blockIdx.x * (4 * U) + (threadIdx.x >> 6);
     const uint64_t tb = 1ull << a.t0;
     double2 v0[U], v1[U];
     uint64_t i0[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-        const uint64_t item = first + 4 * u;
-        if (item < a.items) {
-            i0[u] = item_base(a, item, lane);
-            v0[u] = a.st[i0[u]];
-            v1[u] = a.st[i0[u] | tb];
-        }
-    }
+    // lanes failing a low control never load: with controls on bits >= 3 whole 128-B lines are
+    // skipped (CNOT with a low control moves N/2 amplitudes, not N)
     const bool lane_ok = (lane & a.lane_ctrl) == a.lane_ctrl;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
         const uint64_t item = first + 4 * u;
         if (item < a.items && lane_ok) {
+            i0[u] = item_base(a, item, lane);
+            v0[u] = ld<NT>(a.st + i0[u]);
+            v1[u] = ld<NT>(a.st + (i0[u] | tb));
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const uint64_t item = first + 4 * u;
+        if (item < a.items && lane_ok) {
             m1_pair(a.sub, a.m0, a.m1, a.m2, a.m3, v0[u], v1[u]);
-            a.st[i0[u]] = v0[u];
-            a.st[i0[u] | tb] = v1[u];
+            st<NT>(a.st + i0[u], v0[u]);
+            st<NT>(a.st + (i0[u] | tb), v1[u]);
         }
     }
 }
 
 // Lane mode: target < 6, each wave-item is 64 consecutive amplitudes; partner via shuffle.
-template <int U>
+template <int U, bool NT>
 __global__ __launch_bounds__(256) void k_m1_lane(GArgs a) {
     const int lane = threadIdx.x & 63;
     const uint64_t first = (uint64_t)blockIdx.x * (4 * U) + (threadIdx.x >> 6);
@@ -201,7 +204,7 @@ __global__ __launch_bounds__(256) void k_m1_lane(GArgs a) {
         v[u] = make_double2(0.0, 0.0);
         if (item < a.items && active) {
             idx[u] = item_base(a, item, lane);
-            v[u] = a.st[idx[u]];
+            v[u] = ld<NT>(a.st + idx[u]);
         }
     }
     const int tm = 1 << a.t0;
@@ -212,17 +215,19 @@ __global__ __launch_bounds__(256) void k_m1_lane(GArgs a) {
         const double2 p = shfl_xor2(v[u], tm);
         const uint64_t item = first + 4 * u;
         if (item < a.items && lane_ok) {
-            a.st[idx[u]] = m1_half(a.sub, a.m0, a.m1, a.m2, a.m3, bit, v[u], p);
+            st<NT>(a.st + idx[u], m1_half(a.sub, a.m0, a.m1, a.m2, a.m3, bit, v[u], p));
         }
     }
 }
 
 // Diagonal: per-amplitude phase.  Target may be a forced-1 position (d0 == 1, target >= 6).
-template <int U>
+template <int U, bool NT>
 __global__ __launch_bounds__(256) void k_diag(GArgs a) {
     const int lane = threadIdx.x & 63;
     const uint64_t first = (uint64_t)blockIdx.x * (4 * U) + (threadIdx.x >> 6);
-    const bool lane_ok = lane < a.nlanes && ((lane & a.lane_ctrl) == a.lane_ctrl);
+    // a phase on the |1> side only (d0 == 1) with a low target: lanes on the |0> side never load
+    const bool one_side = a.d0_one && a.t0 < 6 && !((lane >> a.t0) & 1);
+    const bool lane_ok = lane < a.nlanes && ((lane & a.lane_ctrl) == a.lane_ctrl) && !one_side;
     double2 v[U];
     uint64_t idx[U];
 #pragma unroll
@@ -230,7 +235,7 @@ __global__ __launch_bounds__(256) void k_diag(GArgs a) {
         const uint64_t item = first + 4 * u;
         if (item < a.items && lane_ok) {
             idx[u] = item_base(a, item, lane);
-            v[u] = a.st[idx[u]];
+            v[u] = ld<NT>(a.st + idx[u]);
         }
     }
 #pragma unroll
@@ -238,7 +243,7 @@ __global__ __launch_bounds__(256) void k_diag(GArgs a) {
         const uint64_t item = first + 4 * u;
         if (item < a.items && lane_ok) {
             const int bit = (int)((idx[u] >> a.t0) & 1ull);
-            if (bit || !a.d0_one) a.st[idx[u]] = diag_apply(a.sub, a.d0_one, a.m0, a.m1, bit, v[u]);
+            if (bit || !a.d0_one) st<NT>(a.st + idx[u], diag_apply(a.sub, a.d0_one, a.m0, a.m1, bit, v[u]));
         }
     }
 }
@@ -342,6 +347,28 @@ static void add_fix(GArgs& a, int pos) {
     }
 }
 
+// Launch-shape knobs (defaults from MI355X sweeps, DESIGN.md §per-gate kernels); overridable by
+// QSIM_SLICE_U / QSIM_LANE_U / QSIM_DIAG_U (wave-items in flight per lane) and QSIM_NT (0/1:
+// non-temporal HBM loads/stores) for tuning runs.
+struct Tune {
+    int slice_u = 1, lane_u = 2, diag_u = 2;
+    bool nt = true;
+    Tune() {
+        auto env = [](const char* k, int d) {
+            const char* v = std::getenv(k);
+            return v ? std::atoi(v) : d;
+        };
+        slice_u = env("QSIM_SLICE_U", slice_u);
+        lane_u = env("QSIM_LANE_U", lane_u);
+        diag_u = env("QSIM_DIAG_U", diag_u);
+        nt = env("QSIM_NT", nt ? 1 : 0) != 0;
+    }
+};
+static const Tune& tune() {
+    static const Tune t;
+    return t;
+}
+
 template <typename K>
 static void go(K kernel, const GArgs& a, int U, hipStream_t s) {
     const uint64_t per_block = 4ull * U;
@@ -381,20 +408,32 @@ void launch_op(double2* st, int n, uint64_t batch, const Op& op, hipStream_t s, 
         a.ipt_mask = (1ull << lb) - 1ull;
         a.items = batch << lb;
     };
-    const char* name = "?";
+    const Tune& T = tune();
+#define QSIM_GO_U(KERNEL, UVAL, CHOICES)                                            \
+    do {                                                                            \
+        const int u_ = (UVAL);                                                      \
+        if (T.nt) {                                                                 \
+            CHOICES(KERNEL, true)                                                   \
+        } else {                                                                    \
+            CHOICES(KERNEL, false)                                                  \
+        }                                                                           \
+    } while (0)
+#define QSIM_U248(KERNEL, NTV)                                                      \
+    if (u_ <= 1) go(KERNEL<1, NTV>, a, 1, s);                                       \
+    else if (u_ <= 2) go(KERNEL<2, NTV>, a, 2, s);                                  \
+    else if (u_ <= 4) go(KERNEL<4, NTV>, a, 4, s);                                  \
+    else go(KERNEL<8, NTV>, a, 8, s);
     switch (op.kind) {
         case K_M1:
             if (op.t0 >= 6) {
                 add_fix(a, op.t0);
                 finish();
-                name = "m1_slice";
-                TimedLaunch tl(tm, name, bytes, s);
-                go(k_m1_slice<4>, a, 4, s);
+                TimedLaunch tl(tm, "m1_slice", bytes, s);
+                QSIM_GO_U(k_m1_slice, T.slice_u, QSIM_U248);
             } else {
                 finish();
-                name = "m1_lane";
-                TimedLaunch tl(tm, name, bytes, s);
-                go(k_m1_lane<8>, a, 8, s);
+                TimedLaunch tl(tm, "m1_lane", bytes, s);
+                QSIM_GO_U(k_m1_lane, T.lane_u, QSIM_U248);
             }
             break;
         case K_DIAG:
@@ -403,10 +442,9 @@ void launch_op(double2* st, int n, uint64_t batch, const Op& op, hipStream_t s, 
                 a.setmask |= 1ull << op.t0;
             }
             finish();
-            name = "diag";
             {
-                TimedLaunch tl(tm, name, bytes, s);
-                go(k_diag<8>, a, 8, s);
+                TimedLaunch tl(tm, "diag", bytes, s);
+                QSIM_GO_U(k_diag, T.diag_u, QSIM_U248);
             }
             break;
         case K_SWAP:
