@@ -105,6 +105,20 @@ __device__ __forceinline__ void st(double2* p, double2 v) {
     }
 }
 
+// Wave-uniform read of a read-only launch table (fused-pass ops, stages).  Through the constant
+// address space the compiler emits scalar s_load into SGPRs (waited on lgkmcnt); a plain global
+// read of the same data becomes a vector load whose s_waitcnt vmcnt(0) also drains every
+// outstanding HBM load/store of the wave — one L2 round trip per op per tile.
+template <class T>
+__device__ __forceinline__ T ldc(const T* p, int i) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    typedef const __attribute__((address_space(4))) T* CP;
+    return *((CP)(p) + i);
+#else  // host pass of the single-source compile: never executed
+    return p[i];
+#endif
+}
+
 // 64-bit-lane shuffle of a complex amplitude (two ds_bpermute per double).
 __device__ __forceinline__ double2 shfl_xor2(double2 v, int mask) {
     return make_double2(__shfl_xor(v.x, mask), __shfl_xor(v.y, mask));

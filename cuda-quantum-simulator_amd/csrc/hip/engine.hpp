@@ -120,7 +120,8 @@ struct Plan {
     size_t tile_passes = 0;
 };
 constexpr int kTileHMax = 6;  // 64 << 6 = 4096 amplitudes = 64 KiB of LDS per workgroup
-Plan plan_fused(const std::vector<Op>& ops, int n, int hmax = kTileHMax);
+// hmax < 0: the process default (kTileHMax, or QSIM_TILE_HMAX for tuning runs).
+Plan plan_fused(const std::vector<Op>& ops, int n, int hmax = -1);
 void launch_fused(double2* st, int n, uint64_t batch, const Plan& plan, const TileOp* d_ops,
                   const Stage* d_stages, hipStream_t s, Timer* tm);
 

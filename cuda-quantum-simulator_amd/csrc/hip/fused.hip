@@ -132,6 +132,14 @@ static void plan_stages(std::vector<TileOp>& pass_ops, std::vector<int>& pass_sr
 }
 
 Plan plan_fused(const std::vector<Op>& ops, int n, int hmax) {
+    if (hmax < 0) {
+        static const int def = [] {
+            const char* e = std::getenv("QSIM_TILE_HMAX");
+            const int v = e ? std::atoi(e) : kTileHMax;
+            return std::min(kTileHMax, std::max(0, v));
+        }();
+        hmax = def;
+    }
     Plan plan;
     auto add_single = [&](const Op& op) {
         FusedPass p;
@@ -312,7 +320,7 @@ __global__ __launch_bounds__(256) void k_fused_tile(FArgs a) {
     tile_load<H>(a, base, tile);
     __syncthreads();
     for (int o = a.op_begin; o < a.op_end; ++o) {
-        const TileOp& op = a.ops[o];
+        const TileOp op = ldc(a.ops, o);
         const int kind = op.kind, sub = op.sub, b0 = op.b0;
         const uint32_t cm = op.cmask;
         if (kind == K_M1) {
@@ -466,20 +474,14 @@ __device__ __forceinline__ void stage_op(double2 (&v)[1 << RB], uint32_t jb, con
     }
 }
 
-template <int H, bool NT>
-__global__ __launch_bounds__(256, 2) void k_fused_staged(FArgs a) {  // 2 WGs/CU (LDS-bound)
-    constexpr int T = 64 << H;
+// The register stages of one tile (tile already in LDS; ends with a barrier).
+template <int H>
+__device__ __forceinline__ void run_stages(const FArgs& a, double2* tile) {
     constexpr int RB = H - 2;
     constexpr int R = 1 << RB;
-    __shared__ double2 tile[T];
     const int tid = threadIdx.x;
-    const uint64_t tile_id = blockIdx.x;
-    const uint64_t base =
-        (tile_id >> a.log_tpt) * a.stride + deposit_h<H>((tile_id & a.tpt_mask) << 6, a.hpos);
-    tile_load<H, NT>(a, base, tile);
-    __syncthreads();
     for (int s = a.stage_begin; s < a.stage_end; ++s) {
-        const Stage& st = a.stages[s];
+        const Stage st = ldc(a.stages, s);
         uint32_t offs[R];
 #pragma unroll
         for (int r = 0; r < R; ++r) offs[r] = st.offs[r];
@@ -489,11 +491,23 @@ __global__ __launch_bounds__(256, 2) void k_fused_staged(FArgs a) {  // 2 WGs/CU
         double2 v[R];
 #pragma unroll
         for (int r = 0; r < R; ++r) v[r] = tile[sw(jb | offs[r])];
-        for (int o = st.op_begin; o < st.op_end; ++o) stage_op<RB>(v, jb, a.ops[o]);
+        for (int o = st.op_begin; o < st.op_end; ++o) stage_op<RB>(v, jb, ldc(a.ops, o));
 #pragma unroll
         for (int r = 0; r < R; ++r) tile[sw(jb | offs[r])] = v[r];
         __syncthreads();
     }
+}
+
+template <int H, bool NT>
+__global__ __launch_bounds__(256, 2) void k_fused_staged(FArgs a) {  // 2 WGs/CU (LDS-bound)
+    constexpr int T = 64 << H;
+    __shared__ double2 tile[T];
+    const uint64_t tile_id = blockIdx.x;
+    const uint64_t base =
+        (tile_id >> a.log_tpt) * a.stride + deposit_h<H>((tile_id & a.tpt_mask) << 6, a.hpos);
+    tile_load<H, NT>(a, base, tile);
+    __syncthreads();
+    run_stages<H>(a, tile);
     tile_store<H, NT>(a, base, tile);
 }
 
@@ -540,7 +554,7 @@ void launch_fused(double2* st, int n, uint64_t batch, const Plan& plan, const Ti
 #define QSIM_STAGED_CASE(HH) \
     case HH:                                                                                      \
         if (nt) hipLaunchKernelGGL((k_fused_staged<HH, true>), dim3((unsigned)blocks), dim3(256), 0, s, a); \
-        else hipLaunchKernelGGL((k_fused_staged<HH, false>), dim3((unsigned)blocks), dim3(256), 0, s, a);  \
+        else hipLaunchKernelGGL((k_fused_staged<HH, false>), dim3((unsigned)blocks), dim3(256), 0, s, a); \
         break;
             QSIM_TILE_CASE(0)
             QSIM_TILE_CASE(1)
