@@ -128,14 +128,18 @@ def run_single(args):
         per_launch_bytes = dom["alg_bytes"] / dom["launches"]
         avg_s = dom["ms"] / dom["launches"] / 1e3
         achieved = per_launch_bytes / avg_s / 1e9
-        traffic = None
-        if args.pmc_json and os.path.exists(args.pmc_json):
-            with open(args.pmc_json) as f:
+        traffic, traffic_src = None, None
+        pmc_path = args.pmc_json or os.path.join(ROOT, "profiles", f"pmc_{args.workload}_{n}q.json")
+        if os.path.exists(pmc_path):
+            with open(pmc_path) as f:
                 pmc = json.load(f)
-            traffic = pmc.get(dom["name"], {}).get("hbm_bytes_per_launch")
+            ent = pmc.get("kernels", pmc).get(dom["name"], {})
+            traffic = ent.get("hbm_bytes_per_launch")
+            traffic_src = os.path.relpath(pmc_path, ROOT) if traffic is not None else None
         roof = {"bound": "hbm", "kernel": dom["name"], "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
-                "traffic": traffic, "alg_bytes_per_launch": per_launch_bytes,
+                "traffic": traffic, "traffic_source": traffic_src,
+                "alg_bytes_per_launch": per_launch_bytes,
                 "avg_launch_ms": round(dom["ms"] / dom["launches"], 4),
                 "launches": dom["launches"]}
     eff = alg_bytes_of_circuit(circuit, n) * args.steps / wall / 1e9

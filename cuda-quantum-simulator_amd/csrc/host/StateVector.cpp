@@ -52,6 +52,17 @@ StateVector& StateVector::operator=(StateVector&& o) noexcept {
     return *this;
 }
 
+void StateVector::applyMatrix1Q(int target, const std::complex<double> (&m)[4],
+                                const std::vector<int>& controls) {
+    double mm[8];
+    for (int i = 0; i < 4; ++i) {
+        mm[2 * i] = m[i].real();
+        mm[2 * i + 1] = m[i].imag();
+    }
+    check(qsim_apply_matrix1q(h_, target, mm, controls.empty() ? nullptr : controls.data(),
+                              (int)controls.size()));
+}
+
 void StateVector::initializeZero() { check(qsim_state_init_zero(h_)); }
 
 void StateVector::initializeBasis(size_t basis_idx) {

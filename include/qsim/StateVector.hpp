@@ -40,6 +40,11 @@ public:
     Amplitude* devicePtr();
     const Amplitude* devicePtr() const;
 
+    // General controlled 2x2 unitary [[m0, m1], [m2, m3]] on `target` (src/OptimizedGates.cu:165-183
+    // applyGate1Q_coalesced, plus controls); std::out_of_range / std::invalid_argument on bad qubits.
+    void applyMatrix1Q(int target, const std::complex<double> (&m)[4],
+                       const std::vector<int>& controls = {});
+
     std::vector<std::complex<double>> toHost() const;
     void fromHost(const std::vector<std::complex<double>>& amplitudes);
     std::vector<double> getProbabilities() const;
