@@ -152,6 +152,7 @@ struct qsim_state {
     double* d_partials = nullptr;
     double* d_result = nullptr;
     DevBuf ops, stages;  // fused-plan descriptors, re-uploaded only when the plan changes
+    PlanCache plans;
     Timer timer;
     ~qsim_state() {
         if (stream) (void)hipStreamSynchronize(stream);
@@ -179,7 +180,7 @@ static void check_state(const qsim_state* s) {
 }
 
 static void run_fused(qsim_state* s, const std::vector<Op>& ops) {
-    Plan plan = plan_fused(ops, s->n);
+    const Plan& plan = s->plans.get(ops, s->n);
     s->ops.upload(plan.ops.data(), plan.ops.size() * sizeof(TileOp), s->stream);
     s->stages.upload(plan.stages.data(), plan.stages.size() * sizeof(Stage), s->stream);
     launch_fused(s->d, s->n, 1, plan, (const TileOp*)s->ops.ptr, (const Stage*)s->stages.ptr,

@@ -205,6 +205,8 @@ struct qsim_dist {
     ncclComm_t comm = nullptr;
     std::vector<int> perm;
     DevBuf ops, stages;
+    std::vector<PlanCache> fplans;  // one per local segment of a run, in execution order
+    size_t plan_calls = 0;
     Timer timer;
     ~qsim_dist() {
         (void)hipSetDevice(device);
@@ -359,7 +361,8 @@ double allreduce_sum(qsim_dist* d, double local) {
 }
 void run_local(qsim_dist* d, Shard& sh, const std::vector<Op>& ops, int flags) {
     if (flags & QSIM_RUN_FUSED) {
-        Plan plan = plan_fused(ops, d->L);
+        if (d->plan_calls >= d->fplans.size()) d->fplans.resize(d->plan_calls + 1);
+        const Plan& plan = d->fplans[d->plan_calls++].get(ops, d->L);
         d->ops.upload(plan.ops.data(), plan.ops.size() * sizeof(TileOp), d->stream);
         d->stages.upload(plan.stages.data(), plan.stages.size() * sizeof(Stage), d->stream);
         launch_fused(sh.d, d->L, 1, plan, (const TileOp*)d->ops.ptr, (const Stage*)d->stages.ptr,
@@ -452,6 +455,7 @@ int qsim_dist_run(qsim_dist* d, const qsim_gate* gates, size_t count, int flags)
         need(d);
         if (!gates && count) fail(QSIM_ERR_INVALID_ARGUMENT, "null gate list");
         QSIM_HIPCHK(hipSetDevice(d->device));
+        d->plan_calls = 0;
         // Plan per shard (ranks differ only in which global controls/phases apply).
         std::vector<std::vector<DStep>> plans;
         std::vector<int> perm_after;

@@ -87,8 +87,9 @@ void launch_op(double2* st, int n, uint64_t batch, const Op& op, hipStream_t s, 
 // Fused tile passes (fused.hip).
 struct FusedPass {
     int single = -1;       // >= 0: not a tile pass but one per-gate op, Plan::singles[single]
-    int h = 0;             // number of high tile qubits (tile = 64 << h amplitudes)
-    int hpos[8] = {0};     // ascending physical qubit positions of the high tile bits (>= 6)
+    int h = 0;             // tile = 64 << h amplitudes (tile bits 0 .. 5 + h)
+    int r0 = 6;            // tile bits 0 .. r0-1 are qubits 0 .. r0-1 (2^r0-amplitude HBM runs)
+    int hpos[8] = {0};     // ascending physical qubits of tile bits r0 .. 5 + h (all >= r0)
     int op_begin = 0, op_end = 0;  // range in the pass-op buffer (unstaged kernel)
     int stage_begin = 0, stage_end = 0;  // range in Plan::stages (staged kernel, h >= 4)
     int hu_count = 0;      // unnormalized H butterflies in the pass: store scales by 2^(-k/2)
@@ -105,10 +106,15 @@ struct TileOp {            // an Op re-expressed in tile-index bits
 };
 // A stage of a staged tile pass: every thread holds the 2^rb amplitudes spanned by `fix` (the
 // stage's tile bits) in registers; ops in [op_begin, op_end) act on them with no LDS traffic.
+// Register r of a stage holds tile element jb | offs(r), offs(r) = r spread over fix[].  Both
+// address maps are XOR-linear in the element index, so their per-register parts are
+// precomputed here and the kernel combines them with the thread part by one OR / XOR.
 struct Stage {
-    uint32_t offs[16];     // tile-index offset of register r (spread of r over fix[])
+    uint64_t goff[16];     // HBM amplitude offset of offs(r) (its bits >= 6 spread over hpos)
+    uint32_t lds[16];      // LDS byte offset of offs(r) after the XOR swizzle (16 * sw(offs(r)))
     int fix[4];            // ascending stage tile bits
     int op_begin, op_end;
+    int _pad[2];
 };
 struct Plan {
     std::vector<FusedPass> passes;
@@ -120,8 +126,17 @@ struct Plan {
     size_t tile_passes = 0;
 };
 constexpr int kTileHMax = 6;  // 64 << 6 = 4096 amplitudes = 64 KiB of LDS per workgroup
+constexpr int kTileR0 = 6;    // contiguous run bits of a staged tile (QSIM_TILE_R0 in 4..6)
 // hmax < 0: the process default (kTileHMax, or QSIM_TILE_HMAX for tuning runs).
 Plan plan_fused(const std::vector<Op>& ops, int n, int hmax = -1);
+// The last plan of one engine object: re-running the same circuit (the benchmark loop, repeated
+// trajectories) skips the host planning.
+struct PlanCache {
+    int n = -1;
+    std::vector<Op> key;
+    Plan plan;
+    const Plan& get(const std::vector<Op>& ops, int n_qubits);
+};
 void launch_fused(double2* st, int n, uint64_t batch, const Plan& plan, const TileOp* d_ops,
                   const Stage* d_stages, hipStream_t s, Timer* tm);
 

@@ -79,25 +79,57 @@ static void plan_stages(std::vector<TileOp>& pass_ops, std::vector<int>& pass_sr
             else t.sub = S_GEN;              // (no controlled H in the gate set; keep it exact)
         }
     }
-    std::vector<int> rem(ops.size());
-    for (size_t i = 0; i < rem.size(); ++i) rem[i] = (int)i;
-    while (!rem.empty()) {
-        uint32_t sbits = 0, blocked = 0;
+    // The first stage is applied in registers straight after the HBM load and the last one
+    // right before the HBM store, so both may only use high tile bits (>= 6) as register bits:
+    // the 64 lanes must keep the 64 consecutive amplitudes of tile bits 0..5 (1 KiB runs).
+    const uint32_t all_bits = (1u << tile_bits) - 1u, high_bits = all_bits & ~0x3fu;
+    struct Taken {
         std::vector<int> in, deferred;
-        for (int i : rem) {
-            const TileOp& t = ops[i];
-            const uint32_t need = t.kind == K_M1 ? (1u << t.b0) : 0u;
-            const uint32_t touch = t.cmask | (1u << t.b0);
-            if ((touch & blocked) == 0 && __builtin_popcount(sbits | need) <= rb) {
-                sbits |= need;
-                in.push_back(i);
+        uint32_t sbits = 0;
+    };
+    auto take = [&](const std::vector<int>& from, uint32_t allowed) {
+        Taken t;
+        uint32_t blocked = 0;
+        for (int i : from) {
+            const TileOp& o = ops[i];
+            const uint32_t need = o.kind == K_M1 ? (1u << o.b0) : 0u;
+            const uint32_t touch = o.cmask | (1u << o.b0);
+            if ((touch & blocked) == 0 && (need & ~allowed) == 0 &&
+                __builtin_popcount(t.sbits | need) <= rb) {
+                t.sbits |= need;
+                t.in.push_back(i);
             } else {
-                deferred.push_back(i);
+                t.deferred.push_back(i);
                 blocked |= touch;
             }
         }
-        // pad with the highest unused tile bits (threads then walk consecutive LDS slots)
-        for (int b = tile_bits - 1; b >= 0 && __builtin_popcount(sbits) < rb; --b) sbits |= 1u << b;
+        return t;
+    };
+    // pad with the highest unused allowed bits (threads then walk consecutive LDS slots)
+    auto pad = [&](uint32_t sbits, uint32_t allowed) {
+        for (int b = tile_bits - 1; b >= 0 && __builtin_popcount(sbits) < rb; --b)
+            if ((allowed >> b) & 1u) sbits |= 1u << b;
+        return sbits;
+    };
+    std::vector<int> rem(ops.size());
+    for (size_t i = 0; i < rem.size(); ++i) rem[i] = (int)i;
+    std::vector<std::pair<uint32_t, std::vector<int>>> seq;  // (register bits, ops) per stage
+    Taken first = take(rem, high_bits);
+    seq.push_back({pad(first.sbits, high_bits), first.in});
+    rem.swap(first.deferred);
+    while (!rem.empty()) {
+        Taken t = take(rem, all_bits);
+        seq.push_back({t.sbits, t.in});
+        rem.swap(t.deferred);
+    }
+    if (seq.size() > 1) {  // the last stage must be storable straight from registers
+        if ((seq.back().first & ~high_bits) == 0) seq.back().first = pad(seq.back().first, high_bits);
+        else seq.push_back({pad(0u, high_bits), {}});
+    }
+    for (size_t k = 1; k + 1 < seq.size(); ++k) seq[k].first = pad(seq[k].first, all_bits);
+    for (auto& sq : seq) {
+        const uint32_t sbits = sq.first;
+        const std::vector<int>& in = sq.second;
         Stage st{};
         int k = 0;
         int pos_of[32];
@@ -111,7 +143,11 @@ static void plan_stages(std::vector<TileOp>& pass_ops, std::vector<int>& pass_sr
             uint32_t o = 0;
             for (int i = 0; i < rb; ++i)
                 if ((r >> i) & 1) o |= 1u << st.fix[i];
-            st.offs[r] = o;
+            uint64_t g = 0;
+            for (int b = 0; b < tile_bits; ++b)
+                if ((o >> b) & 1u) g |= 1ull << (b < p.r0 ? b : p.hpos[b - p.r0]);
+            st.goff[r] = g;
+            st.lds[r] = 16u * (o ^ ((o >> 4) & 15u));  // == 16 * sw(o)
         }
         st.op_begin = (int)plan.ops.size();
         for (int i : in) {
@@ -126,18 +162,131 @@ static void plan_stages(std::vector<TileOp>& pass_ops, std::vector<int>& pass_sr
         }
         st.op_end = (int)plan.ops.size();
         plan.stages.push_back(st);
-        rem.swap(deferred);
     }
     p.stage_end = (int)plan.stages.size();
 }
 
+// One planned step: a tile pass (chosen qubits `hi` above the run, ops in execution order) or a
+// per-gate step for a gate wider than the tile.
+struct PassChoice {
+    bool single = false;
+    uint64_t hi = 0;
+    std::vector<Op> ops;
+};
+
+// Split `ops` into passes.  Both strategies keep the exact-reordering rule (a gate may move
+// ahead only of gates on disjoint qubits).
+//   greedy: first fit in program order — a gate joins when its qubits still fit the tile.
+//   lookahead: grow the tile's qubit set one qubit (or, when no single qubit helps, one pair) at
+//     a time, each time taking the choice that lets the most upcoming gates into the pass.
+static std::vector<PassChoice> choose_passes(const std::vector<Op>& ops, int n, int r0, int nfree,
+                                             bool lookahead) {
+    const uint64_t low = (1ull << r0) - 1ull;
+    std::vector<PassChoice> out;
+    std::vector<Op> rem = ops;
+    std::vector<uint64_t> qm;
+    const size_t window = 512;  // gates scored per candidate (later ones are almost always blocked)
+    auto score = [&](uint64_t allowed) {
+        uint64_t blocked = 0;
+        int c = 0;
+        const size_t m = std::min(qm.size(), window);
+        for (size_t i = 0; i < m; ++i) {
+            if ((qm[i] & blocked) == 0 && (qm[i] & ~allowed) == 0) ++c;
+            else blocked |= qm[i];
+        }
+        return c;
+    };
+    while (!rem.empty()) {
+        // The first remaining gate is never blocked; if it needs more qubits than the tile's free
+        // slots it runs as a per-gate step (keeps program order, guarantees progress).
+        if (__builtin_popcountll(op_qubits(rem.front()) & ~low) > nfree) {
+            PassChoice c;
+            c.single = true;
+            c.ops.push_back(rem.front());
+            out.push_back(std::move(c));
+            rem.erase(rem.begin());
+            continue;
+        }
+        uint64_t hi = 0;
+        if (lookahead) {
+            qm.resize(rem.size());
+            for (size_t i = 0; i < rem.size(); ++i) qm[i] = op_qubits(rem[i]);
+            while (__builtin_popcountll(hi) < nfree) {
+                const int base = score(low | hi);
+                int best = base, bq = -1;
+                for (int q = r0; q < n; ++q) {
+                    if ((hi >> q) & 1ull) continue;
+                    const int c = score(low | hi | (1ull << q));
+                    if (c > best) best = c, bq = q;
+                }
+                if (bq >= 0) {
+                    hi |= 1ull << bq;
+                    continue;
+                }
+                if (__builtin_popcountll(hi) + 2 > nfree) break;
+                int pa = -1, pb = -1;
+                for (int qa = r0; qa < n; ++qa) {
+                    if ((hi >> qa) & 1ull) continue;
+                    for (int qb = qa + 1; qb < n; ++qb) {
+                        if ((hi >> qb) & 1ull) continue;
+                        const int c = score(low | hi | (1ull << qa) | (1ull << qb));
+                        if (c > best) best = c, pa = qa, pb = qb;
+                    }
+                }
+                if (pa < 0) break;
+                hi |= (1ull << pa) | (1ull << pb);
+            }
+            if (score(low | hi) == 0) hi = op_qubits(rem.front()) & ~low;  // (3-qubit first gate)
+        }
+        PassChoice c;
+        uint64_t blocked = 0;
+        std::vector<Op> deferred;
+        for (const Op& op : rem) {
+            const uint64_t q = op_qubits(op), qh = q & ~low;
+            const bool fits = lookahead ? (qh & ~hi) == 0 : __builtin_popcountll(hi | qh) <= nfree;
+            if ((q & blocked) == 0 && fits) {
+                if (!lookahead) hi |= qh;
+                c.ops.push_back(op);
+            } else {
+                deferred.push_back(op);
+                blocked |= q;
+            }
+        }
+        c.hi = hi;
+        out.push_back(std::move(c));
+        rem.swap(deferred);
+    }
+    return out;
+}
+
+static bool same_op(const Op& a, const Op& b) {
+    if (a.kind != b.kind || a.sub != b.sub || a.t0 != b.t0 || a.t1 != b.t1 || a.cmask != b.cmask ||
+        a.d0_one != b.d0_one || a.src != b.src)
+        return false;
+    for (int i = 0; i < 8; ++i)
+        if (a.m[i] != b.m[i]) return false;
+    return true;
+}
+
+const Plan& PlanCache::get(const std::vector<Op>& ops, int n_qubits) {
+    bool hit = n == n_qubits && key.size() == ops.size();
+    for (size_t i = 0; hit && i < ops.size(); ++i) hit = same_op(key[i], ops[i]);
+    if (!hit) {
+        plan = plan_fused(ops, n_qubits);
+        key = ops;
+        n = n_qubits;
+    }
+    return plan;
+}
+
+static int env_int(const char* k, int d) {
+    const char* e = std::getenv(k);
+    return e ? std::atoi(e) : d;
+}
+
 Plan plan_fused(const std::vector<Op>& ops, int n, int hmax) {
     if (hmax < 0) {
-        static const int def = [] {
-            const char* e = std::getenv("QSIM_TILE_HMAX");
-            const int v = e ? std::atoi(e) : kTileHMax;
-            return std::min(kTileHMax, std::max(0, v));
-        }();
+        static const int def = std::min(kTileHMax, std::max(0, env_int("QSIM_TILE_HMAX", kTileHMax)));
         hmax = def;
     }
     Plan plan;
@@ -152,45 +301,51 @@ Plan plan_fused(const std::vector<Op>& ops, int n, int hmax) {
         return plan;
     }
     const int heff = std::min(hmax, n - 6);
-    const uint64_t low = 0x3full;
-    std::vector<Op> remaining = ops;
-    while (!remaining.empty()) {
-        // The first remaining gate is never blocked; if it needs more high qubits than a tile
-        // holds it runs as a per-gate step (keeps program order, guarantees progress).
-        if (__builtin_popcountll(op_qubits(remaining.front()) & ~low) > heff) {
-            add_single(remaining.front());
-            remaining.erase(remaining.begin());
-            continue;
-        }
-        uint64_t hi = 0, blocked = 0;
-        std::vector<Op> in_pass, deferred;
-        for (const Op& op : remaining) {
-            const uint64_t q = op_qubits(op);
-            const uint64_t qh = q & ~low;
-            if ((q & blocked) == 0 && __builtin_popcountll(hi | qh) <= heff) {
-                hi |= qh;
-                in_pass.push_back(op);
-            } else {
-                deferred.push_back(op);
-                blocked |= q;
+    // Staged tiles (12 bits at h = 6) may shorten the contiguous HBM run to 2^r0 amplitudes
+    // (r0 = 4: 256 B runs, four per wave instruction) to free 12 - r0 tile slots for the planner.
+    // Every (r0, strategy) candidate is planned and the one with the fewest HBM passes wins
+    // (ties: the longer run).  QSIM_TILE_R0 / QSIM_PLANNER (0 greedy, 1 lookahead) pin one.
+    // The small unstaged tiles keep r0 = 6 and the greedy split.
+    static const int r0_pin = env_int("QSIM_TILE_R0", 0);
+    static const int strat_pin = env_int("QSIM_PLANNER", -1);
+    std::vector<PassChoice> best;
+    int best_r0 = 6;
+    for (int r0 = 6; r0 >= (heff >= 4 ? 4 : 6); --r0) {
+        if (r0_pin && heff >= 4 && r0 != std::min(6, std::max(4, r0_pin))) continue;
+        for (int la = 0; la <= (heff >= 4 ? 1 : 0); ++la) {
+            if (strat_pin >= 0 && heff >= 4 && la != (strat_pin ? 1 : 0)) continue;
+            std::vector<PassChoice> c = choose_passes(ops, n, r0, 6 + heff - r0, la != 0);
+            if (best.empty() || c.size() < best.size()) {
+                best.swap(c);
+                best_r0 = r0;
             }
         }
-        // Pad the tile to h = heff high qubits (uniform tile size / occupancy).
-        for (int q = 6; q < n && __builtin_popcountll(hi) < heff; ++q) hi |= 1ull << q;
+    }
+    const int r0 = best_r0;
+    const int nfree = 6 + heff - r0;
+    for (PassChoice& ch : best) {
+        if (ch.single) {
+            add_single(ch.ops.front());
+            continue;
+        }
+        uint64_t hi = ch.hi;
+        // Pad the tile to nfree chosen qubits (uniform tile size / occupancy).
+        for (int q = r0; q < n && __builtin_popcountll(hi) < nfree; ++q) hi |= 1ull << q;
         FusedPass p;
         p.h = heff;
+        p.r0 = r0;
         int k = 0;
         int bit_of[64];
-        for (int q = 0; q < 6; ++q) bit_of[q] = q;
-        for (int q = 6; q < n; ++q)
+        for (int q = 0; q < r0; ++q) bit_of[q] = q;
+        for (int q = r0; q < n; ++q)
             if ((hi >> q) & 1ull) {
                 p.hpos[k] = q;
-                bit_of[q] = 6 + k;
+                bit_of[q] = r0 + k;
                 ++k;
             }
         std::vector<TileOp> tops;
         std::vector<int> tsrc;
-        for (const Op& op : in_pass) {
+        for (const Op& op : ch.ops) {
             uint32_t cm = 0;
             for (int q = 0; q < n; ++q)
                 if ((op.cmask >> q) & 1ull) cm |= 1u << bit_of[q];
@@ -209,10 +364,9 @@ Plan plan_fused(const std::vector<Op>& ops, int n, int hmax) {
             }
             p.op_end = (int)plan.ops.size();
         }
-        plan.fused_gate_count += in_pass.size();
+        plan.fused_gate_count += ch.ops.size();
         plan.tile_passes += 1;
         plan.passes.push_back(p);
-        remaining.swap(deferred);
     }
     return plan;
 }
@@ -230,8 +384,28 @@ struct FArgs {
     int op_begin, op_end;
     int stage_begin, stage_end;
     int hpos[8];
+    int r0;              // run bits (tile bits 0..r0-1 = qubits 0..r0-1); hpos covers the rest
     double scale;        // applied at the store: (1/sqrt2)^(unnormalized H butterflies)
 };
+
+// Runtime-count forms for the staged kernel (count = tile bits above the run, <= 8).
+__device__ __forceinline__ uint64_t spread_n(uint32_t x, const int* hpos, int cnt) {
+    uint64_t r = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+        if (i < cnt) r |= (uint64_t)((x >> i) & 1u) << hpos[i];
+    return r;
+}
+__device__ __forceinline__ uint64_t deposit_n(uint64_t k, const int* hpos, int cnt) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        if (i < cnt) {
+            const uint64_t lo = k & ((1ull << hpos[i]) - 1ull);
+            k = ((k ^ lo) << 1) | lo;
+        }
+    }
+    return k;
+}
 
 template <int H>
 __device__ __forceinline__ uint64_t spread(uint32_t x, const int* hpos) {
@@ -474,41 +648,59 @@ __device__ __forceinline__ void stage_op(double2 (&v)[1 << RB], uint32_t jb, con
     }
 }
 
-// The register stages of one tile (tile already in LDS; ends with a barrier).
-template <int H>
-__device__ __forceinline__ void run_stages(const FArgs& a, double2* tile) {
-    constexpr int RB = H - 2;
-    constexpr int R = 1 << RB;
-    const int tid = threadIdx.x;
-    for (int s = a.stage_begin; s < a.stage_end; ++s) {
-        const Stage st = ldc(a.stages, s);
-        uint32_t offs[R];
+// Thread index spread over the tile bits that are not the stage's register bits.
+template <int RB>
+__device__ __forceinline__ uint32_t stage_jb(const Stage& st) {
+    uint32_t jb = threadIdx.x;
 #pragma unroll
-        for (int r = 0; r < R; ++r) offs[r] = st.offs[r];
-        uint32_t jb = (uint32_t)tid;  // thread index spread over the non-stage tile bits
-#pragma unroll
-        for (int i = 0; i < RB; ++i) jb = ins0(jb, st.fix[i]);
-        double2 v[R];
-#pragma unroll
-        for (int r = 0; r < R; ++r) v[r] = tile[sw(jb | offs[r])];
-        for (int o = st.op_begin; o < st.op_end; ++o) stage_op<RB>(v, jb, ldc(a.ops, o));
-#pragma unroll
-        for (int r = 0; r < R; ++r) tile[sw(jb | offs[r])] = v[r];
-        __syncthreads();
-    }
+    for (int i = 0; i < RB; ++i) jb = ins0(jb, st.fix[i]);
+    return jb;
 }
 
+// Staged pass.  Stage `stage_begin` runs in registers straight from the HBM loads and stage
+// `stage_end - 1` straight into the HBM stores (the planner gives both only high tile bits as
+// register bits, so a wave still moves 64 consecutive amplitudes = one 1 KiB run per
+// instruction); only the stages in between round-trip through LDS (read, ops, write, barrier).
+// A pass whose ops fit one such stage never touches LDS.
 template <int H, bool NT>
 __global__ __launch_bounds__(256, 2) void k_fused_staged(FArgs a) {  // 2 WGs/CU (LDS-bound)
     constexpr int T = 64 << H;
+    constexpr int RB = H - 2;
+    constexpr int R = 1 << RB;
     __shared__ double2 tile[T];
     const uint64_t tile_id = blockIdx.x;
+    const int r0 = a.r0, nh = 6 + H - r0;  // run bits, tile bits above the run
     const uint64_t base =
-        (tile_id >> a.log_tpt) * a.stride + deposit_h<H>((tile_id & a.tpt_mask) << 6, a.hpos);
-    tile_load<H, NT>(a, base, tile);
-    __syncthreads();
-    run_stages<H>(a, tile);
-    tile_store<H, NT>(a, base, tile);
+        (tile_id >> a.log_tpt) * a.stride + deposit_n((tile_id & a.tpt_mask) << r0, a.hpos, nh);
+    const uint32_t run_mask = (1u << r0) - 1u;
+    const int sb = a.stage_begin, se = a.stage_end;
+    double2 v[R];
+    char* const lds = reinterpret_cast<char*>(tile);
+    for (int s = sb; s < se; ++s) {  // one copy of the op interpreter; phase branches are uniform
+        const Stage sg = ldc(a.stages, s);
+        const uint32_t jb = stage_jb<RB>(sg);
+        const uint32_t lb = 16u * sw(jb);  // thread part of the LDS byte address
+        if (s == sb) {
+            const uint64_t gb = base | (jb & run_mask) | spread_n(jb >> r0, a.hpos, nh);
+#pragma unroll
+            for (int r = 0; r < R; ++r) v[r] = ld<NT>(a.st + (gb | sg.goff[r]));
+        } else {
+#pragma unroll
+            for (int r = 0; r < R; ++r) v[r] = *reinterpret_cast<const double2*>(lds + (lb ^ sg.lds[r]));
+        }
+        for (int o = sg.op_begin; o < sg.op_end; ++o) stage_op<RB>(v, jb, ldc(a.ops, o));
+        if (s == se - 1) {
+            const uint64_t gb = base | (jb & run_mask) | spread_n(jb >> r0, a.hpos, nh);
+            const double sc = a.scale;
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+                st<NT>(a.st + (gb | sg.goff[r]), make_double2(v[r].x * sc, v[r].y * sc));
+        } else {
+#pragma unroll
+            for (int r = 0; r < R; ++r) *reinterpret_cast<double2*>(lds + (lb ^ sg.lds[r])) = v[r];
+            __syncthreads();
+        }
+    }
 }
 
 // Staged passes use non-temporal HBM loads/stores (every amplitude is touched once per pass;
@@ -543,6 +735,7 @@ void launch_fused(double2* st, int n, uint64_t batch, const Plan& plan, const Ti
         // (1/sqrt2)^k: exact power of two for even k, one rounding for odd k
         a.scale = std::ldexp(1.0, -(p.hu_count / 2)) * ((p.hu_count & 1) ? kInvSqrt2 : 1.0);
         for (int i = 0; i < 8; ++i) a.hpos[i] = p.hpos[i];
+        a.r0 = p.r0;
         const int lt = n - 6 - p.h;
         a.log_tpt = lt;
         a.tpt_mask = (1ull << lt) - 1ull;
