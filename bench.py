@@ -41,6 +41,9 @@ def parse():
     p.add_argument("--depth", type=int, default=100)
     p.add_argument("--seed", type=int, default=42)
     p.add_argument("--mode", choices=["fused", "per-gate"], default="fused")
+    p.add_argument("--jit", type=int, choices=[0, 1, 2], default=2,
+                   help="circuit-specialised pass kernels: 0 interpreter only, 1 background "
+                        "compile, 2 compile during the first warmup run (default)")
     p.add_argument("--workload", choices=["hc", "ref", "1q"], default="hc",
                    help="hc: W-HC random H+CNOT; ref: reference benchmark_scaling circuit; "
                         "1q: 100 unfused H gates on targets i %% n")
@@ -106,8 +109,10 @@ def run_single(args):
     mode = q.RunMode.Fused if args.mode == "fused" else q.RunMode.PerGate
     if args.workload == "1q":
         mode = q.RunMode.PerGate
+    from qsim_amd.plan import set_jit
+    set_jit(args.jit, -1)
     sim = q.Simulator(n, mode=mode)
-    for _ in range(args.warmup):
+    for _ in range(max(1, args.warmup) if args.jit else args.warmup):
         sim.run(circuit)
     sim.synchronize()
     sim.state.profile(True)
@@ -150,6 +155,7 @@ def run_single(args):
         "scaling": "strong", "vs_baseline": None, "dtype": "c128 (complex<double>)",
         "data": "synthetic",
         "config": {"workload": wl, "qubits": n, "gates": gates, "mode": mode.name,
+                   "pass_kernels": "jit" if args.jit else "interpreter",
                    "state_bytes": 16 << n, "parallelism": "single GPU"},
         "roofline": roof,
         "effective_GBps": round(eff, 1),

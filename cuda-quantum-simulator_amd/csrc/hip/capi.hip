@@ -181,10 +181,11 @@ static void check_state(const qsim_state* s) {
 
 static void run_fused(qsim_state* s, const std::vector<Op>& ops) {
     const Plan& plan = s->plans.get(ops, s->n);
+    const JitModule* jm = jit_for(s->plans.jit, plan, s->n);
     s->ops.upload(plan.ops.data(), plan.ops.size() * sizeof(TileOp), s->stream);
     s->stages.upload(plan.stages.data(), plan.stages.size() * sizeof(Stage), s->stream);
     launch_fused(s->d, s->n, 1, plan, (const TileOp*)s->ops.ptr, (const Stage*)s->stages.ptr,
-                 s->stream, &s->timer);
+                 s->stream, &s->timer, jm);
 }
 
 extern "C" {
@@ -390,6 +391,48 @@ int qsim_plan_fused(int n_qubits, const qsim_gate* gates, size_t count, int hmax
             ++tile;
         }
         if (n_passes) *n_passes = tile;
+    });
+}
+
+int qsim_set_jit(int mode, int min_qubits) {
+    return guarded([&] {
+        if (mode > 2) fail(QSIM_ERR_INVALID_ARGUMENT, "jit mode must be 0 (off), 1 (background) or 2 (inline)");
+        jit_configure(mode, min_qubits);
+    });
+}
+
+int qsim_jit_source(int n_qubits, const qsim_gate* gates, size_t count, char* buf, size_t cap,
+                    size_t* len) {
+    return guarded([&] {
+        QSIM_REQUIRE(gates || count == 0, QSIM_ERR_INVALID_ARGUMENT, "null gate list");
+        if (n_qubits < QSIM_MIN_QUBITS || n_qubits > 40) fail(QSIM_ERR_INVALID_ARGUMENT, "bad qubit count");
+        std::vector<Op> ops;
+        for (size_t i = 0; i < count; ++i) {
+            ops.push_back(lower_gate(gates[i], n_qubits));
+            ops.back().src = (int)i;
+        }
+        const std::string src = jit_source(plan_fused(ops, n_qubits));
+        if (len) *len = src.size();
+        if (buf && cap) {
+            const size_t m = std::min(cap - 1, src.size());
+            std::memcpy(buf, src.data(), m);
+            buf[m] = 0;
+        }
+    });
+}
+
+int qsim_jit_build(int n_qubits, const qsim_gate* gates, size_t count, size_t* code_bytes) {
+    return guarded([&] {
+        size_t len = 0;
+        const int rc = qsim_jit_source(n_qubits, gates, count, nullptr, 0, &len);
+        if (rc != QSIM_OK) fail(rc, qsim_last_error());
+        std::string src(len + 1, '\0');
+        qsim_jit_source(n_qubits, gates, count, &src[0], len + 1, &len);
+        src.resize(len);
+        std::vector<char> code;
+        std::string log;
+        if (!src.empty() && !jit_compile(src, code, log)) fail(QSIM_ERR_RUNTIME, "hipRTC: " + log);
+        if (code_bytes) *code_bytes = code.size();
     });
 }
 

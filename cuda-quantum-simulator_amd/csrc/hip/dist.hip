@@ -362,11 +362,13 @@ double allreduce_sum(qsim_dist* d, double local) {
 void run_local(qsim_dist* d, Shard& sh, const std::vector<Op>& ops, int flags) {
     if (flags & QSIM_RUN_FUSED) {
         if (d->plan_calls >= d->fplans.size()) d->fplans.resize(d->plan_calls + 1);
-        const Plan& plan = d->fplans[d->plan_calls++].get(ops, d->L);
+        PlanCache& pc = d->fplans[d->plan_calls++];
+        const Plan& plan = pc.get(ops, d->L);
+        const JitModule* jm = jit_for(pc.jit, plan, d->L);
         d->ops.upload(plan.ops.data(), plan.ops.size() * sizeof(TileOp), d->stream);
         d->stages.upload(plan.stages.data(), plan.stages.size() * sizeof(Stage), d->stream);
         launch_fused(sh.d, d->L, 1, plan, (const TileOp*)d->ops.ptr, (const Stage*)d->stages.ptr,
-                     d->stream, &d->timer);
+                     d->stream, &d->timer, jm);
     } else {
         for (const Op& op : ops) launch_op(sh.d, d->L, 1, op, d->stream, &d->timer);
     }

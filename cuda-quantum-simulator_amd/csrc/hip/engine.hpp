@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <memory>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -129,16 +130,37 @@ constexpr int kTileHMax = 6;  // 64 << 6 = 4096 amplitudes = 64 KiB of LDS per w
 constexpr int kTileR0 = 6;    // contiguous run bits of a staged tile (QSIM_TILE_R0 in 4..6)
 // hmax < 0: the process default (kTileHMax, or QSIM_TILE_HMAX for tuning runs).
 Plan plan_fused(const std::vector<Op>& ops, int n, int hmax = -1);
+// Circuit-specialised pass kernels (jit.hip): hipRTC code object of one plan on one device.
+struct JitJob;
+struct JitModule {
+    hipModule_t mod = nullptr;
+    std::vector<hipFunction_t> fn;  // per plan pass; null = run by the interpreter
+    ~JitModule();
+};
+struct JitState {
+    std::shared_ptr<JitJob> job;
+    std::unique_ptr<JitModule> mod;
+    bool failed = false;
+};
+int jit_mode();        // 0 off, 1 background compile (default), 2 compile on first use
+int jit_min_qubits();  // smaller states never JIT (QSIM_JIT_MIN_QUBITS, default 20)
+void jit_configure(int mode, int min_qubits);  // < 0 leaves a setting unchanged
+std::string jit_source(const Plan& plan);      // empty when the plan has no staged pass
+bool jit_compile(const std::string& src, std::vector<char>& code, std::string& log);
+// The loaded module for `plan`, or null while it compiles / when JIT does not apply.
+const JitModule* jit_for(JitState& js, const Plan& plan, int n);
+
 // The last plan of one engine object: re-running the same circuit (the benchmark loop, repeated
-// trajectories) skips the host planning.
+// trajectories) skips the host planning and, once compiled, runs the specialised kernels.
 struct PlanCache {
     int n = -1;
     std::vector<Op> key;
     Plan plan;
+    JitState jit;
     const Plan& get(const std::vector<Op>& ops, int n_qubits);
 };
 void launch_fused(double2* st, int n, uint64_t batch, const Plan& plan, const TileOp* d_ops,
-                  const Stage* d_stages, hipStream_t s, Timer* tm);
+                  const Stage* d_stages, hipStream_t s, Timer* tm, const JitModule* jm = nullptr);
 
 // Reductions / readout helpers (reduce.hip)
 void launch_init_basis(double2* st, int n, uint64_t batch, uint64_t basis, hipStream_t s);

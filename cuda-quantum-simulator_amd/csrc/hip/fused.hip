@@ -275,6 +275,7 @@ const Plan& PlanCache::get(const std::vector<Op>& ops, int n_qubits) {
         plan = plan_fused(ops, n_qubits);
         key = ops;
         n = n_qubits;
+        jit = JitState{};  // a new plan needs its own code object
     }
     return plan;
 }
@@ -715,7 +716,7 @@ static bool fused_nt() {
 }
 
 void launch_fused(double2* st, int n, uint64_t batch, const Plan& plan, const TileOp* d_ops,
-                  const Stage* d_stages, hipStream_t s, Timer* tm) {
+                  const Stage* d_stages, hipStream_t s, Timer* tm, const JitModule* jm) {
     const double pass_bytes = 32.0 * (double)(1ull << n) * (double)batch;
     const bool nt = fused_nt();
     for (const FusedPass& p : plan.passes) {
@@ -741,6 +742,15 @@ void launch_fused(double2* st, int n, uint64_t batch, const Plan& plan, const Ti
         a.tpt_mask = (1ull << lt) - 1ull;
         const uint64_t blocks = batch << lt;
         TimedLaunch tl(tm, "fused_tile", pass_bytes, s);
+        const size_t pi = (size_t)(&p - plan.passes.data());
+        if (jm && pi < jm->fn.size() && jm->fn[pi]) {  // circuit-specialised kernel (jit.hip)
+            unsigned long long stride = a.stride, tpt = a.tpt_mask;
+            int lt_arg = lt;
+            void* args[] = {&a.st, &stride, &tpt, &lt_arg};
+            QSIM_HIPCHK(hipModuleLaunchKernel(jm->fn[pi], (unsigned)blocks, 1, 1, 256, 1, 1, 0, s,
+                                              args, nullptr));
+            continue;
+        }
         switch (p.h) {
 #define QSIM_TILE_CASE(HH) \
     case HH: hipLaunchKernelGGL(k_fused_tile<HH>, dim3((unsigned)blocks), dim3(256), 0, s, a); break;

@@ -1,0 +1,417 @@
+// jit.hip — circuit-specialised fused-pass kernels (hipRTC), the second execution tier.
+//
+// The staged pass interpreter (fused.hip, k_fused_staged) dispatches every op at run time: a
+// scalar descriptor load, a branch tree on (kind, sub, register bit) and, because the branch arms
+// produce their register arrays in different VGPRs, v_mov copies of the live amplitudes at every
+// merge.  For deep passes that VALU overhead, not HBM, bounds the pass.
+//
+// Here the same Plan is printed as straight-line HIP: one kernel per staged pass, every op
+// expanded over its 2^rb register pairs with the target bit, register-bit controls and matrix
+// entries as literals (hex-float, exact), uncontrolled X gates as pure register renames, and the
+// load / LDS / store addressing of each stage as constants.  The source is compiled by hipRTC for
+// gfx950 on a background thread the first time a plan is seen; until the code object is ready
+// the interpreter runs the plan (so a one-shot circuit never waits for the compiler), and from
+// then on the state's runs of that plan launch the specialised kernels.  Semantics are those of
+// the interpreter op for op (same unnormalised-H scale, same closed forms as device_ops.hpp).
+#include <hip/hip_runtime.h>
+#include <hip/hiprtc.h>
+
+#include <atomic>
+#include <condition_variable>
+#include <cstdio>
+#include <cstdlib>
+#include <deque>
+#include <memory>
+#include <mutex>
+#include <sstream>
+#include <thread>
+
+#include "engine.hpp"
+
+namespace qsim_hip {
+
+// ---------------------------------------------------------------------------------------
+// Policy
+// ---------------------------------------------------------------------------------------
+static std::atomic<int> g_jit_mode{-1};        // 0 off, 1 background compile, 2 compile inline
+static std::atomic<int> g_jit_min_qubits{-1};  // smaller states always use the interpreter
+
+static int env_or(const char* k, int d) {
+    const char* e = std::getenv(k);
+    return e ? std::atoi(e) : d;
+}
+int jit_mode() {
+    int m = g_jit_mode.load();
+    if (m < 0) {
+        m = env_or("QSIM_JIT", 1);
+        g_jit_mode.store(m);
+    }
+    return m;
+}
+int jit_min_qubits() {
+    int m = g_jit_min_qubits.load();
+    if (m < 0) {
+        m = env_or("QSIM_JIT_MIN_QUBITS", 20);
+        g_jit_min_qubits.store(m);
+    }
+    return m;
+}
+void jit_configure(int mode, int min_qubits) {
+    if (mode >= 0) g_jit_mode.store(mode);
+    if (min_qubits >= 0) g_jit_min_qubits.store(min_qubits);
+}
+
+// ---------------------------------------------------------------------------------------
+// Source generation
+// ---------------------------------------------------------------------------------------
+namespace {
+
+std::string lit(double x) {  // exact double literal
+    char b[64];
+    std::snprintf(b, sizeof b, "%a", x);
+    return b;
+}
+std::string hexu(uint64_t x) {
+    char b[32];
+    std::snprintf(b, sizeof b, "0x%llxull", (unsigned long long)x);
+    return b;
+}
+
+const char* kPrelude = R"(
+typedef double qdv2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ double2 qld(const double2* p) {
+  const qdv2 t = __builtin_nontemporal_load(reinterpret_cast<const qdv2*>(p));
+  return make_double2(t.x, t.y);
+}
+__device__ __forceinline__ void qst(double2* p, double2 v) {
+  qdv2 t; t.x = v.x; t.y = v.y;
+  __builtin_nontemporal_store(t, reinterpret_cast<qdv2*>(p));
+}
+__device__ __forceinline__ double2 qsel(bool c, double2 a, double2 b) {
+  return make_double2(c ? a.x : b.x, c ? a.y : b.y);
+}
+__device__ __forceinline__ double2 qcm(double mr, double mi, double2 a) {
+  return make_double2(mr * a.x - mi * a.y, mr * a.y + mi * a.x);
+}
+__device__ __forceinline__ unsigned qins0(unsigned p, int b) {
+  const unsigned lo = p & ((1u << b) - 1u);
+  return ((p ^ lo) << 1) | lo;
+}
+)";
+
+struct Gen {
+    std::ostringstream o;
+    int R = 16, RB = 4;
+    int nm[16];  // logical register r lives in variable v<nm[r]>
+    int tmp = 0;
+
+    std::string v(int r) const { return "v" + std::to_string(nm[r]); }
+
+    // |1>-side phase of a diagonal op (diag1 in device_ops.hpp)
+    std::string diag1(const TileOp& t, const std::string& a) {
+        const double c = kInvSqrt2;
+        switch (t.sub) {
+            case S_NEG: return "make_double2(-" + a + ".x, -" + a + ".y)";
+            case S_I: return "make_double2(-" + a + ".y, " + a + ".x)";
+            case S_MI: return "make_double2(" + a + ".y, -" + a + ".x)";
+            case S_T:
+                return "make_double2((" + a + ".x - " + a + ".y) * " + lit(c) + ", (" + a + ".x + " + a +
+                       ".y) * " + lit(c) + ")";
+            case S_TDG:
+                return "make_double2((" + a + ".x + " + a + ".y) * " + lit(c) + ", (-" + a + ".x + " + a +
+                       ".y) * " + lit(c) + ")";
+            default: return "qcm(" + lit(t.m[2]) + ", " + lit(t.m[3]) + ", " + a + ")";
+        }
+    }
+    std::string diag0(const TileOp& t, const std::string& a) {
+        return "qcm(" + lit(t.m[0]) + ", " + lit(t.m[1]) + ", " + a + ")";
+    }
+
+    void op(const TileOp& t) {
+        const uint32_t cr = t.cm_reg;
+        std::string pred;  // per-thread control predicate (thread-bit controls)
+        if (t.cm_thr) {
+            pred = "c" + std::to_string(tmp++);
+            o << "  const bool " << pred << " = (jb & " << t.cm_thr << "u) == " << t.cm_thr << "u;\n";
+        }
+        if (t.kind == K_DIAG) {
+            std::string tb;
+            if (t.p0 < 0) {
+                tb = "b" + std::to_string(tmp++);
+                o << "  const bool " << tb << " = ((jb >> " << t.b0 << ") & 1u) != 0u;\n";
+            }
+            for (int r = 0; r < R; ++r) {
+                if ((r & cr) != cr) continue;
+                const std::string a = v(r);
+                std::string nv;
+                if (t.p0 >= 0) {
+                    const bool bit = (r >> t.p0) & 1;
+                    if (!bit && t.d0_one) continue;
+                    nv = bit ? diag1(t, a) : diag0(t, a);
+                } else {
+                    nv = "qsel(" + tb + ", " + diag1(t, a) + ", " + (t.d0_one ? a : diag0(t, a)) + ")";
+                }
+                if (!pred.empty()) nv = "qsel(" + pred + ", " + nv + ", " + a + ")";
+                o << "  " << a << " = " << nv << ";\n";
+            }
+            return;
+        }
+        // K_M1 on register bit P (SWAPs were lowered to controlled X by the planner)
+        const int P = t.p0;
+        for (int r = 0; r < R; ++r) {
+            if ((r >> P) & 1) continue;
+            if ((r & cr) != cr) continue;  // register-bit controls: decided here, not on the GPU
+            const int r1 = r | (1 << P);
+            if (t.sub == S_X && pred.empty()) {  // a relabel: no instruction at all
+                std::swap(nm[r], nm[r1]);
+                continue;
+            }
+            const std::string a0 = v(r), a1 = v(r1);
+            std::string x0, x1;
+            switch (t.sub) {
+                case S_X: x0 = "t1"; x1 = "t0"; break;
+                case S_Y:
+                    x0 = "make_double2(t1.y, -t1.x)";
+                    x1 = "make_double2(-t0.y, t0.x)";
+                    break;
+                case S_H:  // unnormalised butterfly; the pass scale restores (1/sqrt2)^k
+                    x0 = "make_double2(t0.x + t1.x, t0.y + t1.y)";
+                    x1 = "make_double2(t0.x - t1.x, t0.y - t1.y)";
+                    break;
+                default: break;  // S_GEN: below
+            }
+            if (t.sub == S_GEN) {  // double2 has no operator+ here: expand the sums
+                auto sum = [](const std::string& a, const std::string& b) {
+                    return "make_double2(" + a + ".x + " + b + ".x, " + a + ".y + " + b + ".y)";
+                };
+                auto cm = [&](int i, const char* a) {
+                    return "qcm(" + lit(t.m[2 * i]) + ", " + lit(t.m[2 * i + 1]) + ", " + a + ")";
+                };
+                o << "  { const double2 t0 = " << a0 << ", t1 = " << a1 << ";\n"
+                  << "    const double2 u0 = " << cm(0, "t0") << ", u1 = " << cm(1, "t1") << ";\n"
+                  << "    const double2 w0 = " << cm(2, "t0") << ", w1 = " << cm(3, "t1") << ";\n";
+                x0 = sum("u0", "u1");
+                x1 = sum("w0", "w1");
+            } else {
+                o << "  { const double2 t0 = " << a0 << ", t1 = " << a1 << ";\n";
+            }
+            if (!pred.empty()) {
+                x0 = "qsel(" + pred + ", " + x0 + ", t0)";
+                x1 = "qsel(" + pred + ", " + x1 + ", t1)";
+            }
+            o << "    " << a0 << " = " << x0 << ";\n    " << a1 << " = " << x1 << "; }\n";
+        }
+    }
+};
+
+// Thread index spread over the tile bits that are not register bits of stage `st`.
+std::string jb_expr(const Stage& st, int rb) {
+    std::string e = "tid";
+    for (int i = 0; i < rb; ++i) e = "qins0(" + e + ", " + std::to_string(st.fix[i]) + ")";
+    return e;
+}
+
+void gen_pass(std::ostringstream& out, const Plan& plan, const FusedPass& p, int idx) {
+    const int H = p.h, RB = H - 2, R = 1 << RB, T = 64 << H;
+    const int r0 = p.r0, nh = 6 + H - r0;
+    Gen g;
+    g.R = R;
+    g.RB = RB;
+    for (int r = 0; r < R; ++r) g.nm[r] = r;
+    std::ostringstream& o = g.o;
+    o << "extern \"C\" __global__ void __launch_bounds__(256, 2)\nqk" << idx
+      << "(double2* __restrict__ st, unsigned long long stride, unsigned long long tpt_mask, int log_tpt) {\n"
+      << "  __shared__ double2 tile[" << T << "];\n"
+      << "  char* const lds = reinterpret_cast<char*>(tile);\n"
+      << "  const unsigned tid = threadIdx.x;\n"
+      << "  const unsigned long long tile_id = blockIdx.x;\n"
+      << "  unsigned long long k = (tile_id & tpt_mask) << " << r0 << ";\n";
+    for (int i = 0; i < nh; ++i)
+        o << "  { const unsigned long long lo = k & " << hexu((1ull << p.hpos[i]) - 1ull)
+          << "; k = ((k ^ lo) << 1) | lo; }\n";
+    o << "  const unsigned long long base = (tile_id >> log_tpt) * stride + k;\n";
+    o << "  double2";
+    for (int r = 0; r < R; ++r) o << (r ? ", v" : " v") << r;
+    o << ";\n";
+    const int sb = p.stage_begin, se = p.stage_end;
+    for (int s = sb; s < se; ++s) {
+        const Stage& st = plan.stages[s];
+        o << "  {\n  const unsigned jb = " << jb_expr(st, RB) << ";\n";
+        auto gaddr = [&]() {
+            std::string e = "base | (unsigned long long)(jb & " + std::to_string((1u << r0) - 1u) + "u)";
+            for (int i = 0; i < nh; ++i)
+                e += " | ((unsigned long long)((jb >> " + std::to_string(r0 + i) + ") & 1u) << " +
+                     std::to_string(p.hpos[i]) + ")";
+            return e;
+        };
+        if (s == sb || s == se - 1) o << "  const unsigned long long gb = " << gaddr() << ";\n";
+        if (s != sb || s != se - 1) o << "  const unsigned lb = 16u * (jb ^ ((jb >> 4) & 15u));\n";
+        if (s == sb) {
+            for (int r = 0; r < R; ++r) o << "  " << g.v(r) << " = qld(st + (gb | " << hexu(st.goff[r]) << "));\n";
+        } else {
+            for (int r = 0; r < R; ++r)
+                o << "  " << g.v(r) << " = *reinterpret_cast<const double2*>(lds + (lb ^ " << st.lds[r] << "u));\n";
+        }
+        for (int i = st.op_begin; i < st.op_end; ++i) g.op(plan.ops[i]);
+        if (s == se - 1) {
+            const double sc = std::ldexp(1.0, -(p.hu_count / 2)) * ((p.hu_count & 1) ? kInvSqrt2 : 1.0);
+            for (int r = 0; r < R; ++r) {
+                std::string val = g.v(r);
+                if (sc != 1.0) val = "make_double2(" + val + ".x * " + lit(sc) + ", " + val + ".y * " + lit(sc) + ")";
+                o << "  qst(st + (gb | " << hexu(st.goff[r]) << "), " << val << ");\n";
+            }
+        } else {
+            for (int r = 0; r < R; ++r)
+                o << "  *reinterpret_cast<double2*>(lds + (lb ^ " << st.lds[r] << "u)) = " << g.v(r) << ";\n";
+            o << "  __syncthreads();\n";
+        }
+        o << "  }\n";
+    }
+    o << "}\n";
+    out << o.str();
+}
+
+}  // namespace
+
+bool jit_pass_eligible(const FusedPass& p) { return p.single < 0 && p.h >= 4; }
+
+std::string jit_source(const Plan& plan) {
+    std::ostringstream out;
+    bool any = false;
+    out << kPrelude;
+    for (size_t i = 0; i < plan.passes.size(); ++i) {
+        if (!jit_pass_eligible(plan.passes[i])) continue;
+        gen_pass(out, plan, plan.passes[i], (int)i);
+        any = true;
+    }
+    return any ? out.str() : std::string();
+}
+
+// ---------------------------------------------------------------------------------------
+// Compilation (hipRTC) on one background worker
+// ---------------------------------------------------------------------------------------
+struct JitJob {
+    std::string src;
+    std::vector<char> code;
+    std::string log;
+    std::atomic<int> state{0};  // 0 queued, 1 done ok, 2 failed
+};
+
+bool jit_compile(const std::string& src, std::vector<char>& code, std::string& log) {
+    hiprtcProgram prog;
+    if (hiprtcCreateProgram(&prog, src.c_str(), "qsim_pass.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS) {
+        log = "hiprtcCreateProgram failed";
+        return false;
+    }
+    const char* opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17"};
+    const hiprtcResult rc = hiprtcCompileProgram(prog, 3, opts);
+    size_t ls = 0;
+    hiprtcGetProgramLogSize(prog, &ls);
+    if (ls > 1) {
+        log.resize(ls);
+        hiprtcGetProgramLog(prog, &log[0]);
+    }
+    bool ok = rc == HIPRTC_SUCCESS;
+    if (ok) {
+        size_t cs = 0;
+        hiprtcGetCodeSize(prog, &cs);
+        code.resize(cs);
+        ok = cs > 0 && hiprtcGetCode(prog, code.data()) == HIPRTC_SUCCESS;
+    }
+    hiprtcDestroyProgram(&prog);
+    return ok;
+}
+
+namespace {
+class Worker {
+public:
+    static Worker& get() {
+        static Worker w;
+        return w;
+    }
+    void submit(std::shared_ptr<JitJob> j) {
+        {
+            std::lock_guard<std::mutex> l(mu_);
+            q_.push_back(std::move(j));
+            if (!th_.joinable()) th_ = std::thread([this] { loop(); });
+        }
+        cv_.notify_one();
+    }
+    ~Worker() {
+        {
+            std::lock_guard<std::mutex> l(mu_);
+            stop_ = true;
+            q_.clear();
+        }
+        cv_.notify_all();
+        if (th_.joinable()) th_.join();
+    }
+
+private:
+    void loop() {
+        for (;;) {
+            std::shared_ptr<JitJob> j;
+            {
+                std::unique_lock<std::mutex> l(mu_);
+                cv_.wait(l, [&] { return stop_ || !q_.empty(); });
+                if (stop_) return;
+                j = q_.front();
+                q_.pop_front();
+            }
+            const bool ok = jit_compile(j->src, j->code, j->log);
+            j->state.store(ok ? 1 : 2);
+        }
+    }
+    std::mutex mu_;
+    std::condition_variable cv_;
+    std::deque<std::shared_ptr<JitJob>> q_;
+    std::thread th_;
+    bool stop_ = false;
+};
+}  // namespace
+
+JitModule::~JitModule() {
+    if (mod) (void)hipModuleUnload(mod);
+}
+
+const JitModule* jit_for(JitState& js, const Plan& plan, int n) {
+    const int mode = jit_mode();
+    if (mode == 0 || n < jit_min_qubits() || js.failed) return nullptr;
+    if (js.mod) return js.mod.get();
+    if (!js.job) {
+        std::string src = jit_source(plan);
+        if (src.empty()) {
+            js.failed = true;  // nothing to specialise (no staged pass)
+            return nullptr;
+        }
+        js.job = std::make_shared<JitJob>();
+        js.job->src = std::move(src);
+        if (mode == 2) {
+            const bool ok = jit_compile(js.job->src, js.job->code, js.job->log);
+            js.job->state.store(ok ? 1 : 2);
+        } else {
+            Worker::get().submit(js.job);
+        }
+    }
+    const int st = js.job->state.load();
+    if (st == 0) return nullptr;  // still compiling: the interpreter runs this time
+    if (st == 2) {
+        js.failed = true;
+        std::fprintf(stderr, "qsim: pass JIT failed, staying on the interpreter:\n%s\n", js.job->log.c_str());
+        js.job.reset();
+        return nullptr;
+    }
+    auto m = std::make_unique<JitModule>();
+    QSIM_HIPCHK(hipModuleLoadData(&m->mod, js.job->code.data()));
+    m->fn.assign(plan.passes.size(), nullptr);
+    for (size_t i = 0; i < plan.passes.size(); ++i) {
+        if (!jit_pass_eligible(plan.passes[i])) continue;
+        const std::string name = "qk" + std::to_string(i);
+        QSIM_HIPCHK(hipModuleGetFunction(&m->fn[i], m->mod, name.c_str()));
+    }
+    js.job.reset();
+    js.mod = std::move(m);
+    return js.mod.get();
+}
+
+}  // namespace qsim_hip

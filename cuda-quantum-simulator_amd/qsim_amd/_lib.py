@@ -83,6 +83,10 @@ _sig(hip, "qsim_apply_matrix1q", [_P, c_int, POINTER(c_double), POINTER(c_int), 
 _sig(hip, "qsim_apply_gate_raw", [_P, c_int, POINTER(qsim_gate), _P])
 _sig(hip, "qsim_plan_fused", [c_int, POINTER(qsim_gate), c_size_t, c_int, _P, _P,
                               POINTER(c_int32)])
+_sig(hip, "qsim_set_jit", [c_int, c_int])
+_sig(hip, "qsim_jit_source", [c_int, POINTER(qsim_gate), c_size_t, c_char_p, c_size_t,
+                              POINTER(c_size_t)])
+_sig(hip, "qsim_jit_build", [c_int, POINTER(qsim_gate), c_size_t, POINTER(c_size_t)])
 _sig(hip, "qsim_state_to_host", [_P, _P])
 _sig(hip, "qsim_state_from_host", [_P, _P])
 _sig(hip, "qsim_state_probabilities", [_P, _P])

@@ -35,7 +35,12 @@ def run(args, metric: str, peak_gbps: float) -> None:
     dist.broadcast_object_list(obj, src=0)
     sim = DistributedSimulator(n, rank, world, obj[0], device=local)
     fused = args.mode == "fused"
-    for _ in range(args.warmup):
+    jit = getattr(args, "jit", 2)
+    from .plan import set_jit
+    set_jit(jit, -1)
+    # the qubit map reaches its fixed point within two runs, so three warmups see (and, with the
+    # JIT on, compile) the plans every timed run uses
+    for _ in range(max(3, args.warmup) if jit else args.warmup):
         sim.run(circuit, fused=fused)
     sim.synchronize()
     sim.profile(True)
@@ -71,6 +76,7 @@ def run(args, metric: str, peak_gbps: float) -> None:
             "data": "synthetic",
             "config": {"workload": wl, "qubits": n, "gates": gates,
                        "mode": "Fused" if fused else "PerGate", "state_bytes": 16 << n,
+                       "pass_kernels": "jit" if jit else "interpreter",
                        "parallelism": f"state sharded by high qubits over {world} GPUs (RCCL all-to-all remaps)"},
             "roofline": roof, "kernels_rank0": stats, "cpu_baseline": None,
         }

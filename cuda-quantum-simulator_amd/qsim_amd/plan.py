@@ -21,3 +21,29 @@ def plan_fused(circuit: Circuit, hmax: int = 6):
                                         pass_of.ctypes.data_as(ctypes.c_void_p),
                                         ctypes.byref(npass)))
     return order[:cnt], pass_of[:cnt], npass.value
+
+
+def set_jit(mode: int = -1, min_qubits: int = -1) -> None:
+    """Circuit-specialised pass kernels: mode 0 off, 1 background compile (default), 2 compile
+    on a plan's first run; states below `min_qubits` use the pass interpreter (qsim_set_jit)."""
+    _lib.check(_lib.hip.qsim_set_jit(mode, min_qubits))
+
+
+def jit_source(circuit: Circuit) -> str:
+    """The HIP source the engine generates for this circuit's fused plan ('' if no staged pass)."""
+    arr, cnt = circuit.to_abi()
+    n = ctypes.c_size_t(0)
+    _lib.check(_lib.hip.qsim_jit_source(circuit.getNumQubits(), arr, cnt, None, 0, ctypes.byref(n)))
+    buf = ctypes.create_string_buffer(n.value + 1)
+    _lib.check(_lib.hip.qsim_jit_source(circuit.getNumQubits(), arr, cnt, buf, n.value + 1,
+                                        ctypes.byref(n)))
+    return buf.value.decode()
+
+
+def jit_build(circuit: Circuit) -> int:
+    """Compile the circuit's generated pass kernels with hipRTC for gfx950 (no GPU needed);
+    returns the code-object size in bytes (0 when nothing is specialised)."""
+    arr, cnt = circuit.to_abi()
+    n = ctypes.c_size_t(0)
+    _lib.check(_lib.hip.qsim_jit_build(circuit.getNumQubits(), arr, cnt, ctypes.byref(n)))
+    return n.value

@@ -110,6 +110,17 @@ int qsim_apply_matrix1q(qsim_state* s, int target, const double m[8],
  * gates on disjoint qubits. */
 int qsim_plan_fused(int n_qubits, const qsim_gate* gates, size_t count, int hmax,
                     int32_t* order, int32_t* pass_of, int32_t* n_passes);
+/* Circuit-specialised pass kernels (hipRTC, no reference counterpart: the reference launches one
+ * fixed kernel per gate, src/Simulator.cu:38-154).  mode 0 = off, 1 = compile in the background
+ * on a plan's first run and switch to the compiled kernels when ready (default), 2 = compile on
+ * the first run before launching; states below min_qubits always use the pass interpreter.
+ * A negative argument leaves that setting unchanged (env defaults: QSIM_JIT, QSIM_JIT_MIN_QUBITS). */
+int qsim_set_jit(int mode, int min_qubits);
+/* Host-only: the generated source of a circuit's plan (len = its size; buf gets up to cap-1
+ * bytes + NUL), and a hipRTC compile of it for gfx950 (code_bytes = code-object size). */
+int qsim_jit_source(int n_qubits, const qsim_gate* gates, size_t count, char* buf, size_t cap,
+                    size_t* len);
+int qsim_jit_build(int n_qubits, const qsim_gate* gates, size_t count, size_t* code_bytes);
 /* Kernel-level entry on a raw device pointer (the reference's Gates.cuh kernels, launched by
  * tests/test_statevector.cu:151-159).  stream may be NULL (the null stream). */
 int qsim_apply_gate_raw(void* dstate, int n_qubits, const qsim_gate* g, void* stream);
