@@ -44,9 +44,13 @@ def parse():
     p.add_argument("--jit", type=int, choices=[0, 1, 2], default=2,
                    help="circuit-specialised pass kernels: 0 interpreter only, 1 background "
                         "compile, 2 compile during the first warmup run (default)")
-    p.add_argument("--workload", choices=["hc", "ref", "1q"], default="hc",
+    p.add_argument("--workload", choices=["hc", "ref", "1q", "batch"], default="hc",
                    help="hc: W-HC random H+CNOT; ref: reference benchmark_scaling circuit; "
-                        "1q: 100 unfused H gates on targets i %% n")
+                        "1q: 100 unfused H gates on targets i %% n; batch: W-BATCH, the W-HC "
+                        "circuit on --trajectories noisy trajectories (depolarizing on every "
+                        "qubit after every gate, SURVEY §8(d))")
+    p.add_argument("--trajectories", type=int, default=1024)
+    p.add_argument("--noise", type=float, default=0.01)
     p.add_argument("--cpu-budget", type=float, default=12.0,
                    help="seconds of single-thread CPU oracle work for cpu_baseline (0 = skip)")
     p.add_argument("--pmc-json", default=None,
@@ -168,9 +172,62 @@ def run_single(args):
     print(json.dumps(out))
 
 
+def run_batch(args):
+    """W-BATCH (BASELINE config 4): BatchedSimulator, n qubits x B trajectories, depolarizing p on
+    every qubit after every gate (NoiseModel.addDepolarizingAll), the W-HC circuit.  value =
+    trajectory-gates/s.  Algorithmic bytes per gate step: the gate's own bytes x B plus the
+    realised Pauli errors; the dominant-kernel roofline uses each kernel's own
+    per-launch bytes."""
+    import qsim_amd as q
+    n, B = args.qubits, args.trajectories
+    circuit = q.createRandomHCCircuit(n, args.depth, args.seed)
+    nm = q.NoiseModel()
+    nm.addDepolarizingAll(n, args.noise)
+    sim = q.BatchedSimulator(n, B, nm)
+    sim.setSeed(args.seed)
+    for _ in range(args.warmup):
+        sim.run(circuit)
+    sim.synchronize()
+    sim.profile(True)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        sim.run(circuit)
+    sim.synchronize()
+    wall = time.perf_counter() - t0
+    stats = sim.profileStats()
+    sim.profile(False)
+    gates = circuit.getGateCount()
+    gate_stats = [s for s in stats if s["alg_bytes"] > 0]  # (noise kernels carry no byte count)
+    dom = max(gate_stats, key=lambda s: s["ms"]) if gate_stats else None
+    roof = None
+    if dom and dom["launches"]:
+        per = dom["alg_bytes"] / dom["launches"]
+        avg_s = dom["ms"] / dom["launches"] / 1e3
+        ach = per / avg_s / 1e9
+        roof = {"bound": "hbm", "kernel": dom["name"], "achieved": round(ach, 1), "peak": HBM_PEAK_GBPS,
+                "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBPS, 4), "traffic": None,
+                "alg_bytes_per_launch": per, "avg_launch_ms": round(avg_s * 1e3, 4),
+                "launches": dom["launches"]}
+    out = {
+        "metric": "trajectory-gates/s, W-HC circuit on noisy trajectories (BatchedSimulator)",
+        "value": round(gates * B * args.steps / wall, 1), "unit": "trajectory-gates/s",
+        "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(wall / args.steps * 1e3, 3), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "c128 (complex<double>)", "data": "synthetic",
+        "config": {"workload": f"W-BATCH {n}q x {B} trajectories, depolarizing {args.noise} on all "
+                               f"qubits after every gate, W-HC depth {args.depth} seed {args.seed}",
+                   "qubits": n, "trajectories": B, "gates": gates, "state_bytes": (16 << n) * B},
+        "roofline": roof, "kernels": stats, "cpu_baseline": None,
+    }
+    print(json.dumps(out))
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.workload == "batch":
+        run_batch(args)
+        return
     if world > 1 or args.gpus > 1:
         from qsim_amd import dist_bench  # sharded strong-scaling path (RCCL over xGMI)
         dist_bench.run(args, METRIC, HBM_PEAK_GBPS)
