@@ -105,8 +105,23 @@ static void plan_stages(std::vector<TileOp>& pass_ops, std::vector<int>& pass_sr
         }
         return t;
     };
-    // pad with the highest unused allowed bits (threads then walk consecutive LDS slots)
-    auto pad = [&](uint32_t sbits, uint32_t allowed) {
+    // Fill a stage's free register bits: first with the stage ops' control bits, most used first
+    // (a control on a register bit is resolved per register pair — a rename or a skipped pair —
+    // instead of a per-lane select), then with the highest unused allowed bits (threads then walk
+    // consecutive LDS slots).
+    auto pad = [&](uint32_t sbits, uint32_t allowed, const std::vector<int>& in) {
+        int cnt[32] = {0};
+        for (int i : in)
+            for (int b = 0; b < tile_bits; ++b)
+                if ((ops[i].cmask >> b) & 1u) ++cnt[b];
+        while (__builtin_popcount(sbits) < rb) {
+            int best = -1;
+            for (int b = 0; b < tile_bits; ++b)
+                if (((allowed & ~sbits) >> b) & 1u && cnt[b] > 0 && (best < 0 || cnt[b] > cnt[best]))
+                    best = b;
+            if (best < 0) break;
+            sbits |= 1u << best;
+        }
         for (int b = tile_bits - 1; b >= 0 && __builtin_popcount(sbits) < rb; --b)
             if ((allowed >> b) & 1u) sbits |= 1u << b;
         return sbits;
@@ -115,7 +130,7 @@ static void plan_stages(std::vector<TileOp>& pass_ops, std::vector<int>& pass_sr
     for (size_t i = 0; i < rem.size(); ++i) rem[i] = (int)i;
     std::vector<std::pair<uint32_t, std::vector<int>>> seq;  // (register bits, ops) per stage
     Taken first = take(rem, high_bits);
-    seq.push_back({pad(first.sbits, high_bits), first.in});
+    seq.push_back({pad(first.sbits, high_bits, first.in), first.in});
     rem.swap(first.deferred);
     while (!rem.empty()) {
         Taken t = take(rem, all_bits);
@@ -123,10 +138,12 @@ static void plan_stages(std::vector<TileOp>& pass_ops, std::vector<int>& pass_sr
         rem.swap(t.deferred);
     }
     if (seq.size() > 1) {  // the last stage must be storable straight from registers
-        if ((seq.back().first & ~high_bits) == 0) seq.back().first = pad(seq.back().first, high_bits);
-        else seq.push_back({pad(0u, high_bits), {}});
+        if ((seq.back().first & ~high_bits) == 0)
+            seq.back().first = pad(seq.back().first, high_bits, seq.back().second);
+        else
+            seq.push_back({pad(0u, high_bits, {}), {}});
     }
-    for (size_t k = 1; k + 1 < seq.size(); ++k) seq[k].first = pad(seq[k].first, all_bits);
+    for (size_t k = 1; k + 1 < seq.size(); ++k) seq[k].first = pad(seq[k].first, all_bits, seq[k].second);
     for (auto& sq : seq) {
         const uint32_t sbits = sq.first;
         const std::vector<int>& in = sq.second;
