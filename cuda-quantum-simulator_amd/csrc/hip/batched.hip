@@ -15,6 +15,7 @@
 // too: BitFlip/PhaseFlip/BitPhaseFlip are applied (X/Z/Y), damping channels are ignored.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <random>
@@ -44,13 +45,12 @@ struct DevChannel {
     double p;
 };
 
-// One thread per trajectory: compose this step's Pauli picks into (e, x, z).
-__global__ void k_pauli_draw(const DevChannel* ch, int nch, uint64_t seed, uint64_t step,
-                             int batch, uint64_t* xz, int* ephase) {
-    const int b = blockIdx.x * blockDim.x + threadIdx.x;
-    if (b >= batch) return;
-    uint64_t x = 0, z = 0;
-    int e = 0;
+// This step's Pauli picks of trajectory b, composed into i^e X^x Z^z (channels in order).
+__device__ __forceinline__ void draw_step(const DevChannel* ch, int nch, uint64_t seed, uint64_t step,
+                                          int b, uint64_t& x, uint64_t& z, int& e) {
+    x = 0;
+    z = 0;
+    e = 0;
     for (int c = 0; c < nch; ++c) {
         const uint64_t key = mix64(seed ^ mix64(step * 0x100000001b3ull + (uint64_t)c) ^
                                    ((uint64_t)b << 20));
@@ -78,9 +78,48 @@ __global__ void k_pauli_draw(const DevChannel* ch, int nch, uint64_t seed, uint6
             z ^= q;
         }
     }
+    e &= 3;
+}
+
+// One thread per trajectory: compose this step's Pauli picks into (e, x, z).
+__global__ void k_pauli_draw(const DevChannel* ch, int nch, uint64_t seed, uint64_t step,
+                             int batch, uint64_t* xz, int* ephase) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= batch) return;
+    uint64_t x, z;
+    int e;
+    draw_step(ch, nch, seed, step, b, x, z, e);
     xz[2 * b] = x;
     xz[2 * b + 1] = z;
-    ephase[b] = e & 3;
+    ephase[b] = e;
+}
+
+// Pauli frames for a whole run (one thread per trajectory).  With the frame Phi = i^E X^F Z^G
+// (state = Phi * stored vector), the noise P = i^e X^x Z^z after step s updates
+// Phi <- P Phi = i^(e+E) (-1)^popc(z & F) X^(x^F) Z^(z^G); frames[s] is the frame in force
+// BEFORE gate s (gates are applied to the stored vector conjugated by it, fused.hip), fin the
+// frame after the last step (materialised with k_pauli_apply).  Same draws as k_pauli_draw.
+__global__ void k_frame_build(const DevChannel* ch, int nch, uint64_t seed, uint64_t step0,
+                              int count, int batch, uint64_t* frames, uint64_t* fin_xz,
+                              int* fin_e) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= batch) return;
+    uint64_t F = 0, G = 0;
+    int E = 0;
+    for (int s = 0; s < count; ++s) {
+        uint64_t* fr = frames + 2 * ((uint64_t)s * batch + b);
+        fr[0] = F;
+        fr[1] = G;
+        uint64_t x, z;
+        int e;
+        draw_step(ch, nch, seed, step0 + (uint64_t)s, b, x, z, e);
+        E += e + ((__popcll(z & F) & 1) ? 2 : 0);
+        F ^= x;
+        G ^= z;
+    }
+    fin_xz[2 * b] = F;
+    fin_xz[2 * b + 1] = G;
+    fin_e[b] = E & 3;
 }
 
 __device__ __forceinline__ double2 mul_ipow(double2 a, int e) {
@@ -135,6 +174,10 @@ struct qsim_batch {
     int* d_e = nullptr;
     DevChannel* d_ch = nullptr;
     size_t ch_cap = 0;
+    uint64_t* d_frames = nullptr;  // Pauli frames of the current run, [steps][batch][2]
+    size_t frames_cap = 0;
+    DevBuf ops, stages;             // fused-plan descriptors
+    PlanCache plans;
     Timer timer;
     ~qsim_batch() {
         if (stream) (void)hipStreamSynchronize(stream);
@@ -142,6 +185,7 @@ struct qsim_batch {
         if (d_xz) (void)hipFree(d_xz);
         if (d_e) (void)hipFree(d_e);
         if (d_ch) (void)hipFree(d_ch);
+        if (d_frames) (void)hipFree(d_frames);
         if (stream) (void)hipStreamDestroy(stream);
     }
 };
@@ -248,6 +292,54 @@ int qsim_batch_run(qsim_batch* b, const qsim_gate* gates, size_t count,
         }
         const uint64_t N = 1ull << b->n;
         const uint64_t items_per_traj = N / 2 > 0 ? N / 2 : 1;
+        static const bool fused_env = [] {
+            const char* e = std::getenv("QSIM_BATCH_FUSED");
+            return e == nullptr || std::atoi(e) != 0;
+        }();
+        if (b->n >= 10 && fused_env && !(flags & QSIM_BATCH_PER_GATE)) {
+            // Fused tile passes over all trajectories (a tile never straddles two).  Noise is
+            // carried as per-trajectory Pauli frames: no noise kernel per gate, one frame build
+            // before and one materialising Pauli pass after the circuit.
+            std::vector<Op> fops;
+            for (size_t i = 0; i < ops.size(); ++i) {
+                if (ops[i].kind < 0) continue;  // ignored by the reference gate set
+                fops.push_back(ops[i]);
+                fops.back().src = (int)i;       // circuit step (frame index)
+            }
+            const bool noisy = !ch.empty() && count > 0;
+            if (noisy) {
+                const size_t need_frames = 2 * count * (size_t)b->batch;
+                if (need_frames > b->frames_cap) {
+                    QSIM_HIPCHK(hipStreamSynchronize(b->stream));
+                    if (b->d_frames) QSIM_HIPCHK(hipFree(b->d_frames));
+                    b->d_frames = nullptr;
+                    QSIM_HIPCHK(hipMalloc((void**)&b->d_frames, need_frames * sizeof(uint64_t)));
+                    b->frames_cap = need_frames;
+                }
+                TimedLaunch tl(&b->timer, "pauli_frames", 0.0, b->stream);
+                hipLaunchKernelGGL(k_frame_build, dim3((b->batch + 255) / 256), dim3(256), 0, b->stream,
+                                   b->d_ch, (int)ch.size(), b->seed, b->step, (int)count, b->batch,
+                                   b->d_frames, b->d_xz, b->d_e);
+                QSIM_HIPCHK(hipGetLastError());
+            }
+            if (!fops.empty()) {
+                const Plan& plan = b->plans.get(fops, b->n);
+                b->ops.upload(plan.ops.data(), plan.ops.size() * sizeof(TileOp), b->stream);
+                b->stages.upload(plan.stages.data(), plan.stages.size() * sizeof(Stage), b->stream);
+                launch_fused(b->d, b->n, (uint64_t)b->batch, plan, (const TileOp*)b->ops.ptr,
+                             (const Stage*)b->stages.ptr, b->stream, &b->timer, nullptr,
+                             noisy ? b->d_frames : nullptr);
+            }
+            if (noisy) {
+                b->step += count;
+                const uint64_t total = items_per_traj * (uint64_t)b->batch;
+                TimedLaunch tl(&b->timer, "pauli_apply", 0.0, b->stream);
+                hipLaunchKernelGGL(k_pauli_apply, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
+                                   b->stream, b->d, b->n, b->d_xz, b->d_e, items_per_traj);
+                QSIM_HIPCHK(hipGetLastError());
+            }
+            return;
+        }
         for (const Op& op : ops) {
             if (op.kind >= 0) launch_op(b->d, b->n, (uint64_t)b->batch, op, b->stream, &b->timer);
             if (!ch.empty()) {

@@ -102,6 +102,11 @@ struct TileOp {            // an Op re-expressed in tile-index bits
     int p0;                // staged kernel: register-bit position of the target (-1: thread bit)
     uint32_t cm_reg;       // staged kernel: controls among the stage bits, in register-bit space
     uint32_t cm_thr;       // staged kernel: controls among the other tile bits (tile space)
+    // Pauli-frame fields (batched noisy runs, batched.hip): the op's circuit step, its target
+    // qubit, and per control (<= 2) its qubit, register position in its stage (-1: thread bit)
+    // and tile bit.
+    int step, tq;
+    int cq[2], cpos[2], cb[2];
     int _pad;
     double m[8];
 };
@@ -159,8 +164,10 @@ struct PlanCache {
     JitState jit;
     const Plan& get(const std::vector<Op>& ops, int n_qubits);
 };
+// frames != null: batched noisy run under per-trajectory Pauli frames (FArgs::frames).
 void launch_fused(double2* st, int n, uint64_t batch, const Plan& plan, const TileOp* d_ops,
-                  const Stage* d_stages, hipStream_t s, Timer* tm, const JitModule* jm = nullptr);
+                  const Stage* d_stages, hipStream_t s, Timer* tm, const JitModule* jm = nullptr,
+                  const uint64_t* frames = nullptr);
 
 // Reductions / readout helpers (reduce.hip)
 void launch_init_basis(double2* st, int n, uint64_t batch, uint64_t basis, hipStream_t s);

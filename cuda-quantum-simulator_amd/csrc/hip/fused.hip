@@ -63,6 +63,7 @@ static void plan_stages(std::vector<TileOp>& pass_ops, std::vector<int>& pass_sr
             ops.push_back(make_tile_op(K_M1, S_X, t.b1, -1, t.cmask | a, 0, xm));
             ops.push_back(make_tile_op(K_M1, S_X, t.b0, -1, t.cmask | b, 0, xm));
             ops.push_back(make_tile_op(K_M1, S_X, t.b1, -1, t.cmask | a, 0, xm));
+            for (int k = 1; k <= 3; ++k) ops[ops.size() - k].step = t.step;
             src.push_back(pass_src[i]);  // the gate is reported once (introspection skips -1)
             src.push_back(-1);
             src.push_back(-1);
@@ -174,6 +175,18 @@ static void plan_stages(std::vector<TileOp>& pass_ops, std::vector<int>& pass_sr
             for (int b = 0; b < tile_bits; ++b)
                 if (((t.cmask & sbits) >> b) & 1u) t.cm_reg |= 1u << pos_of[b];
             t.cm_thr = t.cmask & ~sbits;
+            auto qubit_of = [&](int b) { return b < p.r0 ? b : p.hpos[b - p.r0]; };
+            t.tq = qubit_of(t.b0);
+            int nc = 0;
+            for (int b = 0; b < tile_bits; ++b) {
+                if (!((t.cmask >> b) & 1u)) continue;
+                if (nc == 2) fail(QSIM_ERR_RUNTIME, "tile op with more than two controls");
+                t.cq[nc] = qubit_of(b);
+                t.cb[nc] = b;
+                t.cpos[nc] = ((sbits >> b) & 1u) ? pos_of[b] : -1;
+                ++nc;
+            }
+            for (; nc < 2; ++nc) t.cq[nc] = t.cb[nc] = t.cpos[nc] = -1;
             plan.ops.push_back(t);
             plan.order.push_back(src[i]);
         }
@@ -370,6 +383,7 @@ Plan plan_fused(const std::vector<Op>& ops, int n, int hmax) {
             int b0 = bit_of[op.t0], b1 = op.kind == K_SWAP ? bit_of[op.t1] : -1;
             if (op.kind == K_SWAP && b0 > b1) std::swap(b0, b1);
             tops.push_back(make_tile_op(op.kind, op.sub, b0, b1, cm, op.d0_one ? 1 : 0, op.m));
+            tops.back().step = op.src;
             tsrc.push_back(op.src);
         }
         if (heff >= 4) {
@@ -404,6 +418,10 @@ struct FArgs {
     int hpos[8];
     int r0;              // run bits (tile bits 0..r0-1 = qubits 0..r0-1); hpos covers the rest
     double scale;        // applied at the store: (1/sqrt2)^(unnormalized H butterflies)
+    // Pauli frames of a batched noisy run: frames[2 * (step * nbatch + traj)] = {F, G}, the
+    // frame X^F Z^G (phase dropped) in force before circuit step `step` (batched.hip).
+    const uint64_t* frames;
+    int nbatch;
 };
 
 // Runtime-count forms for the staged kernel (count = tile bits above the run, <= 8).
@@ -666,6 +684,77 @@ __device__ __forceinline__ void stage_op(double2 (&v)[1 << RB], uint32_t jb, con
     }
 }
 
+// One op under a Pauli frame X^F Z^G (batched noisy runs).  The stored vector phi relates to the
+// trajectory's state by psi = X^F Z^G phi (up to a phase), so a gate U on psi is applied to phi as
+// Z^G X^F U X^F Z^G: for the target qubit t that is M -> X^f M X^f (rows and columns swapped
+// when f = F_t) then the off-diagonal signs flipped when g = G_t; a control c is satisfied when
+// the stored bit is 1 ^ F_c; a diagonal op applies d(stored bit ^ f).  Everything runs through
+// the general arms (one select per dword); F and G are uniform over a tile (one trajectory).
+template <int RB, int P>
+__device__ __forceinline__ void frame_m1(double2 (&v)[1 << RB], uint32_t jb, const TileOp& op,
+                                         double2 m0, double2 m1, double2 m2, double2 m3,
+                                         uint32_t pol_reg, uint32_t pol_thr) {
+    const uint32_t cr = op.cm_reg, ct = op.cm_thr;
+    const bool thr_ok = ((jb ^ pol_thr) & ct) == ct;
+#pragma unroll
+    for (int r = 0; r < (1 << RB); ++r) {
+        if (r & (1 << P)) continue;
+        const double2 a0 = v[r], a1 = v[r | (1 << P)];
+        const bool ok = ((((uint32_t)r ^ pol_reg) & cr) == cr) && thr_ok;
+        v[r] = sel(ok, cadd(cmul(m0, a0), cmul(m1, a1)), a0);
+        v[r | (1 << P)] = sel(ok, cadd(cmul(m2, a0), cmul(m3, a1)), a1);
+    }
+}
+
+template <int RB>
+__device__ __forceinline__ void stage_op_frame(double2 (&v)[1 << RB], uint32_t jb, const TileOp& op,
+                                               const uint64_t* frames, int nbatch, uint64_t traj) {
+    const uint64_t* fr = frames + 2 * ((uint64_t)op.step * (uint64_t)nbatch + traj);
+    const uint64_t F = fr[0], G = fr[1];  // uniform: scalar loads
+    uint32_t pol_reg = 0, pol_thr = 0;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        if (op.cq[k] < 0 || !((F >> op.cq[k]) & 1ull)) continue;
+        if (op.cpos[k] >= 0) pol_reg |= 1u << op.cpos[k];
+        else pol_thr |= 1u << op.cb[k];
+    }
+    const bool f = (F >> op.tq) & 1ull, g = (G >> op.tq) & 1ull;
+    if (op.kind == K_DIAG) {
+        const double2 d0 = make_double2(op.m[0], op.m[1]), d1 = make_double2(op.m[2], op.m[3]);
+        const uint32_t cr = op.cm_reg, ct = op.cm_thr;
+        const bool thr_ok = ((jb ^ pol_thr) & ct) == ct;
+        const bool tbit = (((jb >> op.b0) & 1u) != 0) != f;
+#pragma unroll
+        for (int r = 0; r < (1 << RB); ++r) {
+            const bool bit = op.p0 >= 0 ? ((((r >> op.p0) & 1) != 0) != f) : tbit;  // logical bit
+            const bool ok = ((((uint32_t)r ^ pol_reg) & cr) == cr) && thr_ok && (bit || !op.d0_one);
+            const double2 d = make_double2(bit ? d1.x : d0.x, bit ? d1.y : d0.y);
+            v[r] = sel(ok, cmul(d, v[r]), v[r]);
+        }
+        return;
+    }
+    double2 m0 = make_double2(op.m[0], op.m[1]), m1 = make_double2(op.m[2], op.m[3]);
+    double2 m2 = make_double2(op.m[4], op.m[5]), m3 = make_double2(op.m[6], op.m[7]);
+    if (f) {  // X M X
+        const double2 t0 = m0, t1 = m1;
+        m0 = m3;
+        m1 = m2;
+        m2 = t1;
+        m3 = t0;
+    }
+    if (g) {  // Z M Z
+        m1 = make_double2(-m1.x, -m1.y);
+        m2 = make_double2(-m2.x, -m2.y);
+    }
+    switch (op.p0) {
+        case 0: frame_m1<RB, 0>(v, jb, op, m0, m1, m2, m3, pol_reg, pol_thr); break;
+        case 1: frame_m1<RB, 1>(v, jb, op, m0, m1, m2, m3, pol_reg, pol_thr); break;
+        case 2: if constexpr (RB > 2) frame_m1<RB, 2>(v, jb, op, m0, m1, m2, m3, pol_reg, pol_thr); break;
+        case 3: if constexpr (RB > 3) frame_m1<RB, 3>(v, jb, op, m0, m1, m2, m3, pol_reg, pol_thr); break;
+        default: break;
+    }
+}
+
 // Thread index spread over the tile bits that are not the stage's register bits.
 template <int RB>
 __device__ __forceinline__ uint32_t stage_jb(const Stage& st) {
@@ -680,7 +769,7 @@ __device__ __forceinline__ uint32_t stage_jb(const Stage& st) {
 // register bits, so a wave still moves 64 consecutive amplitudes = one 1 KiB run per
 // instruction); only the stages in between round-trip through LDS (read, ops, write, barrier).
 // A pass whose ops fit one such stage never touches LDS.
-template <int H, bool NT>
+template <int H, bool NT, bool FR = false>
 __global__ __launch_bounds__(256, 2) void k_fused_staged(FArgs a) {  // 2 WGs/CU (LDS-bound)
     constexpr int T = 64 << H;
     constexpr int RB = H - 2;
@@ -706,7 +795,13 @@ __global__ __launch_bounds__(256, 2) void k_fused_staged(FArgs a) {  // 2 WGs/CU
 #pragma unroll
             for (int r = 0; r < R; ++r) v[r] = *reinterpret_cast<const double2*>(lds + (lb ^ sg.lds[r]));
         }
-        for (int o = sg.op_begin; o < sg.op_end; ++o) stage_op<RB>(v, jb, ldc(a.ops, o));
+        if constexpr (FR) {
+            const uint64_t traj = tile_id >> a.log_tpt;
+            for (int o = sg.op_begin; o < sg.op_end; ++o)
+                stage_op_frame<RB>(v, jb, ldc(a.ops, o), a.frames, a.nbatch, traj);
+        } else {
+            for (int o = sg.op_begin; o < sg.op_end; ++o) stage_op<RB>(v, jb, ldc(a.ops, o));
+        }
         if (s == se - 1) {
             const uint64_t gb = base | (jb & run_mask) | spread_n(jb >> r0, a.hpos, nh);
             const double sc = a.scale;
@@ -733,10 +828,13 @@ static bool fused_nt() {
 }
 
 void launch_fused(double2* st, int n, uint64_t batch, const Plan& plan, const TileOp* d_ops,
-                  const Stage* d_stages, hipStream_t s, Timer* tm, const JitModule* jm) {
+                  const Stage* d_stages, hipStream_t s, Timer* tm, const JitModule* jm,
+                  const uint64_t* frames) {
     const double pass_bytes = 32.0 * (double)(1ull << n) * (double)batch;
     const bool nt = fused_nt();
     for (const FusedPass& p : plan.passes) {
+        if (frames && (p.single >= 0 || p.h < 4))
+            fail(QSIM_ERR_RUNTIME, "Pauli-frame passes need staged tiles (n >= 10)");
         if (p.single >= 0) {
             launch_op(st, n, batch, plan.singles[p.single], s, tm);
             continue;
@@ -759,6 +857,18 @@ void launch_fused(double2* st, int n, uint64_t batch, const Plan& plan, const Ti
         a.tpt_mask = (1ull << lt) - 1ull;
         const uint64_t blocks = batch << lt;
         TimedLaunch tl(tm, "fused_tile", pass_bytes, s);
+        if (frames) {  // batched noisy run: general arms under the trajectory's Pauli frame
+            a.frames = frames;
+            a.nbatch = (int)batch;
+            a.scale = 1.0;  // H runs as its normalised matrix here
+            switch (p.h) {
+                case 4: hipLaunchKernelGGL((k_fused_staged<4, true, true>), dim3((unsigned)blocks), dim3(256), 0, s, a); break;
+                case 5: hipLaunchKernelGGL((k_fused_staged<5, true, true>), dim3((unsigned)blocks), dim3(256), 0, s, a); break;
+                default: hipLaunchKernelGGL((k_fused_staged<6, true, true>), dim3((unsigned)blocks), dim3(256), 0, s, a); break;
+            }
+            QSIM_HIPCHK(hipGetLastError());
+            continue;
+        }
         const size_t pi = (size_t)(&p - plan.passes.data());
         if (jm && pi < jm->fn.size() && jm->fn[pi]) {  // circuit-specialised kernel (jit.hip)
             unsigned long long stride = a.stride, tpt = a.tpt_mask;

@@ -356,12 +356,15 @@ class BatchedSimulator:
 
     def reset(self) -> None: _lib.check(_lib.hip.qsim_batch_reset(self._h))
 
-    def run(self, circuit: Circuit) -> None:
+    def run(self, circuit: Circuit, per_gate: bool = False) -> None:
+        """per_gate: one kernel per gate and one Pauli pass per noisy step (the reference's
+        structure) instead of fused passes under Pauli frames; identical trajectories."""
         if circuit.getNumQubits() != self._n:
             raise ValueError("Circuit qubit count doesn't match simulator")
         g, ng = circuit.to_abi()
         ch, nch = self._noise.to_abi()
-        _lib.check(_lib.hip.qsim_batch_run(self._h, g, ng, ch, nch, int(self._gate_set)))
+        flags = int(self._gate_set) | (_lib.QSIM_BATCH_PER_GATE if per_gate else 0)
+        _lib.check(_lib.hip.qsim_batch_run(self._h, g, ng, ch, nch, flags))
 
     def synchronize(self) -> None: _lib.check(_lib.hip.qsim_batch_sync(self._h))
 

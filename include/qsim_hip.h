@@ -163,8 +163,11 @@ int qsim_batch_reset(qsim_batch* b);
 int qsim_batch_set_seed(qsim_batch* b, uint64_t seed);
 /* Apply the circuit to every trajectory; after each gate apply every channel (reference
  * BatchedSimulator::run, src/NoiseModel.cu:815-831).  Gate semantics follow
- * src/NoiseModel.cu:717-801 when flags has QSIM_BATCH_REFERENCE_GATESET, else the full gate set. */
-enum { QSIM_BATCH_FULL_GATESET = 0, QSIM_BATCH_REFERENCE_GATESET = 1 };
+ * src/NoiseModel.cu:717-801 when flags has QSIM_BATCH_REFERENCE_GATESET, else the full gate set.
+ * For n >= 10 the gates run as fused tile passes with the noise carried as per-trajectory Pauli
+ * frames (same draws, same trajectories); QSIM_BATCH_PER_GATE forces one kernel per gate plus
+ * one Pauli pass per noisy step (the reference's structure). */
+enum { QSIM_BATCH_FULL_GATESET = 0, QSIM_BATCH_REFERENCE_GATESET = 1, QSIM_BATCH_PER_GATE = 2 };
 int qsim_batch_run(qsim_batch* b, const qsim_gate* gates, size_t count,
                    const qsim_noise_channel* channels, size_t n_channels, int flags);
 int qsim_batch_avg_probabilities(qsim_batch* b, double* dst);           /* 2^n */

@@ -1,0 +1,103 @@
+"""Batched trajectories on fused tile passes (batched.hip + fused.hip): the Pauli-frame execution
+must give exactly the trajectories of the per-gate execution (one kernel per gate and one Pauli
+pass per noisy step — the reference's structure, src/NoiseModel.cu:815-892) for the same seed,
+and noise-free trajectories must equal the oracle state."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _mixed(q, n, depth, seed, gateset="full"):
+    rng = np.random.default_rng(seed)
+    c = q.Circuit(n)
+    for _ in range(depth):
+        a, b, d = (int(x) for x in rng.choice(n, 3, replace=False))
+        th = float(rng.uniform(-3.0, 3.0))
+        k = int(rng.integers(0, 6 if gateset == "reference" else 17))
+        if gateset == "reference":
+            (c.x, c.y, c.z, c.h)[k](a) if k < 4 else c.cnot(a, b)
+            continue
+        if k < 8:
+            getattr(c, ("x", "y", "z", "h", "s", "t", "sdag", "tdag")[k])(a)
+        elif k < 11:
+            getattr(c, ("rx", "ry", "rz")[k - 8])(a, th)
+        elif k == 11:
+            c.cnot(a, b)
+        elif k == 12:
+            c.cz(a, b)
+        elif k == 13:
+            c.cry(a, b, th)
+        elif k == 14:
+            c.crz(a, b, th)
+        elif k == 15:
+            c.swap(a, b)
+        else:
+            c.toffoli(a, b, d)
+    return c
+
+
+def _noise(q, n):
+    nm = q.NoiseModel()
+    nm.addDepolarizingAll(n, 0.12)
+    nm.addBitFlip([0, n - 1], 0.2)
+    nm.addPhaseFlip([1, n // 2], 0.2)
+    nm.addBitPhaseFlip([2, n - 2], 0.1)
+    return nm
+
+
+@pytest.mark.parametrize("n,B,seed", [(10, 8, 1), (12, 16, 2), (13, 4, 3)])
+def test_frames_equal_per_gate(qsim, gpu_ready, n, B, seed):
+    c = _mixed(qsim, n, 60, seed)
+    nm = _noise(qsim, n)
+    fused, ref = qsim.BatchedSimulator(n, B, nm), qsim.BatchedSimulator(n, B, nm)
+    fused.setSeed(seed)
+    ref.setSeed(seed)
+    for _ in range(2):  # the second run continues the noise stream (step counter)
+        fused.run(c)
+        ref.run(c, per_gate=True)
+    for t in range(B):
+        np.testing.assert_allclose(fused.getStateVector(t), ref.getStateVector(t), atol=1e-12, rtol=0)
+    avg = fused.getAverageProbabilities()
+    assert abs(avg.sum() - 1.0) < 1e-10
+
+
+def test_frames_reference_gateset(qsim, gpu_ready):
+    n, B = 11, 8
+    c = _mixed(qsim, n, 80, 7)
+    c.rz(3, 0.4)  # ignored by the reference gate set, still followed by noise
+    nm = _noise(qsim, n)
+    out = []
+    for per_gate in (False, True):
+        s = qsim.BatchedSimulator(n, B, nm, gate_set=qsim.BatchedGateSet.Reference)
+        s.setSeed(5)
+        s.run(c, per_gate=per_gate)
+        out.append([s.getStateVector(t) for t in range(B)])
+    for a, b in zip(*out):
+        np.testing.assert_allclose(a, b, atol=1e-12, rtol=0)
+
+
+def test_noise_free_fused_batch_matches_oracle(qsim, oracle, gpu_ready):
+    n, B = 12, 6
+    c = _mixed(qsim, n, 150, 11)
+    s = qsim.BatchedSimulator(n, B)
+    s.run(c)
+    ref = oracle.run_cpu(n, oracle.gates_of(c))
+    for t in range(B):
+        np.testing.assert_allclose(s.getStateVector(t), ref, atol=1e-12, rtol=0)
+
+
+def test_frames_noise_actually_applied(qsim, gpu_ready):
+    """With p = 1 bit flips on qubit 0 after every gate the trajectories are deterministic."""
+    n, B = 10, 4
+    c = qsim.Circuit(n)
+    c.h(3).cnot(3, 5).x(7)  # 3 gates -> 3 flips of qubit 0 -> net X on qubit 0
+    nm = qsim.NoiseModel()
+    nm.addBitFlip([0], 1.0)
+    s = qsim.BatchedSimulator(n, B, nm)
+    s.run(c)
+    ideal = qsim.Simulator(n)
+    ideal.run(c)
+    ideal.applyGate(qsim.GateOp(qsim.GateType.X, [0]))
+    for t in range(B):
+        np.testing.assert_allclose(s.getStateVector(t), ideal.getStateVector(), atol=1e-12, rtol=0)
