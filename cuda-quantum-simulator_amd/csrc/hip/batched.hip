@@ -94,26 +94,39 @@ __global__ void k_pauli_draw(const DevChannel* ch, int nch, uint64_t seed, uint6
     ephase[b] = e;
 }
 
-// Pauli frames for a whole run (one thread per trajectory).  With the frame Phi = i^E X^F Z^G
-// (state = Phi * stored vector), the noise P = i^e X^x Z^z after step s updates
-// Phi <- P Phi = i^(e+E) (-1)^popc(z & F) X^(x^F) Z^(z^G); frames[s] is the frame in force
-// BEFORE gate s (gates are applied to the stored vector conjugated by it, fused.hip), fin the
-// frame after the last step (materialised with k_pauli_apply).  Same draws as k_pauli_draw.
-__global__ void k_frame_build(const DevChannel* ch, int nch, uint64_t seed, uint64_t step0,
-                              int count, int batch, uint64_t* frames, uint64_t* fin_xz,
-                              int* fin_e) {
+// Pauli frames for a whole run.  With the frame Phi = i^E X^F Z^G (state = Phi * stored vector),
+// the noise P = i^e X^x Z^z after step s updates Phi <- P Phi = i^(e+E) (-1)^popc(z & F)
+// X^(x^F) Z^(z^G); frames[s] is the frame in force BEFORE gate s (gates are applied to the stored
+// vector conjugated by it, fused.hip), fin the frame after the last step (materialised with
+// k_pauli_apply).  Same draws as k_pauli_draw.  Two kernels: every (step, trajectory) draw in
+// parallel (written into frames[s] as (x, z) plus ephase[s]), then one thread per trajectory
+// scans the steps in order, replacing each draw by the frame before it.
+__global__ void k_draw_steps(const DevChannel* ch, int nch, uint64_t seed, uint64_t step0,
+                             int count, int batch, uint64_t* frames, int* ephase) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (uint64_t)count * batch) return;
+    const int s = (int)(i / batch), b = (int)(i - (uint64_t)s * batch);
+    uint64_t x, z;
+    int e;
+    draw_step(ch, nch, seed, step0 + (uint64_t)s, b, x, z, e);
+    frames[2 * i] = x;
+    frames[2 * i + 1] = z;
+    ephase[i] = e;
+}
+
+__global__ void k_frame_build(int count, int batch, uint64_t* frames, const int* ephase,
+                              uint64_t* fin_xz, int* fin_e) {
     const int b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= batch) return;
     uint64_t F = 0, G = 0;
     int E = 0;
     for (int s = 0; s < count; ++s) {
-        uint64_t* fr = frames + 2 * ((uint64_t)s * batch + b);
+        const uint64_t i = (uint64_t)s * batch + b;
+        uint64_t* fr = frames + 2 * i;
+        const uint64_t x = fr[0], z = fr[1];
         fr[0] = F;
         fr[1] = G;
-        uint64_t x, z;
-        int e;
-        draw_step(ch, nch, seed, step0 + (uint64_t)s, b, x, z, e);
-        E += e + ((__popcll(z & F) & 1) ? 2 : 0);
+        E += ephase[i] + ((__popcll(z & F) & 1) ? 2 : 0);
         F ^= x;
         G ^= z;
     }
@@ -175,6 +188,7 @@ struct qsim_batch {
     DevChannel* d_ch = nullptr;
     size_t ch_cap = 0;
     uint64_t* d_frames = nullptr;  // Pauli frames of the current run, [steps][batch][2]
+    int* d_fe = nullptr;           // per-(step, trajectory) draw phases (frame build scratch)
     size_t frames_cap = 0;
     DevBuf ops, stages;             // fused-plan descriptors
     PlanCache plans;
@@ -186,6 +200,7 @@ struct qsim_batch {
         if (d_e) (void)hipFree(d_e);
         if (d_ch) (void)hipFree(d_ch);
         if (d_frames) (void)hipFree(d_frames);
+        if (d_fe) (void)hipFree(d_fe);
         if (stream) (void)hipStreamDestroy(stream);
     }
 };
@@ -312,14 +327,20 @@ int qsim_batch_run(qsim_batch* b, const qsim_gate* gates, size_t count,
                 if (need_frames > b->frames_cap) {
                     QSIM_HIPCHK(hipStreamSynchronize(b->stream));
                     if (b->d_frames) QSIM_HIPCHK(hipFree(b->d_frames));
+                    if (b->d_fe) QSIM_HIPCHK(hipFree(b->d_fe));
                     b->d_frames = nullptr;
+                    b->d_fe = nullptr;
                     QSIM_HIPCHK(hipMalloc((void**)&b->d_frames, need_frames * sizeof(uint64_t)));
+                    QSIM_HIPCHK(hipMalloc((void**)&b->d_fe, need_frames / 2 * sizeof(int)));
                     b->frames_cap = need_frames;
                 }
                 TimedLaunch tl(&b->timer, "pauli_frames", 0.0, b->stream);
-                hipLaunchKernelGGL(k_frame_build, dim3((b->batch + 255) / 256), dim3(256), 0, b->stream,
-                                   b->d_ch, (int)ch.size(), b->seed, b->step, (int)count, b->batch,
-                                   b->d_frames, b->d_xz, b->d_e);
+                const uint64_t draws = (uint64_t)count * b->batch;
+                hipLaunchKernelGGL(k_draw_steps, dim3((unsigned)((draws + 255) / 256)), dim3(256), 0,
+                                   b->stream, b->d_ch, (int)ch.size(), b->seed, b->step, (int)count,
+                                   b->batch, b->d_frames, b->d_fe);
+                hipLaunchKernelGGL(k_frame_build, dim3((b->batch + 63) / 64), dim3(64), 0, b->stream,
+                                   (int)count, b->batch, b->d_frames, b->d_fe, b->d_xz, b->d_e);
                 QSIM_HIPCHK(hipGetLastError());
             }
             if (!fops.empty()) {

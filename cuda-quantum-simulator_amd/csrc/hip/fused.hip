@@ -690,7 +690,9 @@ __device__ __forceinline__ void stage_op(double2 (&v)[1 << RB], uint32_t jb, con
 // when f = F_t) then the off-diagonal signs flipped when g = G_t; a control c is satisfied when
 // the stored bit is 1 ^ F_c; a diagonal op applies d(stored bit ^ f).  Everything runs through
 // the general arms (one select per dword); F and G are uniform over a tile (one trajectory).
-template <int RB, int P>
+// REAL: all four entries real (X, H, Ry, CX and their frame conjugates) — half the FP64 work;
+// PRED: the op has controls (per-pair select), else pure arithmetic.
+template <int RB, int P, bool REAL, bool PRED>
 __device__ __forceinline__ void frame_m1(double2 (&v)[1 << RB], uint32_t jb, const TileOp& op,
                                          double2 m0, double2 m1, double2 m2, double2 m3,
                                          uint32_t pol_reg, uint32_t pol_thr) {
@@ -700,9 +702,36 @@ __device__ __forceinline__ void frame_m1(double2 (&v)[1 << RB], uint32_t jb, con
     for (int r = 0; r < (1 << RB); ++r) {
         if (r & (1 << P)) continue;
         const double2 a0 = v[r], a1 = v[r | (1 << P)];
-        const bool ok = ((((uint32_t)r ^ pol_reg) & cr) == cr) && thr_ok;
-        v[r] = sel(ok, cadd(cmul(m0, a0), cmul(m1, a1)), a0);
-        v[r | (1 << P)] = sel(ok, cadd(cmul(m2, a0), cmul(m3, a1)), a1);
+        double2 x0, x1;
+        if constexpr (REAL) {
+            x0 = make_double2(m0.x * a0.x + m1.x * a1.x, m0.x * a0.y + m1.x * a1.y);
+            x1 = make_double2(m2.x * a0.x + m3.x * a1.x, m2.x * a0.y + m3.x * a1.y);
+        } else {
+            x0 = cadd(cmul(m0, a0), cmul(m1, a1));
+            x1 = cadd(cmul(m2, a0), cmul(m3, a1));
+        }
+        if constexpr (PRED) {
+            const bool ok = ((((uint32_t)r ^ pol_reg) & cr) == cr) && thr_ok;
+            x0 = sel(ok, x0, a0);
+            x1 = sel(ok, x1, a1);
+        }
+        v[r] = x0;
+        v[r | (1 << P)] = x1;
+    }
+}
+
+template <int RB, int P>
+__device__ __forceinline__ void frame_m1_arm(double2 (&v)[1 << RB], uint32_t jb, const TileOp& op,
+                                             double2 m0, double2 m1, double2 m2, double2 m3,
+                                             uint32_t pol_reg, uint32_t pol_thr) {
+    const bool real = m0.y == 0.0 && m1.y == 0.0 && m2.y == 0.0 && m3.y == 0.0;  // uniform
+    const bool pred = (op.cm_reg | op.cm_thr) != 0;
+    if (real) {
+        if (pred) frame_m1<RB, P, true, true>(v, jb, op, m0, m1, m2, m3, pol_reg, pol_thr);
+        else frame_m1<RB, P, true, false>(v, jb, op, m0, m1, m2, m3, pol_reg, pol_thr);
+    } else {
+        if (pred) frame_m1<RB, P, false, true>(v, jb, op, m0, m1, m2, m3, pol_reg, pol_thr);
+        else frame_m1<RB, P, false, false>(v, jb, op, m0, m1, m2, m3, pol_reg, pol_thr);
     }
 }
 
@@ -747,10 +776,10 @@ __device__ __forceinline__ void stage_op_frame(double2 (&v)[1 << RB], uint32_t j
         m2 = make_double2(-m2.x, -m2.y);
     }
     switch (op.p0) {
-        case 0: frame_m1<RB, 0>(v, jb, op, m0, m1, m2, m3, pol_reg, pol_thr); break;
-        case 1: frame_m1<RB, 1>(v, jb, op, m0, m1, m2, m3, pol_reg, pol_thr); break;
-        case 2: if constexpr (RB > 2) frame_m1<RB, 2>(v, jb, op, m0, m1, m2, m3, pol_reg, pol_thr); break;
-        case 3: if constexpr (RB > 3) frame_m1<RB, 3>(v, jb, op, m0, m1, m2, m3, pol_reg, pol_thr); break;
+        case 0: frame_m1_arm<RB, 0>(v, jb, op, m0, m1, m2, m3, pol_reg, pol_thr); break;
+        case 1: frame_m1_arm<RB, 1>(v, jb, op, m0, m1, m2, m3, pol_reg, pol_thr); break;
+        case 2: if constexpr (RB > 2) frame_m1_arm<RB, 2>(v, jb, op, m0, m1, m2, m3, pol_reg, pol_thr); break;
+        case 3: if constexpr (RB > 3) frame_m1_arm<RB, 3>(v, jb, op, m0, m1, m2, m3, pol_reg, pol_thr); break;
         default: break;
     }
 }
