@@ -115,3 +115,25 @@ def test_jit_sharded_virtual(qsim, oracle, jit_inline):
     d = DistributedSimulator.virtual(n, 4)
     d.run(c)
     np.testing.assert_allclose(d.getStateVector(), ref, atol=1e-12, rtol=0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [26, 28])
+def test_full_size_paths_agree(qsim, gpu_ready, n):
+    """At BASELINE sizes (beyond the oracle): W-HC through the per-gate kernels, the pass
+    interpreter and the specialised kernels gives the same state, and the norm stays 1."""
+    from qsim_amd.plan import set_jit
+    c = qsim.createRandomHCCircuit(n, 100, 42)
+    states = []
+    try:
+        for mode, jit in ((qsim.RunMode.PerGate, 0), (qsim.RunMode.Fused, 0), (qsim.RunMode.Fused, 2)):
+            set_jit(jit, 0)
+            sim = qsim.Simulator(n, mode=mode)
+            sim.run(c)
+            assert abs(sim.state.getTotalProbability() - 1.0) < 1e-10
+            states.append(sim.getStateVector())
+            del sim
+    finally:
+        set_jit(1, 20)
+    np.testing.assert_allclose(states[1], states[0], atol=1e-12, rtol=0)
+    np.testing.assert_allclose(states[2], states[0], atol=1e-12, rtol=0)
