@@ -19,6 +19,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <string>
@@ -51,6 +52,16 @@ static int needs_local(const qsim_gate& g) {
         default:
             return -1;
     }
+}
+
+// QSIM_DIST_FULL_REMAP=0 lets a remap move only the globals that must leave (fewer bytes, fewer
+// links); the default swaps all of them (see plan_dist).
+static bool full_remap() {
+    static const bool v = [] {
+        const char* e = std::getenv("QSIM_DIST_FULL_REMAP");
+        return e == nullptr || std::atoi(e) != 0;
+    }();
+    return v;
 }
 
 static std::vector<DStep> plan_dist(const qsim_gate* gates, size_t count, int n, int g, int rank,
@@ -89,7 +100,19 @@ static std::vector<DStep> plan_dist(const qsim_gate* gates, size_t count, int n,
                 return perm[a] > perm[b];         // prefer high local positions (coalesced pack)
             });
             std::vector<char> want(n, 0);
-            for (int j = 0; j < g; ++j) want[order[j]] = 1;
+            if (full_remap()) {
+                // Swap ALL g global qubits: a k-qubit remap sends (1 - 2^-k) of the shard over
+                // 2^k - 1 xGMI links, i.e. S / 2^k per link, so k = g is the fastest remap even
+                // though it moves more bytes.  New globals: the locals used furthest ahead.
+                int taken = 0;
+                for (int j = 0; j < n && taken < g; ++j)
+                    if (perm[order[j]] < L) {
+                        want[order[j]] = 1;
+                        ++taken;
+                    }
+            } else {
+                for (int j = 0; j < g; ++j) want[order[j]] = 1;
+            }
             std::vector<int> out, in;
             for (int q = 0; q < n; ++q) {
                 if (perm[q] >= L && !want[q]) out.push_back(q);
