@@ -94,6 +94,9 @@ struct FusedPass {
     int op_begin = 0, op_end = 0;  // range in the pass-op buffer (unstaged kernel)
     int stage_begin = 0, stage_end = 0;  // range in Plan::stages (staged kernel, h >= 4)
     int hu_count = 0;      // unnormalized H butterflies in the pass: store scales by 2^(-k/2)
+    // Algorithmic HBM bytes per amplitude of the pass: min(32, sum of its gates' SURVEY §8(d)
+    // bytes) — a pass of one CNOT is charged 16, not the 32 a full read+write would move.
+    double alg_bpa = 32.0;
 };
 struct TileOp {            // an Op re-expressed in tile-index bits
     int kind, sub, b0, b1;

@@ -365,6 +365,9 @@ Plan plan_fused(const std::vector<Op>& ops, int n, int hmax) {
         FusedPass p;
         p.h = heff;
         p.r0 = r0;
+        double bpa = 0.0;
+        for (const Op& op : ch.ops) bpa += op_alg_bytes(op, 1.0);
+        p.alg_bpa = std::min(32.0, bpa);
         int k = 0;
         int bit_of[64];
         for (int q = 0; q < r0; ++q) bit_of[q] = q;
@@ -885,7 +888,7 @@ void launch_fused(double2* st, int n, uint64_t batch, const Plan& plan, const Ti
         a.log_tpt = lt;
         a.tpt_mask = (1ull << lt) - 1ull;
         const uint64_t blocks = batch << lt;
-        TimedLaunch tl(tm, "fused_tile", pass_bytes, s);
+        TimedLaunch tl(tm, "fused_tile", pass_bytes * (p.alg_bpa / 32.0), s);
         if (frames) {  // batched noisy run: general arms under the trajectory's Pauli frame
             a.frames = frames;
             a.nbatch = (int)batch;
