@@ -187,11 +187,17 @@ __device__ __forceinline__ uint64_t xlocal(const XArgs& a, uint64_t e) {
     return off;
 }
 
+// Pack (state -> send slabs) or unpack (receive slabs -> state) the offsets [lo, lo + 2^sub_log)
+// of every slab (one pipeline part of a remap); the own slab never moves.
 template <bool PACK>
-__global__ __launch_bounds__(256) void k_exchange_copy(XArgs a, uint64_t total) {
+__global__ __launch_bounds__(256) void k_exchange_copy(XArgs a, uint64_t lo, int sub_log) {
+    const uint64_t total = (uint64_t)1 << (sub_log + a.k);
+    const uint64_t sub_mask = ((uint64_t)1 << sub_log) - 1;
     const uint64_t step = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += step) {
-        if ((int)(e >> a.chunk_log) == a.my_c) continue;
+    for (uint64_t x = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; x < total; x += step) {
+        const uint64_t c = x >> sub_log;
+        if ((int)c == a.my_c) continue;
+        const uint64_t e = (c << a.chunk_log) | (lo + (x & sub_mask));
         const uint64_t i = xlocal(a, e);
         if (PACK) a.buf[e] = a.st[i];
         else a.st[i] = a.buf[e];
@@ -224,7 +230,9 @@ struct qsim_dist {
     std::vector<Shard> shards;
     double* d_partials = nullptr;
     double* d_result = nullptr;
-    hipStream_t stream = nullptr;
+    hipStream_t stream = nullptr;       // compute: passes, pack / unpack
+    hipStream_t comm_stream = nullptr;  // remap transfers (RCCL or, virtual, device copies)
+    std::vector<hipEvent_t> events;     // remap pipeline: packed part p, transferred part p
     ncclComm_t comm = nullptr;
     std::vector<int> perm;
     DevBuf ops, stages;
@@ -240,6 +248,10 @@ struct qsim_dist {
                 if (p) (void)hipFree(p);
         if (d_partials) (void)hipFree(d_partials);
         if (d_result) (void)hipFree(d_result);
+        if (comm_stream) (void)hipStreamSynchronize(comm_stream);
+        for (hipEvent_t e : events)
+            if (e) (void)hipEventDestroy(e);
+        if (comm_stream) (void)hipStreamDestroy(comm_stream);
         if (stream) (void)hipStreamDestroy(stream);
     }
 };
@@ -322,11 +334,26 @@ XPlan xplan(const qsim_dist* d, const Shard& sh, const DStep& ex) {
     }
     return x;
 }
-void copy_kernel(bool pack, XArgs a, uint64_t total, hipStream_t s) {
+void copy_kernel(bool pack, XArgs a, uint64_t lo, int sub_log, hipStream_t s) {
+    const uint64_t total = (uint64_t)1 << (sub_log + a.k);
     const unsigned blocks = (unsigned)std::min<uint64_t>((total + 255) / 256, 256 * 64);
-    if (pack) hipLaunchKernelGGL(k_exchange_copy<true>, dim3(blocks), dim3(256), 0, s, a, total);
-    else hipLaunchKernelGGL(k_exchange_copy<false>, dim3(blocks), dim3(256), 0, s, a, total);
+    if (pack) hipLaunchKernelGGL(k_exchange_copy<true>, dim3(blocks), dim3(256), 0, s, a, lo, sub_log);
+    else hipLaunchKernelGGL(k_exchange_copy<false>, dim3(blocks), dim3(256), 0, s, a, lo, sub_log);
     QSIM_HIPCHK(hipGetLastError());
+}
+// Pipeline parts of a remap (QSIM_DIST_PIPELINE, default 4): slab offsets are split into parts
+// so that part p's transfer overlaps the packing of later parts and the unpacking of earlier
+// ones (pack and unpack run on the compute stream, transfers on the comm stream, ordered by
+// events).  Parts below 1 MiB of amplitudes are not split further.
+static int pipeline_parts(uint64_t chunk) {
+    static const int want = [] {
+        const char* e = std::getenv("QSIM_DIST_PIPELINE");
+        const int v = e ? std::atoi(e) : 4;
+        return v < 1 ? 1 : (v > 16 ? 16 : v);
+    }();
+    int parts = 1;
+    while (parts * 2 <= want && (chunk / (uint64_t)(parts * 2)) >= (1ull << 16)) parts *= 2;
+    return parts;
 }
 // Qubit remap: rank r sends its amplitudes with local bits lpos == c to the rank whose bits at
 // gpos are c, and stores what that rank sends at local bits == c (the swap of the two qubit
@@ -337,40 +364,63 @@ void exchange(qsim_dist* d, const DStep& ex) {
     const uint64_t chunk = total >> ex.k;
     const double bytes = 2.0 * 16.0 * (double)(total - chunk) * (double)d->shards.size();
     TimedLaunch tl(&d->timer, "alltoall_remap", bytes, d->stream);
-    std::vector<XPlan> xs;
-    for (Shard& sh : d->shards) {
-        xs.push_back(xplan(d, sh, ex));
-        XArgs a = xs.back().a;
-        a.buf = sh.sendbuf;
-        copy_kernel(true, a, total, d->stream);
+    const int parts = pipeline_parts(chunk);
+    int sub_log = d->L - ex.k;
+    for (int p = parts; p > 1; p >>= 1) --sub_log;
+    const uint64_t sub = 1ull << sub_log;
+    if ((int)d->events.size() < 2 * parts) {
+        const size_t have = d->events.size();
+        d->events.resize(2 * parts, nullptr);
+        for (size_t i = have; i < d->events.size(); ++i)
+            QSIM_HIPCHK(hipEventCreateWithFlags(&d->events[i], hipEventDisableTiming));
     }
-    if (!d->virt) {
-        const Shard& sh = d->shards[0];
-        const XPlan& x = xs[0];
-        QSIM_NCCLCHK(ncclGroupStart());
-        for (int c = 0; c < (1 << ex.k); ++c) {
-            if (c == x.a.my_c) continue;
-            const size_t cnt = (size_t)chunk * 2;
-            QSIM_NCCLCHK(ncclSend(sh.sendbuf + (uint64_t)c * chunk, cnt, ncclDouble, x.peer_of[c], d->comm, d->stream));
-            QSIM_NCCLCHK(ncclRecv(sh.recvbuf + (uint64_t)c * chunk, cnt, ncclDouble, x.peer_of[c], d->comm, d->stream));
-        }
-        QSIM_NCCLCHK(ncclGroupEnd());
-    } else {  // shard r's chunk c goes to shard peer(c), into that shard's slot my_c(r)
+    std::vector<XPlan> xs;
+    for (Shard& sh : d->shards) xs.push_back(xplan(d, sh, ex));
+    for (int p = 0; p < parts; ++p) {
         for (size_t i = 0; i < d->shards.size(); ++i) {
-            const XPlan& x = xs[i];
+            XArgs a = xs[i].a;
+            a.buf = d->shards[i].sendbuf;
+            copy_kernel(true, a, (uint64_t)p * sub, sub_log, d->stream);
+        }
+        QSIM_HIPCHK(hipEventRecord(d->events[p], d->stream));
+    }
+    for (int p = 0; p < parts; ++p) {
+        const uint64_t off = (uint64_t)p * sub;
+        QSIM_HIPCHK(hipStreamWaitEvent(d->comm_stream, d->events[p], 0));
+        if (!d->virt) {
+            const Shard& sh = d->shards[0];
+            const XPlan& x = xs[0];
+            QSIM_NCCLCHK(ncclGroupStart());
             for (int c = 0; c < (1 << ex.k); ++c) {
                 if (c == x.a.my_c) continue;
-                Shard& dst = d->shards[x.peer_of[c]];
-                QSIM_HIPCHK(hipMemcpyAsync(dst.recvbuf + (uint64_t)x.a.my_c * chunk,
-                                           d->shards[i].sendbuf + (uint64_t)c * chunk,
-                                           chunk * sizeof(double2), hipMemcpyDeviceToDevice, d->stream));
+                const size_t cnt = (size_t)sub * 2;
+                const uint64_t at = (uint64_t)c * chunk + off;
+                QSIM_NCCLCHK(ncclSend(sh.sendbuf + at, cnt, ncclDouble, x.peer_of[c], d->comm, d->comm_stream));
+                QSIM_NCCLCHK(ncclRecv(sh.recvbuf + at, cnt, ncclDouble, x.peer_of[c], d->comm, d->comm_stream));
+            }
+            QSIM_NCCLCHK(ncclGroupEnd());
+        } else {  // shard r's slab c goes to shard peer(c), into that shard's slot my_c(r)
+            for (size_t i = 0; i < d->shards.size(); ++i) {
+                const XPlan& x = xs[i];
+                for (int c = 0; c < (1 << ex.k); ++c) {
+                    if (c == x.a.my_c) continue;
+                    Shard& dst = d->shards[x.peer_of[c]];
+                    QSIM_HIPCHK(hipMemcpyAsync(dst.recvbuf + (uint64_t)x.a.my_c * chunk + off,
+                                               d->shards[i].sendbuf + (uint64_t)c * chunk + off,
+                                               sub * sizeof(double2), hipMemcpyDeviceToDevice,
+                                               d->comm_stream));
+                }
             }
         }
+        QSIM_HIPCHK(hipEventRecord(d->events[parts + p], d->comm_stream));
     }
-    for (size_t i = 0; i < d->shards.size(); ++i) {
-        XArgs a = xs[i].a;
-        a.buf = d->shards[i].recvbuf;
-        copy_kernel(false, a, total, d->stream);
+    for (int p = 0; p < parts; ++p) {
+        QSIM_HIPCHK(hipStreamWaitEvent(d->stream, d->events[parts + p], 0));
+        for (size_t i = 0; i < d->shards.size(); ++i) {
+            XArgs a = xs[i].a;
+            a.buf = d->shards[i].recvbuf;
+            copy_kernel(false, a, (uint64_t)p * sub, sub_log, d->stream);
+        }
     }
 }
 double allreduce_sum(qsim_dist* d, double local) {
@@ -428,6 +478,7 @@ int qsim_dist_create(int n_qubits, int rank, int world, const void* unique_id, i
         d->perm.resize(n_qubits);
         QSIM_HIPCHK(hipSetDevice(device));
         QSIM_HIPCHK(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
+        QSIM_HIPCHK(hipStreamCreateWithFlags(&d->comm_stream, hipStreamNonBlocking));
         d->timer.stream = d->stream;
         alloc_shards(d.get(), {rank});
         ncclUniqueId id;
@@ -454,6 +505,7 @@ int qsim_dist_create_virtual(int n_qubits, int world, int device, qsim_dist** ou
         d->perm.resize(n_qubits);
         QSIM_HIPCHK(hipSetDevice(device));
         QSIM_HIPCHK(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
+        QSIM_HIPCHK(hipStreamCreateWithFlags(&d->comm_stream, hipStreamNonBlocking));
         d->timer.stream = d->stream;
         std::vector<int> ranks(world);
         for (int r = 0; r < world; ++r) ranks[r] = r;

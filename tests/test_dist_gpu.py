@@ -59,6 +59,22 @@ def test_virtual_ranks_run_twice_and_reset(qsim, oracle, gpu_ready):
     assert abs(s[0] - 1) < 1e-15 and np.all(np.abs(s[1:]) == 0)
 
 
+@pytest.mark.parametrize("world,n", [(4, 22), (8, 23), (2, 21)])
+def test_virtual_pipelined_remaps_match_single_gpu(qsim, gpu_ready, world, n):
+    """Shards large enough that every remap is split into pipeline parts (transfers on the comm
+    stream, packs/unpacks on the compute stream, event-ordered); three runs so the qubit map
+    moves through several layouts.  Beyond the oracle's size the reference is the single-GPU
+    engine."""
+    from qsim_amd.dist import DistributedSimulator
+    c = qsim.createRandomHCCircuit(n, 100, 7)
+    d = DistributedSimulator.virtual(n, world)
+    s = qsim.Simulator(n)
+    for _ in range(3):
+        d.run(c)
+        s.run(c)
+    np.testing.assert_allclose(d.getStateVector(), s.getStateVector(), atol=1e-12, rtol=0)
+
+
 def test_single_rank_rccl_path(qsim, oracle, gpu_ready):
     from qsim_amd.dist import DistributedSimulator
     n = 14
