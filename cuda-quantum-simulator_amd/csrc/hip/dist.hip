@@ -64,6 +64,119 @@ static bool full_remap() {
     return v;
 }
 
+static uint64_t gate_qmask(const qsim_gate& g) {
+    uint64_t m = 0;
+    for (int j = 0; j < g.nqubits; ++j) m |= 1ull << g.qubits[j];
+    return m;
+}
+
+// Gates of `window` (indices into `gates`, in program order) that can run before any further
+// remap when the logical qubits in `glob` are global: a gate runs unless its target is global or
+// an earlier gate that shares a qubit with it could not run.  SWAPs relabel `glob`.
+static int count_runnable(const qsim_gate* gates, const std::vector<uint64_t>& qm,
+                          const std::vector<int>& window, size_t upto, uint64_t glob) {
+    uint64_t blocked = 0;
+    int cnt = 0;
+    for (size_t w = 0; w < upto; ++w) {
+        const int i = window[w];
+        const qsim_gate& gt = gates[i];
+        if (qm[i] & blocked) {
+            blocked |= qm[i];
+            continue;
+        }
+        if (gt.type == QSIM_GATE_SWAP) {
+            const uint64_t a = 1ull << gt.qubits[0], b = 1ull << gt.qubits[1];
+            if (((glob & a) != 0) != ((glob & b) != 0)) glob ^= a | b;
+            continue;
+        }
+        const int tq = needs_local(gt);
+        if (tq >= 0 && ((glob >> tq) & 1ull)) {
+            blocked |= qm[i];
+            continue;
+        }
+        ++cnt;
+    }
+    return cnt;
+}
+
+// The logical qubits to make global at a remap.  Scored, in order, by the gates that can then run
+// before the next remap (i) in the rest of this circuit and (ii) over the rest plus one more run
+// of the circuit (a benchmark or trajectory loop re-runs it from the map this run ends with), then
+// by the physical positions of the incoming qubits (high positions give long pack runs).
+// Exhaustive over the candidate g-sets when that is cheap (C(27,3) = 2925 at 30 qubits on 8
+// ranks), greedy one qubit at a time otherwise.
+static uint64_t choose_globals(const qsim_gate* gates, size_t count, const std::vector<uint64_t>& qm,
+                               const std::vector<char>& done, const std::vector<int>& perm, int n,
+                               int g, int L, bool full) {
+    std::vector<int> window;
+    for (size_t i = 0; i < count; ++i)
+        if (!done[i]) window.push_back((int)i);
+    const size_t rest = window.size();
+    const size_t cap = std::max<size_t>(rest, 1024);
+    for (size_t i = 0; i < count && window.size() < cap; ++i) window.push_back((int)i);
+    std::vector<int> cand;  // full remap: every current global leaves, so only locals may enter
+    for (int q = 0; q < n; ++q)
+        if (!full || perm[q] < L) cand.push_back(q);
+    struct Score {
+        int a = -1, b = -1, c = -1;
+        bool operator<(const Score& o) const {
+            return a != o.a ? a < o.a : (b != o.b ? b < o.b : c < o.c);
+        }
+    };
+    auto score = [&](uint64_t set) {
+        Score s;
+        s.a = count_runnable(gates, qm, window, rest, set);
+        s.b = count_runnable(gates, qm, window, window.size(), set);
+        s.c = 0;
+        for (int q = 0; q < n; ++q)
+            if ((set >> q) & 1ull) s.c += perm[q];
+        return s;
+    };
+    const int m = (int)cand.size();
+    double combos = 1.0;
+    for (int j = 0; j < g; ++j) combos = combos * (m - j) / (j + 1);
+    uint64_t best_set = 0;
+    Score best;
+    if (combos <= 20000.0) {
+        std::vector<int> idx(g);
+        for (int j = 0; j < g; ++j) idx[j] = j;
+        for (;;) {
+            uint64_t set = 0;
+            for (int j = 0; j < g; ++j) set |= 1ull << cand[idx[j]];
+            const Score s = score(set);
+            if (best < s) {
+                best = s;
+                best_set = set;
+            }
+            int j = g - 1;
+            while (j >= 0 && idx[j] == m - g + j) --j;
+            if (j < 0) break;
+            ++idx[j];
+            for (int k = j + 1; k < g; ++k) idx[k] = idx[k - 1] + 1;
+        }
+    } else {
+        for (int j = 0; j < g; ++j) {
+            uint64_t pick = 0;
+            Score bj;
+            for (int q : cand) {
+                if ((best_set >> q) & 1ull) continue;
+                const Score s = score(best_set | (1ull << q));
+                if (bj < s) {
+                    bj = s;
+                    pick = 1ull << q;
+                }
+            }
+            best_set |= pick;
+        }
+    }
+    return best_set;
+}
+
+// Host plan of one run for one rank.  Gates are reordered only past gates on disjoint qubits
+// (exact).  Each sweep in program order runs every gate whose target is local and whose earlier
+// qubit-sharing gates have all run; when a sweep leaves gates, one remap brings in the targets
+// (choose_globals) and the next sweep continues.  W-HC at 30 qubits on 8 ranks needs one remap
+// per run this way (two in plain program order).
 static std::vector<DStep> plan_dist(const qsim_gate* gates, size_t count, int n, int g, int rank,
                                     std::vector<int>& perm) {
     const int L = n - g;
@@ -75,59 +188,13 @@ static std::vector<DStep> plan_dist(const qsim_gate* gates, size_t count, int n,
         cur = DStep();
     };
     for (size_t i = 0; i < count; ++i) validate_gate(gates[i], n);
-    for (size_t i = 0; i < count; ++i) {
+    std::vector<uint64_t> qm(count);
+    for (size_t i = 0; i < count; ++i) qm[i] = gate_qmask(gates[i]);
+    auto emit = [&](size_t i) {
         const qsim_gate& gt = gates[i];
         if (gt.type == QSIM_GATE_SWAP) {  // relabel only
             std::swap(perm[gt.qubits[0]], perm[gt.qubits[1]]);
-            continue;
-        }
-        const int tq = needs_local(gt);
-        if (tq >= 0 && perm[tq] >= L) {
-            flush();
-            // desired global set: the g logical qubits whose next target use is furthest away
-            const size_t INF = count + 1;
-            std::vector<size_t> next(n, INF);
-            for (size_t j = count; j-- > i;) {
-                const int q = needs_local(gates[j]);
-                if (q >= 0) next[q] = j;
-            }
-            std::vector<int> order(n);
-            for (int q = 0; q < n; ++q) order[q] = q;
-            std::stable_sort(order.begin(), order.end(), [&](int a, int b) {
-                if (next[a] != next[b]) return next[a] > next[b];
-                const bool ga = perm[a] >= L, gb = perm[b] >= L;
-                if (ga != gb) return ga;          // keep current globals (no movement)
-                return perm[a] > perm[b];         // prefer high local positions (coalesced pack)
-            });
-            std::vector<char> want(n, 0);
-            if (full_remap()) {
-                // Swap ALL g global qubits: a k-qubit remap sends (1 - 2^-k) of the shard over
-                // 2^k - 1 xGMI links, i.e. S / 2^k per link, so k = g is the fastest remap even
-                // though it moves more bytes.  New globals: the locals used furthest ahead.
-                int taken = 0;
-                for (int j = 0; j < n && taken < g; ++j)
-                    if (perm[order[j]] < L) {
-                        want[order[j]] = 1;
-                        ++taken;
-                    }
-            } else {
-                for (int j = 0; j < g; ++j) want[order[j]] = 1;
-            }
-            std::vector<int> out, in;
-            for (int q = 0; q < n; ++q) {
-                if (perm[q] >= L && !want[q]) out.push_back(q);
-                if (perm[q] < L && want[q]) in.push_back(q);
-            }
-            DStep ex;
-            ex.kind = 1;
-            ex.k = (int)out.size();
-            for (int j = 0; j < ex.k; ++j) {
-                ex.gpos[j] = perm[out[j]];
-                ex.lpos[j] = perm[in[j]];
-                perm[out[j]] = ex.lpos[j];
-                perm[in[j]] = ex.gpos[j];
-            }
-            steps.push_back(ex);
+            return;
         }
         qsim_gate pg = gt;
         for (int j = 0; j < gt.nqubits; ++j) pg.qubits[j] = perm[gt.qubits[j]];
@@ -139,10 +206,10 @@ static std::vector<DStep> plan_dist(const qsim_gate* gates, size_t count, int n,
                 if (!rank_bit(c)) skip = true;
                 op.cmask &= ~(1ull << c);
             }
-        if (skip) continue;
+        if (skip) return;
         if (op.kind == K_DIAG && op.t0 >= L) {
             const int b = rank_bit(op.t0);
-            if (!b && op.d0_one) continue;  // factor 1 on this rank
+            if (!b && op.d0_one) return;  // factor 1 on this rank
             const double fr = b ? op.m[2] : op.m[0], fi = b ? op.m[3] : op.m[1];
             int t = 0;
             while (t < L - 1 && ((op.cmask >> t) & 1ull)) ++t;
@@ -155,6 +222,48 @@ static std::vector<DStep> plan_dist(const qsim_gate* gates, size_t count, int n,
         if (op.t0 >= L || (op.kind == K_SWAP && op.t1 >= L))
             fail(QSIM_ERR_RUNTIME, "distributed planner left a global target");
         cur.ops.push_back(op);
+    };
+    std::vector<char> done(count, 0);
+    size_t left = count;
+    for (;;) {
+        uint64_t blocked = 0;
+        for (size_t i = 0; i < count; ++i) {
+            if (done[i]) continue;
+            if (qm[i] & blocked) {
+                blocked |= qm[i];
+                continue;
+            }
+            const int tq = needs_local(gates[i]);
+            if (tq >= 0 && perm[tq] >= L) {
+                blocked |= qm[i];
+                continue;
+            }
+            emit(i);
+            done[i] = 1;
+            --left;
+        }
+        if (left == 0) break;
+        flush();
+        const bool full = full_remap();
+        const uint64_t want = choose_globals(gates, count, qm, done, perm, n, g, L, full);
+        std::vector<int> out, in;
+        for (int q = 0; q < n; ++q) {
+            const bool w = (want >> q) & 1ull;
+            if (perm[q] >= L && !w) out.push_back(q);
+            if (perm[q] < L && w) in.push_back(q);
+        }
+        if (out.empty() || out.size() != in.size())
+            fail(QSIM_ERR_RUNTIME, "distributed planner: no remap makes progress");
+        DStep ex;
+        ex.kind = 1;
+        ex.k = (int)out.size();
+        for (int j = 0; j < ex.k; ++j) {
+            ex.gpos[j] = perm[out[j]];
+            ex.lpos[j] = perm[in[j]];
+            perm[out[j]] = ex.lpos[j];
+            perm[in[j]] = ex.gpos[j];
+        }
+        steps.push_back(ex);
     }
     flush();
     return steps;
@@ -236,8 +345,17 @@ struct qsim_dist {
     ncclComm_t comm = nullptr;
     std::vector<int> perm;
     DevBuf ops, stages;
-    std::vector<PlanCache> fplans;  // one per local segment of a run, in execution order
-    size_t plan_calls = 0;
+    // Plans of recent runs, keyed by (gate list, map at the start of the run): a repeated circuit
+    // alternates between a few start maps, each with its own segment plans and compiled kernels.
+    struct RunPlan {
+        std::vector<qsim_gate> gates;
+        std::vector<int> perm_in, perm_out;
+        std::vector<std::vector<DStep>> steps;              // per shard
+        std::vector<std::unique_ptr<PlanCache>> fplans;     // per (shard, local segment)
+        uint64_t used = 0;
+    };
+    std::vector<std::unique_ptr<RunPlan>> run_plans;
+    uint64_t run_clock = 0;
     Timer timer;
     ~qsim_dist() {
         (void)hipSetDevice(device);
@@ -432,10 +550,8 @@ double allreduce_sum(qsim_dist* d, double local) {
     QSIM_HIPCHK(hipStreamSynchronize(d->stream));
     return out;
 }
-void run_local(qsim_dist* d, Shard& sh, const std::vector<Op>& ops, int flags) {
+void run_local(qsim_dist* d, Shard& sh, const std::vector<Op>& ops, int flags, PlanCache& pc) {
     if (flags & QSIM_RUN_FUSED) {
-        if (d->plan_calls >= d->fplans.size()) d->fplans.resize(d->plan_calls + 1);
-        PlanCache& pc = d->fplans[d->plan_calls++];
         const Plan& plan = pc.get(ops, d->L);
         const JitModule* jm = jit_for(pc.jit, plan, d->L);
         d->ops.upload(plan.ops.data(), plan.ops.size() * sizeof(TileOp), d->stream);
@@ -445,6 +561,34 @@ void run_local(qsim_dist* d, Shard& sh, const std::vector<Op>& ops, int flags) {
     } else {
         for (const Op& op : ops) launch_op(sh.d, d->L, 1, op, d->stream, &d->timer);
     }
+}
+// The cached plan of this run (same gates, same start map), or a new one (LRU of 8).
+qsim_dist::RunPlan& run_plan(qsim_dist* d, const qsim_gate* gates, size_t count) {
+    for (auto& rp : d->run_plans)
+        if (rp->perm_in == d->perm && rp->gates.size() == count &&
+            (count == 0 || std::memcmp(rp->gates.data(), gates, count * sizeof(qsim_gate)) == 0)) {
+            rp->used = ++d->run_clock;
+            return *rp;
+        }
+    auto rp = std::make_unique<qsim_dist::RunPlan>();
+    rp->gates.assign(gates, gates + count);
+    rp->perm_in = d->perm;
+    // Plan per shard (ranks differ only in which global controls/phases apply).
+    for (const Shard& sh : d->shards) {
+        std::vector<int> perm = d->perm;
+        rp->steps.push_back(plan_dist(gates, count, d->n, d->g, sh.rank, perm));
+        rp->perm_out = perm;
+        for (const DStep& s : rp->steps.back())
+            if (s.kind == 0) rp->fplans.push_back(std::make_unique<PlanCache>());
+    }
+    rp->used = ++d->run_clock;
+    if (d->run_plans.size() >= 8) {
+        auto lru = std::min_element(d->run_plans.begin(), d->run_plans.end(),
+                                    [](const auto& a, const auto& b) { return a->used < b->used; });
+        d->run_plans.erase(lru);
+    }
+    d->run_plans.push_back(std::move(rp));
+    return *d->run_plans.back();
 }
 }  // namespace
 
@@ -532,35 +676,25 @@ int qsim_dist_run(qsim_dist* d, const qsim_gate* gates, size_t count, int flags)
         need(d);
         if (!gates && count) fail(QSIM_ERR_INVALID_ARGUMENT, "null gate list");
         QSIM_HIPCHK(hipSetDevice(d->device));
-        d->plan_calls = 0;
-        // Plan per shard (ranks differ only in which global controls/phases apply).
-        std::vector<std::vector<DStep>> plans;
-        std::vector<int> perm_after;
-        for (const Shard& sh : d->shards) {
-            std::vector<int> perm = d->perm;
-            plans.push_back(plan_dist(gates, count, d->n, d->g, sh.rank, perm));
-            perm_after = perm;
-        }
+        qsim_dist::RunPlan& rp = run_plan(d, gates, count);
+        const auto& plans = rp.steps;
+        size_t fp = 0;
         // Every rank's plan has the same exchange skeleton: walk the steps in lockstep.
         std::vector<size_t> pos(d->shards.size(), 0);
         for (;;) {
-            bool any = false;
             for (size_t i = 0; i < d->shards.size(); ++i)  // local ops up to the next exchange
                 while (pos[i] < plans[i].size() && plans[i][pos[i]].kind == 0) {
-                    run_local(d, d->shards[i], plans[i][pos[i]].ops, flags);
+                    run_local(d, d->shards[i], plans[i][pos[i]].ops, flags, *rp.fplans[fp++]);
                     ++pos[i];
-                    any = true;
                 }
-            bool ex = pos[0] < plans[0].size();
+            const bool ex = pos[0] < plans[0].size();
             for (size_t i = 1; i < d->shards.size(); ++i)
                 if ((pos[i] < plans[i].size()) != ex) fail(QSIM_ERR_RUNTIME, "exchange skeleton mismatch");
             if (!ex) break;
             exchange(d, plans[0][pos[0]]);
             for (size_t i = 0; i < d->shards.size(); ++i) ++pos[i];
-            any = true;
-            if (!any) break;
         }
-        d->perm = perm_after;
+        d->perm = rp.perm_out;
     });
 }
 

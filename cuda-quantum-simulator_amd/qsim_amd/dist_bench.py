@@ -38,10 +38,16 @@ def run(args, metric: str, peak_gbps: float) -> None:
     jit = getattr(args, "jit", 2)
     from .plan import set_jit
     set_jit(jit, -1)
-    # the qubit map reaches its fixed point within two runs, so three warmups see (and, with the
-    # JIT on, compile) the plans every timed run uses
-    for _ in range(max(3, args.warmup) if jit else args.warmup):
+    # Each run starts from the qubit map the previous one ended with; the maps soon cycle (the
+    # remap planner is deterministic).  Warm up until the start map repeats, so every plan (and,
+    # with the JIT on, every compiled pass kernel) the timed runs use has been seen.
+    seen = {tuple(sim.perm())}
+    for i in range(max(12, args.warmup)):
         sim.run(circuit, fused=fused)
+        p = tuple(sim.perm())
+        if i + 1 >= args.warmup and p in seen:
+            break
+        seen.add(p)
     sim.synchronize()
     sim.profile(True)
     dist.barrier()
