@@ -200,6 +200,7 @@ static void plan_stages(std::vector<TileOp>& pass_ops, std::vector<int>& pass_sr
 // per-gate step for a gate wider than the tile.
 struct PassChoice {
     bool single = false;
+    int r0 = 6;         // run width of this pass
     uint64_t hi = 0;
     std::vector<Op> ops;
 };
@@ -289,6 +290,129 @@ static std::vector<PassChoice> choose_passes(const std::vector<Op>& ops, int n, 
     return out;
 }
 
+// Beam search over pass sequences (n >= QSIM_PLAN_BEAM_MIN_QUBITS, staged tiles).  A search
+// state is the list of gates not yet run; a step is one tile pass, described by its run width r0
+// (4..6, chosen per pass) and its 12 - r0 free tile qubits.  Each state proposes its best
+// `width` tiles per r0 — grown one qubit at a time from the first remaining gate's qubits, keeping
+// the `width` best partial sets, scored by the gates the tile admits (then by the gates it
+// partly covers, so a 2-qubit gate's first qubit already counts) — and the `width` states with
+// the fewest remaining gates survive each step.  The first state to run out of gates gives the
+// plan.  W-HC 30q: 7 passes (one-tile-at-a-time lookahead) -> 5.
+static std::vector<PassChoice> beam_passes(const std::vector<Op>& ops, int n, int heff, int width) {
+    const size_t window = 512;
+    std::vector<uint64_t> qm(ops.size());
+    for (size_t i = 0; i < ops.size(); ++i) qm[i] = op_qubits(ops[i]);
+    auto run_mask = [](int r0) { return (1ull << r0) - 1ull; };
+    // (admitted, partly covered) over the first `window` remaining gates
+    auto score = [&](const std::vector<int>& rem, uint64_t allowed, uint64_t low) {
+        uint64_t blocked = 0;
+        int full = 0, part = 0;
+        const size_t m = std::min(rem.size(), window);
+        for (size_t i = 0; i < m; ++i) {
+            const uint64_t q = qm[rem[i]];
+            if (q & blocked) {
+                blocked |= q;
+            } else if ((q & ~allowed) == 0) {
+                ++full;
+            } else {
+                if (q & allowed & ~low) ++part;
+                blocked |= q;
+            }
+        }
+        return full * 4096 + part;
+    };
+    auto apply = [&](const std::vector<int>& rem, uint64_t allowed) {
+        std::vector<int> out;
+        uint64_t blocked = 0;
+        for (int i : rem) {
+            const uint64_t q = qm[i];
+            if ((q & blocked) == 0 && (q & ~allowed) == 0) continue;
+            out.push_back(i);
+            blocked |= q;
+        }
+        return out;
+    };
+    struct St {
+        std::vector<int> rem;
+        std::vector<std::pair<int, uint64_t>> hist;  // (r0, free tile qubits) per pass
+    };
+    std::vector<St> states(1);
+    states[0].rem.resize(ops.size());
+    for (size_t i = 0; i < ops.size(); ++i) states[0].rem[i] = (int)i;
+    for (int guard = 0; guard <= (int)ops.size(); ++guard) {
+        for (const St& s : states)
+            if (s.rem.empty()) {
+                std::vector<PassChoice> out;
+                std::vector<Op> rest = ops;
+                for (const auto& h : s.hist) {
+                    PassChoice c;
+                    c.r0 = h.first;
+                    c.hi = h.second;
+                    const uint64_t allowed = run_mask(h.first) | h.second;
+                    std::vector<Op> deferred;
+                    uint64_t blocked = 0;
+                    for (const Op& op : rest) {
+                        const uint64_t q = op_qubits(op);
+                        if ((q & blocked) == 0 && (q & ~allowed) == 0) {
+                            c.ops.push_back(op);
+                        } else {
+                            deferred.push_back(op);
+                            blocked |= q;
+                        }
+                    }
+                    rest.swap(deferred);
+                    out.push_back(std::move(c));
+                }
+                return out;
+            }
+        std::vector<St> next;
+        std::vector<std::vector<int>> seen;
+        for (const St& s : states) {
+            for (int r0 = 6; r0 >= 4; --r0) {
+                const uint64_t low = run_mask(r0);
+                const int nfree = 6 + heff - r0;
+                const uint64_t seed = qm[s.rem.front()] & ~low;
+                if (__builtin_popcountll(seed) > nfree) continue;
+                std::vector<std::pair<int, uint64_t>> part = {{score(s.rem, low | seed, low), seed}};
+                for (int k = __builtin_popcountll(seed); k < nfree; ++k) {
+                    std::vector<std::pair<int, uint64_t>> grown;
+                    for (const auto& pp : part)
+                        for (int q = r0; q < n; ++q) {
+                            if ((pp.second >> q) & 1ull) continue;
+                            const uint64_t h = pp.second | (1ull << q);
+                            bool dup = false;
+                            for (const auto& g2 : grown) dup = dup || g2.second == h;
+                            if (!dup) grown.push_back({score(s.rem, low | h, low), h});
+                        }
+                    if (grown.empty()) break;
+                    std::stable_sort(grown.begin(), grown.end(),
+                                     [](const auto& a, const auto& b) { return a.first > b.first; });
+                    if ((int)grown.size() > width) grown.resize(width);
+                    part.swap(grown);
+                }
+                for (const auto& pp : part) {
+                    St t;
+                    t.rem = apply(s.rem, low | pp.second);
+                    if (t.rem.size() == s.rem.size()) continue;
+                    bool dup = false;
+                    for (const auto& v : seen) dup = dup || v == t.rem;
+                    if (dup) continue;
+                    seen.push_back(t.rem);
+                    t.hist = s.hist;
+                    t.hist.push_back({r0, pp.second});
+                    next.push_back(std::move(t));
+                }
+            }
+        }
+        if (next.empty()) break;
+        std::stable_sort(next.begin(), next.end(),
+                         [](const St& a, const St& b) { return a.rem.size() < b.rem.size(); });
+        if ((int)next.size() > width) next.resize(width);
+        states.swap(next);
+    }
+    return {};  // (no progress possible: the caller keeps its other candidates)
+}
+
 static bool same_op(const Op& a, const Op& b) {
     if (a.kind != b.kind || a.sub != b.sub || a.t0 != b.t0 || a.t1 != b.t1 || a.cmask != b.cmask ||
         a.d0_one != b.d0_one || a.src != b.src)
@@ -340,25 +464,30 @@ Plan plan_fused(const std::vector<Op>& ops, int n, int hmax) {
     static const int r0_pin = env_int("QSIM_TILE_R0", 0);
     static const int strat_pin = env_int("QSIM_PLANNER", -1);
     std::vector<PassChoice> best;
-    int best_r0 = 6;
     for (int r0 = 6; r0 >= (heff >= 4 ? 4 : 6); --r0) {
         if (r0_pin && heff >= 4 && r0 != std::min(6, std::max(4, r0_pin))) continue;
         for (int la = 0; la <= (heff >= 4 ? 1 : 0); ++la) {
             if (strat_pin >= 0 && heff >= 4 && la != (strat_pin ? 1 : 0)) continue;
             std::vector<PassChoice> c = choose_passes(ops, n, r0, 6 + heff - r0, la != 0);
-            if (best.empty() || c.size() < best.size()) {
-                best.swap(c);
-                best_r0 = r0;
-            }
+            for (PassChoice& ch : c) ch.r0 = r0;
+            if (best.empty() || c.size() < best.size()) best.swap(c);
         }
     }
-    const int r0 = best_r0;
-    const int nfree = 6 + heff - r0;
+    static const int beam = env_int("QSIM_PLAN_BEAM", 32);
+    static const int beam_min_q = env_int("QSIM_PLAN_BEAM_MIN_QUBITS", 20);
+    if (beam > 0 && heff >= 4 && n >= beam_min_q && !r0_pin && strat_pin < 0 && best.size() > 1) {
+        // width shrinks with the circuit so the search stays ~O(10^8) simple steps
+        const int w = std::max(2, std::min(beam, (int)(32.0 * 256.0 / std::max<size_t>(256, ops.size()))));
+        std::vector<PassChoice> c = beam_passes(ops, n, heff, w);
+        if (!c.empty() && c.size() < best.size()) best.swap(c);
+    }
     for (PassChoice& ch : best) {
         if (ch.single) {
             add_single(ch.ops.front());
             continue;
         }
+        const int r0 = ch.r0;
+        const int nfree = 6 + heff - r0;
         uint64_t hi = ch.hi;
         // Pad the tile to nfree chosen qubits (uniform tile size / occupancy).
         for (int q = r0; q < n && __builtin_popcountll(hi) < nfree; ++q) hi |= 1ull << q;

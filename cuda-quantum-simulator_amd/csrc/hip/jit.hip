@@ -211,6 +211,13 @@ std::string jb_expr(const Stage& st, int rb) {
     return e;
 }
 
+// QSIM_JIT_XCD=1: consecutive workgroups (dispatched round-robin over the 8 XCDs) take tiles
+// 1/8 of the state apart, so each XCD streams one contiguous eighth.
+bool jit_xcd() {
+    static const bool v = env_or("QSIM_JIT_XCD", 0) != 0;
+    return v;
+}
+
 void gen_pass(std::ostringstream& out, const Plan& plan, const FusedPass& p, int idx) {
     const int H = p.h, RB = H - 2, R = 1 << RB, T = 64 << H;
     const int r0 = p.r0, nh = 6 + H - r0;
@@ -224,7 +231,9 @@ void gen_pass(std::ostringstream& out, const Plan& plan, const FusedPass& p, int
       << "  __shared__ double2 tile[" << T << "];\n"
       << "  char* const lds = reinterpret_cast<char*>(tile);\n"
       << "  const unsigned tid = threadIdx.x;\n"
-      << "  const unsigned long long tile_id = blockIdx.x;\n"
+      << (jit_xcd() ? "  const unsigned long long tile_id = (gridDim.x & 7u) ? blockIdx.x : "
+                      "(unsigned long long)(blockIdx.x & 7u) * (gridDim.x >> 3) + (blockIdx.x >> 3);\n"
+                    : "  const unsigned long long tile_id = blockIdx.x;\n")
       << "  unsigned long long k = (tile_id & tpt_mask) << " << r0 << ";\n";
     for (int i = 0; i < nh; ++i)
         o << "  { const unsigned long long lo = k & " << hexu((1ull << p.hpos[i]) - 1ull)

@@ -133,9 +133,10 @@ def test_planner_reordering_preserves_circuit(qsim, oracle, n, depth, seed, hmax
 
 def test_plan_pass_counts_for_bench_workload(qsim):
     from qsim_amd.plan import plan_fused
-    for n in (20, 28, 30):
+    # beam-searched pass sequences (QSIM_PLAN_BEAM): W-HC 100 gates in 5-6 HBM passes
+    for n, most in ((20, 8), (28, 6), (30, 5)):
         _, _, npass = plan_fused(qsim.createRandomHCCircuit(n, 100, 42))
-        assert npass <= 14, (n, npass)  # 100 gates collapse to ~10 HBM passes
+        assert npass <= most, (n, npass)
 
 
 def test_noise_model_host_semantics(qsim):
