@@ -332,16 +332,35 @@ static std::vector<PassChoice> beam_passes(const std::vector<Op>& ops, int n, in
         }
         return out;
     };
+    // HBM cost of a pass layout beyond a 1 KiB-run pass (single-pass probes at 30q,
+    // profiles/r01/layout): a wave instruction spans the 2^r0-amplitude run plus the tile bits
+    // just above it (the lane bits); 256 B runs cost ~15 %, lane bits at qubit >= 12 (segments
+    // >= 64 KiB apart within one instruction) ~30 %.  Ranks plans with equal pass counts.
+    auto layout_cost = [](int r0, uint64_t hi) {
+        if (r0 >= 6) return 0;
+        uint64_t h = hi;
+        int lane_hi = 0;
+        for (int k = 0; k < 6 - r0 && h; ++k) {
+            lane_hi = __builtin_ctzll(h);
+            h &= h - 1;
+        }
+        return (r0 == 5 ? 1 : 2) + (lane_hi >= 12 ? 2 : 0);
+    };
     struct St {
         std::vector<int> rem;
         std::vector<std::pair<int, uint64_t>> hist;  // (r0, free tile qubits) per pass
+        int cost = 0;
     };
     std::vector<St> states(1);
     states[0].rem.resize(ops.size());
     for (size_t i = 0; i < ops.size(); ++i) states[0].rem[i] = (int)i;
     for (int guard = 0; guard <= (int)ops.size(); ++guard) {
+        const St* done = nullptr;
         for (const St& s : states)
-            if (s.rem.empty()) {
+            if (s.rem.empty() && (!done || s.cost < done->cost)) done = &s;
+        if (done) {
+            const St& s = *done;
+            {
                 std::vector<PassChoice> out;
                 std::vector<Op> rest = ops;
                 for (const auto& h : s.hist) {
@@ -365,6 +384,7 @@ static std::vector<PassChoice> beam_passes(const std::vector<Op>& ops, int n, in
                 }
                 return out;
             }
+        }
         std::vector<St> next;
         std::vector<std::vector<int>> seen;
         for (const St& s : states) {
@@ -400,13 +420,15 @@ static std::vector<PassChoice> beam_passes(const std::vector<Op>& ops, int n, in
                     seen.push_back(t.rem);
                     t.hist = s.hist;
                     t.hist.push_back({r0, pp.second});
+                    t.cost = s.cost + layout_cost(r0, pp.second);
                     next.push_back(std::move(t));
                 }
             }
         }
         if (next.empty()) break;
-        std::stable_sort(next.begin(), next.end(),
-                         [](const St& a, const St& b) { return a.rem.size() < b.rem.size(); });
+        std::stable_sort(next.begin(), next.end(), [](const St& a, const St& b) {
+            return a.rem.size() != b.rem.size() ? a.rem.size() < b.rem.size() : a.cost < b.cost;
+        });
         if ((int)next.size() > width) next.resize(width);
         states.swap(next);
     }

@@ -211,11 +211,31 @@ std::string jb_expr(const Stage& st, int rb) {
     return e;
 }
 
-// QSIM_JIT_XCD=1: consecutive workgroups (dispatched round-robin over the 8 XCDs) take tiles
-// 1/8 of the state apart, so each XCD streams one contiguous eighth.
-bool jit_xcd() {
-    static const bool v = env_or("QSIM_JIT_XCD", 0) != 0;
+// Workgroup -> tile order (workgroups are dispatched round-robin over the 8 XCDs, so the low 3
+// bits of blockIdx pick the XCD).  QSIM_JIT_XCD: 0 natural (consecutive workgroups take
+// consecutive tiles); 1 each XCD streams one contiguous eighth of the tiles; s >= 2: the XCD bits
+// move to tile-id bits s-2 .. s (XCDs interleave at that granularity); -1 bit-reversed ids.
+int jit_xcd() {
+    static const int v = env_or("QSIM_JIT_XCD", 1);
     return v;
+}
+std::string tile_id_expr() {
+    const int x = jit_xcd();
+    const std::string b = "(unsigned long long)blockIdx.x";
+    if (x == 1)
+        return "  const unsigned long long tile_id = (gridDim.x & 7u) ? " + b + " : (" + b +
+               " & 7ull) * (gridDim.x >> 3) + (" + b + " >> 3);\n";
+    if (x >= 2) {
+        const int s = x - 2;  // XCD bits land at tile-id bits s..s+2
+        const std::string lo = "((" + b + " >> 3) & " + hexu((1ull << s) - 1ull) + ")";
+        const std::string hi = "((" + b + " >> " + std::to_string(3 + s) + ") << " + std::to_string(s + 3) + ")";
+        return "  const unsigned long long tile_id = (gridDim.x & " + std::to_string((8u << s) - 1u) + "u) ? " + b +
+               " : (" + hi + " | ((" + b + " & 7ull) << " + std::to_string(s) + ") | " + lo + ");\n";
+    }
+    if (x == -1)
+        return "  const unsigned long long tile_id = (gridDim.x & (gridDim.x - 1u)) ? " + b +
+               " : (unsigned long long)(__builtin_bitreverse32(blockIdx.x) >> (32 - (31 - __builtin_clz(gridDim.x))));\n";
+    return "  const unsigned long long tile_id = blockIdx.x;\n";
 }
 
 void gen_pass(std::ostringstream& out, const Plan& plan, const FusedPass& p, int idx) {
@@ -231,9 +251,7 @@ void gen_pass(std::ostringstream& out, const Plan& plan, const FusedPass& p, int
       << "  __shared__ double2 tile[" << T << "];\n"
       << "  char* const lds = reinterpret_cast<char*>(tile);\n"
       << "  const unsigned tid = threadIdx.x;\n"
-      << (jit_xcd() ? "  const unsigned long long tile_id = (gridDim.x & 7u) ? blockIdx.x : "
-                      "(unsigned long long)(blockIdx.x & 7u) * (gridDim.x >> 3) + (blockIdx.x >> 3);\n"
-                    : "  const unsigned long long tile_id = blockIdx.x;\n")
+      << tile_id_expr()
       << "  unsigned long long k = (tile_id & tpt_mask) << " << r0 << ";\n";
     for (int i = 0; i < nh; ++i)
         o << "  { const unsigned long long lo = k & " << hexu((1ull << p.hpos[i]) - 1ull)

@@ -40,20 +40,20 @@ def hc(qs, ngates, seed=3):
     return c
 
 
-W = [list(range(4)) + [6, 12, 15, 16, 19, 22, 27, 28],   # W-HC 30q pass 1 tile (r0 = 4)
-     list(range(4)) + [6, 8, 13, 18, 23, 25, 26, 29],    # pass 0 tile (r0 = 4)
-     list(range(4)) + [6, 8, 10, 12, 14, 16, 18, 20],
-     list(range(4)) + [6, 7, 8, 9, 10, 11, 12, 13],
-     list(range(4)) + [22, 23, 24, 25, 26, 27, 28, 29],
+W = [list(range(4)) + [6, 12, 15, 16, 19, 22, 27, 28],   # old W-HC 30q pass 1 tile (r0 = 4)
+     list(range(4)) + [6, 13, 16, 23, 25, 26, 28, 29],   # 5-pass plan: pass 0 tile
+     list(range(4)) + [9, 10, 14, 17, 19, 21, 23, 26],   # pass 3 tile
+     list(range(4)) + [5, 9, 11, 12, 15, 18, 20, 21],    # pass 1 tile
      list(range(6)) + [6 + i for i in range(6)],
-     list(range(6)) + [24, 25, 26, 27, 28, 29],
-     list(range(6)) + [10, 14, 17, 19, 21, 24],           # pass 2 tile (r0 = 6)
-     list(range(5)) + [6, 9, 12, 15, 18, 21, 24]]
+     list(range(6)) + [24, 25, 26, 27, 28, 29]]
+if os.environ.get("PROBE_LANES"):  # r0 = 4 with lane bits (a, b), registers on 20..25
+    W = [list(range(4)) + [a, b] + list(range(20, 26))
+         for a, b in ((6, 7), (6, 13), (9, 10), (5, 9), (12, 13), (16, 17), (6, 9), (7, 8))]
 probes = []
 for qs in W:
     probes.append(("light", qs, light(qs)))
-    probes.append(("hc20", qs, hc(qs, 20)))
-    probes.append(("hc40", qs, hc(qs, 40)))
+    if not os.environ.get("PROBE_LANES"):
+        probes.append(("hc20", qs, hc(qs, 20)))
 set_jit(2, -1)
 sv = q.StateVector(n)
 sv.applyGate(q.GateOp(G.H, [0]))
