@@ -523,6 +523,49 @@ int qsim_state_sample(qsim_state* s, const double* uniforms, int shots, int64_t*
     });
 }
 
+int qsim_noise_apply(qsim_state* s, int type, int qubit, double probability, uint64_t seed,
+                     uint64_t counter) {
+    return guarded([&] {
+        check_state(s);
+        DeviceGuard dg(s->device);
+        launch_noise(s->d, s->n, type, qubit, probability, seed, counter, s->stream, &s->timer);
+    });
+}
+
+int qsim_noisy_run(qsim_state* s, const qsim_gate* gates, size_t count,
+                   const qsim_noise_channel* channels, size_t n_channels, uint64_t seed,
+                   uint64_t* counter, int flags) {
+    return guarded([&] {
+        check_state(s);
+        QSIM_REQUIRE(gates || count == 0, QSIM_ERR_INVALID_ARGUMENT, "null gate list");
+        QSIM_REQUIRE(channels || n_channels == 0, QSIM_ERR_INVALID_ARGUMENT, "null channel list");
+        QSIM_REQUIRE(counter, QSIM_ERR_INVALID_ARGUMENT, "null counter");
+        DeviceGuard dg(s->device);
+        std::vector<Op> ops;
+        for (size_t i = 0; i < count; ++i) {
+            ops.push_back(lower_gate(gates[i], s->n));
+            ops.back().src = (int)i;
+        }
+        for (size_t c = 0; c < n_channels; ++c) {
+            if (channels[c].type < 0 || channels[c].type > 5)
+                fail(QSIM_ERR_INVALID_ARGUMENT, "unknown noise type");
+            if (channels[c].qubit < 0 || channels[c].qubit >= s->n)
+                fail(QSIM_ERR_OUT_OF_RANGE, "Qubit index " + std::to_string(channels[c].qubit) + " out of range");
+        }
+        if (n_channels == 0) {
+            if (flags & QSIM_RUN_FUSED) run_fused(s, ops);
+            else for (const Op& op : ops) launch_op(s->d, s->n, 1, op, s->stream, &s->timer);
+            return;
+        }
+        for (const Op& op : ops) {
+            launch_op(s->d, s->n, 1, op, s->stream, &s->timer);
+            for (size_t c = 0; c < n_channels; ++c)
+                launch_noise(s->d, s->n, channels[c].type, channels[c].qubit, channels[c].probability,
+                             seed, (*counter)++, s->stream, &s->timer);
+        }
+    });
+}
+
 int qsim_state_profile(qsim_state* s, int enable) {
     return guarded([&] {
         check_state(s);

@@ -172,6 +172,11 @@ void launch_fused(double2* st, int n, uint64_t batch, const Plan& plan, const Ti
                   const Stage* d_stages, hipStream_t s, Timer* tm, const JitModule* jm = nullptr,
                   const uint64_t* frames = nullptr);
 
+// Single-trajectory Monte-Carlo noise (noise.hip): one per-pair pass of channel `type`
+// (reference NoiseType numbering) on `qubit`, uniforms from the hash of (seed, counter, pair).
+void launch_noise(double2* st, int n, int type, int qubit, double p, uint64_t seed,
+                  uint64_t counter, hipStream_t s, Timer* tm);
+
 // Reductions / readout helpers (reduce.hip)
 void launch_init_basis(double2* st, int n, uint64_t batch, uint64_t basis, hipStream_t s);
 void launch_probabilities(const double2* st, uint64_t count, double* out, hipStream_t s);

@@ -2,6 +2,8 @@
 // BatchedSimulator front end (src/NoiseModel.cu:653-972) over the qsim_batch C ABI.
 #include "qsim/NoiseModel.hpp"
 
+#include <algorithm>
+#include <cmath>
 #include <numeric>
 #include <stdexcept>
 
@@ -38,6 +40,67 @@ static std::vector<int> allQubits(int n) {
 void NoiseModel::addDepolarizingAll(int n, double p) { addDepolarizing(allQubits(n), p); }
 void NoiseModel::addAmplitudeDampingAll(int n, double g) { addAmplitudeDamping(allQubits(n), g); }
 void NoiseModel::addPhaseDampingAll(int n, double g) { addPhaseDamping(allQubits(n), g); }
+
+// ---- NoisySimulator (src/NoiseModel.cu:320-651)
+NoisySimulator::NoisySimulator(int num_qubits, const NoiseModel& noise_model)
+    : state_(num_qubits), noise_model_(noise_model) {
+    setSeed(std::random_device{}());
+}
+NoisySimulator::NoisySimulator(int num_qubits) : NoisySimulator(num_qubits, NoiseModel{}) {}
+
+void NoisySimulator::setSeed(unsigned int seed) {
+    rng_.seed(seed);
+    seed_ = seed;
+    counter_ = 0;
+}
+
+void NoisySimulator::reset() { state_.initializeZero(); }
+
+void NoisySimulator::run(const Circuit& circuit) {
+    if (circuit.getNumQubits() != state_.getNumQubits())
+        throw std::invalid_argument("Circuit qubit count doesn't match simulator");
+    const std::vector<qsim_gate> gates = detail::toAbi(circuit);
+    std::vector<qsim_noise_channel> ch;
+    for (const NoiseChannel& c : noise_model_.getChannels())
+        for (int q : c.qubits) ch.push_back(qsim_noise_channel{static_cast<int>(c.type), q, c.probability});
+    check(qsim_noisy_run(state_.handle(), gates.data(), gates.size(), ch.data(), ch.size(), seed_,
+                         &counter_, QSIM_RUN_FUSED));
+}
+
+void NoisySimulator::applyGate(const GateOp& gate) {
+    const qsim_gate g = detail::toAbi(gate);
+    check(qsim_apply_gate(state_.handle(), &g));
+}
+
+void NoisySimulator::applyNoise(const NoiseChannel& channel) {
+    for (int q : channel.qubits) applyNoiseToQubit(channel.type, q, channel.probability);
+}
+
+void NoisySimulator::applyNoiseToQubit(NoiseType type, int qubit, double probability) {
+    check(qsim_noise_apply(state_.handle(), static_cast<int>(type), qubit, probability, seed_, counter_));
+    ++counter_;
+}
+
+std::vector<int> NoisySimulator::sample(int n_shots) {
+    const std::vector<double> p = getProbabilities();
+    std::vector<double> cdf(p.size());
+    std::partial_sum(p.begin(), p.end(), cdf.begin());
+    std::uniform_real_distribution<double> dist(0.0, 1.0);
+    std::vector<int> out(n_shots > 0 ? n_shots : 0);
+    for (int& o : out) o = (int)(std::lower_bound(cdf.begin(), cdf.end(), dist(rng_)) - cdf.begin());
+    return out;
+}
+
+int NoisySimulator::measureQubit(int qubit) {
+    double p0 = 0.0, total = 0.0;
+    check(qsim_state_prob_bit_zero(state_.handle(), qubit, &p0));
+    check(qsim_state_total_probability(state_.handle(), &total));
+    std::uniform_real_distribution<double> dist(0.0, 1.0);
+    const int result = dist(rng_) < p0 ? 0 : 1;
+    const double kept = result == 0 ? p0 : total - p0;
+    check(qsim_state_collapse(state_.handle(), qubit, result, 1.0 / std::sqrt(kept)));
+    return result;
+}
 
 // ---- BatchedSimulator
 BatchedSimulator::BatchedSimulator(int num_qubits, int batch_size)

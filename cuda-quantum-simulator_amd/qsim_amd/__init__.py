@@ -8,12 +8,12 @@ from .circuit import (Circuit, GateOp, GateType, MAX_QUBITS, MIN_QUBITS, createB
                       createGHZCircuit, createRandomCircuit, createRandomHCCircuit,
                       createScalingBenchmarkCircuit, is_valid_qubit_count)
 from .simulator import (BatchedGateSet, BatchedSimulator, NoiseChannel, NoiseModel, NoiseType,
-                        RunMode, Simulator, StateVector, device_count, device_info)
+                        NoisySimulator, RunMode, Simulator, StateVector, device_count, device_info)
 
 __all__ = [
     "Circuit", "GateOp", "GateType", "MAX_QUBITS", "MIN_QUBITS", "createBellCircuit",
     "createGHZCircuit", "createRandomCircuit", "createRandomHCCircuit",
     "createScalingBenchmarkCircuit", "is_valid_qubit_count", "BatchedGateSet",
-    "BatchedSimulator", "NoiseChannel", "NoiseModel", "NoiseType", "RunMode", "Simulator",
+    "BatchedSimulator", "NoiseChannel", "NoiseModel", "NoiseType", "NoisySimulator", "RunMode", "Simulator",
     "StateVector", "device_count", "device_info",
 ]

@@ -10,6 +10,7 @@ from __future__ import annotations
 
 import ctypes
 import enum
+import os
 from typing import List, Optional, Sequence
 
 import numpy as np
@@ -319,6 +320,73 @@ class NoiseModel:
         for i, (t, q, p) in enumerate(flat):
             arr[i].type, arr[i].qubit, arr[i].probability = int(t), q, p
         return arr, len(flat)
+
+
+class NoisySimulator:
+    """Reference NoisySimulator (include/NoiseModel.cuh:139-214, src/NoiseModel.cu:320-651):
+    Monte-Carlo noise on one state vector.  run() applies each gate and then every channel entry
+    of the model (one per-pair noise pass each, noise.hip); global channels act on no qubit (F6).
+    measureQubit measures index bit `qubit` (LSB-first, src/NoiseModel.cu:615-651) unlike
+    StateVector.measure (F2).  Seeded from os.urandom like the reference's random_device."""
+
+    def __init__(self, num_qubits: int, noise_model: Optional[NoiseModel] = None):
+        self._state = StateVector(num_qubits)
+        self._noise = noise_model or NoiseModel()
+        self.setSeed(int.from_bytes(os.urandom(4), "little"))
+
+    def setNoiseModel(self, nm: NoiseModel) -> None: self._noise = nm
+    def getNoiseModel(self) -> NoiseModel: return self._noise
+
+    def setSeed(self, seed: int) -> None:
+        self._seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+        self._counter = 0
+        self._rng = np.random.default_rng(seed)
+
+    @property
+    def state(self) -> StateVector:
+        return self._state
+
+    def reset(self) -> None: self._state.initializeZero()
+
+    def run(self, circuit: Circuit, mode: RunMode = RunMode.Fused) -> None:
+        if circuit.getNumQubits() != self._state.getNumQubits():
+            raise ValueError("Circuit qubit count doesn't match simulator")
+        g, ng = circuit.to_abi()
+        ch, nch = self._noise.to_abi()
+        ctr = _c.c_uint64(self._counter)
+        _lib.check(_lib.hip.qsim_noisy_run(self._state.handle, g, ng, ch, nch, self._seed,
+                                           _c.byref(ctr), int(mode)))
+        self._counter = ctr.value
+
+    def applyGate(self, op: GateOp) -> None: self._state.applyGate(op)
+
+    def applyNoise(self, channel: NoiseChannel) -> None:
+        for q in channel.qubits:
+            self.applyNoiseToQubit(channel.type, q, channel.probability)
+
+    def applyNoiseToQubit(self, type: NoiseType, qubit: int, probability: float) -> None:
+        _lib.check(_lib.hip.qsim_noise_apply(self._state.handle, int(type), qubit, probability,
+                                             self._seed, self._counter))
+        self._counter += 1
+
+    def getStateVector(self) -> np.ndarray: return self._state.toHost()
+    def getProbabilities(self) -> np.ndarray: return self._state.getProbabilities()
+
+    def sample(self, n_shots: int) -> np.ndarray:
+        """Host CDF + lower_bound like the reference (src/NoiseModel.cu:599-613)."""
+        cdf = np.cumsum(self.getProbabilities())
+        return np.searchsorted(cdf, self._rng.random(n_shots), side="left").astype(np.int64)
+
+    def measureQubit(self, qubit: int) -> int:
+        p0 = self._state.probBitZero(qubit)
+        result = 0 if float(self._rng.random()) < p0 else 1
+        kept = p0 if result == 0 else self._state.getTotalProbability() - p0
+        self._state.collapse(qubit, result, 1.0 / np.sqrt(kept))
+        return result
+
+    def getNumQubits(self) -> int: return self._state.getNumQubits()
+    def getStateSize(self) -> int: return self._state.getSize()
+    def synchronize(self) -> None: self._state.synchronize()
 
 
 class BatchedGateSet(enum.IntEnum):

@@ -6,11 +6,14 @@
 #pragma once
 
 #include <algorithm>
+#include <complex>
+#include <cstdint>
 #include <cstddef>
 #include <random>
 #include <vector>
 
 #include "Circuit.hpp"
+#include "StateVector.hpp"
 
 struct qsim_batch;
 
@@ -58,6 +61,42 @@ public:
 private:
     std::vector<NoiseChannel> channels_;
     void addPerQubit(NoiseType t, const std::vector<int>& qubits, double p);
+};
+
+// Reference NoisySimulator (include/NoiseModel.cuh:139-214): Monte-Carlo noise on one state.
+// run() applies each gate and then every channel entry (one per-pair noise pass each, reference
+// kernels src/NoiseModel.cu:115-314); global channels act on no qubit (F6).  measureQubit uses
+// index bit `qubit` (LSB-first, :615-651).
+class NoisySimulator {
+public:
+    NoisySimulator(int num_qubits, const NoiseModel& noise_model);
+    explicit NoisySimulator(int num_qubits);
+    NoisySimulator(const NoisySimulator&) = delete;
+    NoisySimulator& operator=(const NoisySimulator&) = delete;
+    NoisySimulator(NoisySimulator&&) noexcept = default;
+    NoisySimulator& operator=(NoisySimulator&&) noexcept = default;
+
+    void setNoiseModel(const NoiseModel& noise_model) { noise_model_ = noise_model; }
+    const NoiseModel& getNoiseModel() const { return noise_model_; }
+    void setSeed(unsigned int seed);
+    void reset();
+    void run(const Circuit& circuit);
+    void applyGate(const GateOp& gate);
+    void applyNoise(const NoiseChannel& channel);
+    void applyNoiseToQubit(NoiseType type, int qubit, double probability);
+    std::vector<std::complex<double>> getStateVector() const { return state_.toHost(); }
+    std::vector<double> getProbabilities() const { return state_.getProbabilities(); }
+    std::vector<int> sample(int n_shots);
+    int measureQubit(int qubit);
+    int getNumQubits() const { return state_.getNumQubits(); }
+    size_t getStateSize() const { return state_.getSize(); }
+    StateVector& state() { return state_; }
+
+private:
+    StateVector state_;
+    NoiseModel noise_model_;
+    uint64_t seed_ = 0, counter_ = 0;
+    std::mt19937 rng_;
 };
 
 // Gate set applied per trajectory.  Reference: only X/Y/Z/H and CNOT act, everything else is

@@ -22,6 +22,7 @@
  *   sample                           src/Simulator.cu:164-185, src/StateVector.cu:316-342
  *   OptimizedGates applyGate1Q_opt   include/OptimizedGates.cuh:91-93
  *   BatchedSimulator                 include/NoiseModel.cuh:231-297, src/NoiseModel.cu:653-972
+ *   NoisySimulator noise kernels     include/NoiseModel.cuh:139-214, src/NoiseModel.cu:115-577
  */
 #ifndef QSIM_HIP_H
 #define QSIM_HIP_H
@@ -179,6 +180,19 @@ int qsim_batch_profile(qsim_batch* b, int enable);
 int qsim_batch_profile_count(qsim_batch* b, int* n);
 int qsim_batch_profile_get(qsim_batch* b, int i, char* name, size_t name_len,
                            double* total_ms, int64_t* launches, double* alg_bytes);
+
+/* ---- single-trajectory Monte-Carlo noise (NoisySimulator, include/NoiseModel.cuh:139-214) ----
+ * One noise pass on `qubit` with the reference kernels' per-pair semantics
+ * (applyBitFlipKernel ... applyPhaseDampingKernel, src/NoiseModel.cu:115-314): every amplitude
+ * pair draws from a counter hash of (seed, counter, pair index).  Asynchronous. */
+int qsim_noise_apply(qsim_state* s, int type, int qubit, double probability, uint64_t seed,
+                     uint64_t counter);
+/* NoisySimulator::run (src/NoiseModel.cu:369-382): each gate, then every channel entry in order,
+ * one noise pass each; *counter advances by one per pass.  With no channel entries the circuit
+ * runs as fused passes (flags = QSIM_RUN_*), else one kernel per gate (the noise interleaves). */
+int qsim_noisy_run(qsim_state* s, const qsim_gate* gates, size_t count,
+                   const qsim_noise_channel* channels, size_t n_channels, uint64_t seed,
+                   uint64_t* counter, int flags);
 
 /* ---- multi-GPU: state sharded by its high physical qubits, one process per GPU, RCCL ----
  * (the reference is single-GPU, README.md:361-367).  World size W = 2^g ranks;

@@ -177,3 +177,92 @@ def time_prefix(n: int, gates: Sequence[Gate], budget_s: float):
     lib().qsim_oracle_time_prefix(n, _to_abi(gates), len(gates), budget_s, ctypes.byref(done),
                                   ctypes.byref(secs))
     return done.value, secs.value
+
+
+# ---- NoisySimulator per-pair noise (test infrastructure) ---------------------------------
+# Restates the reference kernels src/NoiseModel.cu:115-314 (per-pair draws, per-pair damping
+# renormalisation) driven by the engine's documented counter hash (csrc/hip/noise.hip), so the
+# GPU pass can be checked exactly; the reference's cuRAND stream itself is parity-unpinned.
+_M64 = (1 << 64) - 1
+
+
+def _mix(z):
+    z = (z + 0x9e3779b97f4a7c15) & _M64
+    z = ((z ^ (z >> 30)) * 0xbf58476d1ce4e5b9) & _M64
+    z = ((z ^ (z >> 27)) * 0x94d049bb133111eb) & _M64
+    return z ^ (z >> 31)
+
+
+def _mix_np(z):
+    with np.errstate(over="ignore"):
+        z = z + np.uint64(0x9e3779b97f4a7c15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xbf58476d1ce4e5b9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94d049bb133111eb)
+        return z ^ (z >> np.uint64(31))
+
+
+def noise_key(seed, counter):
+    return _mix(_mix(seed & _M64) ^ ((counter * 0x9e3779b97f4a7c15 + 0x632be59bd9b4e019) & _M64))
+
+
+def _uniform(h):
+    return ((h >> np.uint64(40)).astype(np.uint32).astype(np.float32) + np.float32(1.0)) * \
+        np.float32(1.0 / 16777216.0)
+
+
+def noise_pass(state, n, ntype, q, p, seed, counter):
+    """One reference noise kernel (type numbering == NoiseType) on `state` (modified copy)."""
+    s = np.array(state, dtype=complex)
+    idx = np.arange(1 << (n - 1), dtype=np.uint64)
+    h = _mix_np(np.uint64(noise_key(seed, counter)) ^ _mix_np(idx))
+    r1 = _uniform(h)
+    mask = np.uint64((1 << q) - 1)
+    i0 = ((idx & mask) | ((idx & ~mask) << np.uint64(1))).astype(np.int64)
+    i1 = i0 | (1 << q)
+    a0, a1 = s[i0].copy(), s[i1].copy()
+    if ntype in (0, 3, 4, 5):
+        fire = r1 < np.float32(p)
+        if ntype == 0:
+            r2 = _uniform(_mix_np(h ^ np.uint64(0x5bd1e9955bd1e995)))
+            pauli = np.where(r2 < np.float32(1.0) / np.float32(3.0), 1,
+                             np.where(r2 < np.float32(2.0) / np.float32(3.0), 2, 3))
+        else:
+            pauli = np.full(idx.size, {3: 1, 4: 3, 5: 2}[ntype])
+        x, y, z = fire & (pauli == 1), fire & (pauli == 2), fire & (pauli == 3)
+        s[i0[x]], s[i1[x]] = a1[x], a0[x]
+        s[i0[y]], s[i1[y]] = -1j * a1[y], 1j * a0[y]
+        s[i1[z]] = -a1[z]
+        return s
+    g = p
+    p1 = np.abs(a1) ** 2
+    n0 = np.abs(a0) ** 2
+    if ntype == 1:
+        dec = r1 < p1 * g
+        nd = np.sqrt(n0 + g * p1)
+        nk = np.sqrt(n0 + (1.0 - g) * p1)
+        ok_d, ok_k = dec & (nd > 1e-15), ~dec & (nk > 1e-15)
+        s[i0[ok_d]] = (a0[ok_d] + np.sqrt(g) * a1[ok_d]) / nd[ok_d]
+        s[i1[ok_d]] = 0
+        s[i0[ok_k]] = a0[ok_k] / nk[ok_k]
+        s[i1[ok_k]] = np.sqrt(1.0 - g) * a1[ok_k] / nk[ok_k]
+        return s
+    k1 = r1 < g * p1
+    s[i0[k1]] = 0
+    pos = k1 & (p1 > 1e-15)
+    s[i1[pos]] = a1[pos] / np.sqrt(p1[pos])
+    ns = n0 + (1.0 - g) * p1
+    ok = ~k1 & (ns > 1e-15)
+    s[i0[ok]] = a0[ok] / np.sqrt(ns[ok])
+    s[i1[ok]] = np.sqrt(1.0 - g) * a1[ok] / np.sqrt(ns[ok])
+    return s
+
+
+def noisy_run(n, gates, channels, seed, counter=0, state=None):
+    """NoisySimulator::run (src/NoiseModel.cu:369-382): gate, then every (type, qubit, p) entry."""
+    s = zero_state(n) if state is None else np.array(state, dtype=complex)
+    for g in gates:
+        s = apply_numpy(s, n, g)
+        for (t, q, p) in channels:
+            s = noise_pass(s, n, t, q, p, seed, counter)
+            counter += 1
+    return s, counter
