@@ -566,6 +566,74 @@ int qsim_noisy_run(qsim_state* s, const qsim_gate* gates, size_t count,
     });
 }
 
+static void check_dm(const qsim_state* s, int n) {
+    check_state(s);
+    if (n < 1 || n > QSIM_DM_MAX_QUBITS)
+        fail(QSIM_ERR_INVALID_ARGUMENT, "Density matrix supports 1-" + std::to_string(QSIM_DM_MAX_QUBITS) + " qubits");
+    if (s->n != 2 * n) fail(QSIM_ERR_INVALID_ARGUMENT, "density matrix state must have 2n qubits");
+}
+
+int qsim_dm_run(qsim_state* s, int n, const qsim_gate* gates, size_t count,
+                const qsim_noise_channel* channels, size_t n_channels, int flags) {
+    return guarded([&] {
+        check_dm(s, n);
+        QSIM_REQUIRE(gates || count == 0, QSIM_ERR_INVALID_ARGUMENT, "null gate list");
+        QSIM_REQUIRE(channels || n_channels == 0, QSIM_ERR_INVALID_ARGUMENT, "null channel list");
+        DeviceGuard dg(s->device);
+        std::vector<Op> ops;
+        dm_lower(n, gates, count, channels, n_channels, ops);
+        if (flags & QSIM_RUN_FUSED) run_fused(s, ops);
+        else for (const Op& op : ops) launch_op(s->d, s->n, 1, op, s->stream, &s->timer);
+    });
+}
+
+int qsim_dm_apply_channel(qsim_state* s, int n, int type, int qubit, double p) {
+    return guarded([&] {
+        check_dm(s, n);
+        DeviceGuard dg(s->device);
+        std::vector<Op> ops;
+        dm_lower_channel(n, type, qubit, p, ops);
+        for (const Op& op : ops) launch_op(s->d, s->n, 1, op, s->stream, &s->timer);
+    });
+}
+
+int qsim_dm_diagonal(qsim_state* s, int n, double* dst) {
+    return guarded([&] {
+        check_dm(s, n);
+        QSIM_REQUIRE(dst, QSIM_ERR_INVALID_ARGUMENT, "null destination");
+        DeviceGuard dg(s->device);
+        double* d_p = nullptr;
+        QSIM_HIPCHK(hipMallocAsync((void**)&d_p, sizeof(double) << n, s->stream));
+        launch_dm_diag(s->d, n, d_p, s->stream);
+        QSIM_HIPCHK(hipMemcpyAsync(dst, d_p, sizeof(double) << n, hipMemcpyDeviceToHost, s->stream));
+        QSIM_HIPCHK(hipFreeAsync(d_p, s->stream));
+        QSIM_HIPCHK(hipStreamSynchronize(s->stream));
+    });
+}
+
+int qsim_dm_init_pure(qsim_state* s, int n, const double* psi) {
+    return guarded([&] {
+        check_dm(s, n);
+        QSIM_REQUIRE(psi, QSIM_ERR_INVALID_ARGUMENT, "null state");
+        DeviceGuard dg(s->device);
+        double2* d_psi = nullptr;
+        QSIM_HIPCHK(hipMallocAsync((void**)&d_psi, sizeof(double2) << n, s->stream));
+        QSIM_HIPCHK(hipMemcpyAsync(d_psi, psi, sizeof(double2) << n, hipMemcpyHostToDevice, s->stream));
+        launch_dm_init(s->d, d_psi, n, s->stream);
+        QSIM_HIPCHK(hipFreeAsync(d_psi, s->stream));
+        QSIM_HIPCHK(hipStreamSynchronize(s->stream));
+    });
+}
+
+int qsim_dm_init_maximally_mixed(qsim_state* s, int n) {
+    return guarded([&] {
+        check_dm(s, n);
+        DeviceGuard dg(s->device);
+        launch_dm_init(s->d, nullptr, n, s->stream);
+        QSIM_HIPCHK(hipStreamSynchronize(s->stream));
+    });
+}
+
 int qsim_state_profile(qsim_state* s, int enable) {
     return guarded([&] {
         check_state(s);

@@ -177,6 +177,13 @@ void launch_fused(double2* st, int n, uint64_t batch, const Plan& plan, const Ti
 void launch_noise(double2* st, int n, int type, int qubit, double p, uint64_t seed,
                   uint64_t counter, hipStream_t s, Timer* tm);
 
+// Density matrices as 2n-index-bit states (density.hip).
+void dm_lower(int n, const qsim_gate* gates, size_t count, const qsim_noise_channel* ch,
+              size_t nch, std::vector<Op>& out);
+void dm_lower_channel(int n, int type, int qubit, double p, std::vector<Op>& out);
+void launch_dm_diag(const double2* rho, int n, double* out, hipStream_t s);
+void launch_dm_init(double2* rho, const double2* psi, int n, hipStream_t s);
+
 // Reductions / readout helpers (reduce.hip)
 void launch_init_basis(double2* st, int n, uint64_t batch, uint64_t basis, hipStream_t s);
 void launch_probabilities(const double2* st, uint64_t count, double* out, hipStream_t s);

@@ -9,8 +9,10 @@ from .circuit import (Circuit, GateOp, GateType, MAX_QUBITS, MIN_QUBITS, createB
                       createScalingBenchmarkCircuit, is_valid_qubit_count)
 from .simulator import (BatchedGateSet, BatchedSimulator, NoiseChannel, NoiseModel, NoiseType,
                         NoisySimulator, RunMode, Simulator, StateVector, device_count, device_info)
+from .density import DensityMatrix, DensityMatrixSimulator
 
 __all__ = [
+    "DensityMatrix", "DensityMatrixSimulator",
     "Circuit", "GateOp", "GateType", "MAX_QUBITS", "MIN_QUBITS", "createBellCircuit",
     "createGHZCircuit", "createRandomCircuit", "createRandomHCCircuit",
     "createScalingBenchmarkCircuit", "is_valid_qubit_count", "BatchedGateSet",

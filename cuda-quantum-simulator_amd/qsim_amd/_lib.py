@@ -120,6 +120,13 @@ _sig(hip, "qsim_noise_apply", [_P, c_int, c_int, c_double, c_uint64, c_uint64])
 _sig(hip, "qsim_noisy_run", [_P, POINTER(qsim_gate), c_size_t, POINTER(qsim_noise_channel), c_size_t,
                              c_uint64, POINTER(c_uint64), c_int])
 
+_sig(hip, "qsim_dm_run", [_P, c_int, POINTER(qsim_gate), c_size_t, POINTER(qsim_noise_channel),
+                          c_size_t, c_int])
+_sig(hip, "qsim_dm_apply_channel", [_P, c_int, c_int, c_int, c_double])
+_sig(hip, "qsim_dm_diagonal", [_P, c_int, _P])
+_sig(hip, "qsim_dm_init_pure", [_P, c_int, _P])
+_sig(hip, "qsim_dm_init_maximally_mixed", [_P, c_int])
+
 # ---- multi-GPU (sharded) state
 class qsim_op(Structure):
     _fields_ = [("kind", c_int32), ("sub", c_int32), ("t0", c_int32), ("t1", c_int32),

@@ -22,6 +22,7 @@
  *   sample                           src/Simulator.cu:164-185, src/StateVector.cu:316-342
  *   OptimizedGates applyGate1Q_opt   include/OptimizedGates.cuh:91-93
  *   BatchedSimulator                 include/NoiseModel.cuh:231-297, src/NoiseModel.cu:653-972
+ *   DensityMatrix(Simulator)         include/DensityMatrix.cuh:63-224, src/DensityMatrix.cu
  *   NoisySimulator noise kernels     include/NoiseModel.cuh:139-214, src/NoiseModel.cu:115-577
  */
 #ifndef QSIM_HIP_H
@@ -193,6 +194,23 @@ int qsim_noise_apply(qsim_state* s, int type, int qubit, double probability, uin
 int qsim_noisy_run(qsim_state* s, const qsim_gate* gates, size_t count,
                    const qsim_noise_channel* channels, size_t n_channels, uint64_t seed,
                    uint64_t* counter, int flags);
+
+/* ---- density matrices (DensityMatrix / DensityMatrixSimulator, include/DensityMatrix.cuh:63-224)
+ * rho of n qubits (1 <= n <= QSIM_DM_MAX_QUBITS) lives in a qsim_state created with 2n qubits:
+ * amplitude k = i * 2^n + j holds rho[i][j] (the reference's row-major layout,
+ * src/DensityMatrix.cu:29-30); purity = qsim_state_total_probability, the matrix =
+ * qsim_state_to_host, measurement collapse = qsim_state_collapse on bits q + n and q. */
+#define QSIM_DM_MAX_QUBITS 15
+/* DensityMatrixSimulator::run (src/DensityMatrix.cu:201-212): each gate as U rho U^dag, then for
+ * each of its qubits every channel entry on that qubit or with qubit = -1 (a global channel).
+ * CRY/CRZ/Toffoli -> QSIM_ERR_RUNTIME (:264-266).  flags = QSIM_RUN_*.  Asynchronous. */
+int qsim_dm_run(qsim_state* rho, int n_qubits, const qsim_gate* gates, size_t count,
+                const qsim_noise_channel* channels, size_t n_channels, int flags);
+/* One channel (applyDepolarizing ... applyBitPhaseFlip, :298-356) on `qubit`. */
+int qsim_dm_apply_channel(qsim_state* rho, int n_qubits, int type, int qubit, double p);
+int qsim_dm_diagonal(qsim_state* rho, int n_qubits, double* dst);          /* 2^n: Re rho_ii */
+int qsim_dm_init_pure(qsim_state* rho, int n_qubits, const double* psi);   /* rho = |psi><psi| */
+int qsim_dm_init_maximally_mixed(qsim_state* rho, int n_qubits);          /* rho = I / 2^n */
 
 /* ---- multi-GPU: state sharded by its high physical qubits, one process per GPU, RCCL ----
  * (the reference is single-GPU, README.md:361-367).  World size W = 2^g ranks;

@@ -266,3 +266,55 @@ def noisy_run(n, gates, channels, seed, counter=0, state=None):
             s = noise_pass(s, n, t, q, p, seed, counter)
             counter += 1
     return s, counter
+
+
+# ---- DensityMatrixSimulator (test infrastructure) ----------------------------------------
+# rho' = U rho U^dag with textbook matrices, channels per the reference kernels
+# src/DensityMatrix.cu:978-1122 (depolarizing: off-diagonal x (1 - 4p/3) only; bit-phase flip =
+# phase flip, :343-356; amplitude damping with the pre-channel rho11).
+def dm_apply_gate(rho, n, gate):
+    t, qubits, th = gate
+    if t in (13, 14, 16):
+        raise RuntimeError("Gate not supported in density matrix simulation")
+    d = 1 << n
+    cols = np.stack([apply_numpy(rho[:, j], n, gate) for j in range(d)], axis=1)  # U rho
+    return np.stack([apply_numpy(cols[i, :].conj(), n, gate).conj() for i in range(d)], axis=0)
+
+
+def dm_channel(rho, n, ntype, q, p):
+    d = 1 << n
+    r = (np.arange(d) >> q) & 1
+    R, C = np.meshgrid(r, r, indexing="ij")
+    off = R != C
+    out = rho.copy()
+    flip = np.arange(d) ^ (1 << q)
+    if ntype == 0:
+        out[off] *= 1.0 - 4.0 * p / 3.0
+    elif ntype == 1:
+        partner = rho[np.ix_(flip, flip)]
+        d00 = (R == 0) & (C == 0)
+        out[d00] = rho[d00] + p * partner[d00]
+        out[(R == 1) & (C == 1)] *= 1.0 - p
+        out[off] *= np.sqrt(1.0 - p)
+    elif ntype == 2:
+        out[off] *= np.sqrt(1.0 - p)
+    elif ntype == 3:
+        out = (1.0 - p) * rho + p * rho[np.ix_(flip, flip)]
+    else:
+        out[off] *= 1.0 - 2.0 * p
+    return out
+
+
+def dm_run(n, gates, channels=(), rho=None):
+    """DensityMatrixSimulator::run (src/DensityMatrix.cu:201-212); channel qubit -1 = global."""
+    d = 1 << n
+    if rho is None:
+        rho = np.zeros((d, d), complex)
+        rho[0, 0] = 1.0
+    for g in gates:
+        rho = dm_apply_gate(rho, n, g)
+        for q in g[1]:
+            for (t, cq, p) in channels:
+                if cq < 0 or cq == q:
+                    rho = dm_channel(rho, n, t, q, p)
+    return rho
