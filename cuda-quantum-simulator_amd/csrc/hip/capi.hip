@@ -355,6 +355,53 @@ int qsim_apply_matrix1q(qsim_state* s, int target, const double m[8], const int*
     });
 }
 
+int qsim_apply_matrix2q(qsim_state* s, int q0, int q1, const double m[32], const int* controls,
+                        int n_controls) {
+    return guarded([&] {
+        check_state(s);
+        QSIM_REQUIRE(m, QSIM_ERR_INVALID_ARGUMENT, "null matrix");
+        QSIM_REQUIRE(controls || n_controls == 0, QSIM_ERR_INVALID_ARGUMENT, "null controls");
+        for (int q : {q0, q1})
+            if (q < 0 || q >= s->n) fail(QSIM_ERR_OUT_OF_RANGE, "Qubit index " + std::to_string(q) + " out of range");
+        if (q0 == q1) fail(QSIM_ERR_INVALID_ARGUMENT, "Two-qubit gate requires distinct qubits");
+        uint64_t cm = 0;
+        for (int i = 0; i < n_controls; ++i) {
+            const int c = controls[i];
+            if (c < 0 || c >= s->n) fail(QSIM_ERR_OUT_OF_RANGE, "Qubit index " + std::to_string(c) + " out of range");
+            if (c == q0 || c == q1 || ((cm >> c) & 1ull))
+                fail(QSIM_ERR_INVALID_ARGUMENT, "control qubits must be distinct from the targets");
+            cm |= 1ull << c;
+        }
+        DeviceGuard dg(s->device);
+        launch_matrix2q(s->d, s->n, q0, q1, m, cm, s->stream, &s->timer);
+    });
+}
+
+int qsim_apply_diagonal_layer(qsim_state* s, const double* gp, uint64_t active) {
+    return guarded([&] {
+        check_state(s);
+        QSIM_REQUIRE(gp || active == 0, QSIM_ERR_INVALID_ARGUMENT, "null gate_params");
+        if (s->n < 64 && (active >> s->n)) fail(QSIM_ERR_OUT_OF_RANGE, "active mask names a qubit >= n");
+        std::vector<Op> ops;
+        for (int q = 0; q < s->n; ++q) {
+            if (!((active >> q) & 1ull)) continue;
+            Op o;
+            o.kind = K_DIAG;
+            o.sub = S_GEN;
+            o.t0 = q;
+            o.m[0] = gp[8 * q + 0];
+            o.m[1] = gp[8 * q + 1];
+            o.m[2] = gp[8 * q + 6];
+            o.m[3] = gp[8 * q + 7];
+            o.d0_one = o.m[0] == 1.0 && o.m[1] == 0.0;
+            o.src = (int)ops.size();
+            ops.push_back(o);
+        }
+        DeviceGuard dg(s->device);
+        if (!ops.empty()) run_fused(s, ops);
+    });
+}
+
 int qsim_plan_fused(int n_qubits, const qsim_gate* gates, size_t count, int hmax, int32_t* order,
                     int32_t* pass_of, int32_t* n_passes) {
     return guarded([&] {

@@ -469,4 +469,70 @@ void launch_op(double2* st, int n, uint64_t batch, const Op& op, hipStream_t s, 
     }
 }
 
+// ---------------------------------------------------------------------------------------
+// General two-qubit matrix (the k = 2 case of applyMatrix; the reference
+// only has the 2x2 applyGate1Q_opt, include/OptimizedGates.cuh:91-93).  One thread per group of
+// four amplitudes {b1 b0} (b0 = bit q0, b1 = bit q1) of the control == 1 subspace; the group
+// index is spread over the other bits by zero insertion (fix[] ascending: q0, q1, controls).
+// ---------------------------------------------------------------------------------------
+struct M2Args {
+    double2* st;
+    uint64_t groups;
+    uint64_t setmask;  // control bits forced to 1
+    int nfix;
+    int fix[8];
+    int q0, q1;
+    double2 m[16];     // row-major 4x4 on index (b1 << 1) | b0
+};
+
+__global__ __launch_bounds__(256) void k_m2(M2Args a) {
+    const uint64_t step = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < a.groups; g += step) {
+        uint64_t i = g;
+        for (int k = 0; k < a.nfix; ++k) {
+            const uint64_t lo = i & ((1ull << a.fix[k]) - 1ull);
+            i = ((i ^ lo) << 1) | lo;
+        }
+        i |= a.setmask;
+        const uint64_t b0 = 1ull << a.q0, b1 = 1ull << a.q1;
+        const uint64_t idx[4] = {i, i | b0, i | b1, i | b0 | b1};
+        double2 v[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[k] = a.st[idx[k]];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            double2 acc = make_double2(0.0, 0.0);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) acc = cadd(acc, cmul(a.m[4 * r + k], v[k]));
+            a.st[idx[r]] = acc;
+        }
+    }
+}
+
+void launch_matrix2q(double2* st, int n, int q0, int q1, const double* m, uint64_t cmask,
+                     hipStream_t s, Timer* tm) {
+    M2Args a{};
+    a.st = st;
+    a.q0 = q0;
+    a.q1 = q1;
+    for (int k = 0; k < 16; ++k) a.m[k] = make_double2(m[2 * k], m[2 * k + 1]);
+    int pos[8], np = 0;
+    pos[np++] = q0;
+    pos[np++] = q1;
+    for (int q = 0; q < n; ++q)
+        if ((cmask >> q) & 1ull) {
+            if (np == 8) fail(QSIM_ERR_INVALID_ARGUMENT, "at most 6 controls");
+            pos[np++] = q;
+            a.setmask |= 1ull << q;
+        }
+    std::sort(pos, pos + np);
+    a.nfix = np;
+    for (int k = 0; k < np; ++k) a.fix[k] = pos[k];
+    a.groups = 1ull << (n - np);
+    const uint64_t blocks = std::min<uint64_t>((a.groups + 255) / 256, 256ull * 32);
+    TimedLaunch tl(tm, "matrix2q", 64.0 * (double)a.groups, s);
+    hipLaunchKernelGGL(k_m2, dim3((unsigned)blocks), dim3(256), 0, s, a);
+    QSIM_HIPCHK(hipGetLastError());
+}
+
 }  // namespace qsim_hip

@@ -184,6 +184,23 @@ class StateVector:
         ctl = (_c.c_int * max(1, len(controls)))(*controls)
         _lib.check(_lib.hip.qsim_apply_matrix1q(self._h, target, buf, ctl, len(controls)))
 
+    def applyMatrix2Q(self, q0: int, q1: int, m, controls: Sequence[int] = ()) -> None:
+        """General 4x4 on (q0, q1), row-major over (bit q1 << 1) | bit q0 (qsim_apply_matrix2q)."""
+        mm = np.asarray(m, dtype=np.complex128).reshape(16)
+        buf = (_c.c_double * 32)(*[v for z in mm for v in (z.real, z.imag)])
+        ctl = (_c.c_int * max(1, len(controls)))(*controls)
+        _lib.check(_lib.hip.qsim_apply_matrix2q(self._h, q0, q1, buf, ctl, len(controls)))
+
+    def applyDiagonalLayer(self, gate_params, active_qubits: int) -> None:
+        """applyFusedSingleQubitLayer (src/OptimizedGates.cu:344-382): gate_params[q][0] / [q][3]
+        scale the bit-q = 0 / 1 amplitudes of every active qubit."""
+        gp = np.ascontiguousarray(np.asarray(gate_params, dtype=np.complex128).reshape(-1, 4))
+        if gp.shape[0] < self._n:
+            raise ValueError("gate_params needs 4 entries per qubit")
+        flat = gp.view(np.float64).reshape(-1)
+        _lib.check(_lib.hip.qsim_apply_diagonal_layer(
+            self._h, flat.ctypes.data_as(_c.POINTER(_c.c_double)), active_qubits))
+
     def run(self, circuit: Circuit, mode: RunMode = RunMode.Fused) -> None:
         arr, n = circuit.to_abi()
         _lib.check(_lib.hip.qsim_run(self._h, arr, n, int(mode)))

@@ -106,6 +106,14 @@ int qsim_run(qsim_state* s, const qsim_gate* gates, size_t count, int flags);
  * (applyGate1Q_opt, include/OptimizedGates.cuh:91-93), optionally controlled on `controls`. */
 int qsim_apply_matrix1q(qsim_state* s, int target, const double m[8],
                         const int* controls, int n_controls);
+/* General 4x4 matrix on (q0, q1), m = 32 doubles, row-major over the index (bit q1 << 1) | bit q0,
+ * optionally controlled (the k = 2 applyMatrix of SURVEY §8(f) rank 3).  Asynchronous. */
+int qsim_apply_matrix2q(qsim_state* s, int q0, int q1, const double m[32], const int* controls,
+                        int n_controls);
+/* applyFusedSingleQubitLayer (src/OptimizedGates.cu:344-382): for every qubit q in `active`,
+ * amplitudes with bit q = 0 are scaled by gate_params[q*4+0] and those with bit q = 1 by
+ * gate_params[q*4+3] (complex, re/im interleaved: 8 doubles per qubit).  Runs as fused passes. */
+int qsim_apply_diagonal_layer(qsim_state* s, const double* gate_params, uint64_t active);
 /* Host-only introspection of the fused-pass planner (no device needed).  Writes, for each gate
  * in execution order, its index in `gates` (order[count]) and its pass number (pass_of[count],
  * -1 for gates executed per-gate), and the number of passes.  Gates are only reordered past

@@ -1,0 +1,73 @@
+"""general matrix APIs beyond the reference's 2x2 applyGate1Q_opt
+(include/OptimizedGates.cuh:91-93) and the diagonal layer applyFusedSingleQubitLayer
+(src/OptimizedGates.cu:344-382), checked against dense numpy application on random states
+(re/im ~ normal(0,1), normalised, like tests/test_optimized_gates.cu:45-61)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _rand_state(n, seed):
+    rng = np.random.default_rng(seed)
+    s = rng.normal(size=1 << n) + 1j * rng.normal(size=1 << n)
+    return s / np.linalg.norm(s)
+
+
+def _apply2(state, n, m, q0, q1, controls=()):
+    out = state.copy()
+    idx = np.arange(1 << n)
+    base = idx[((idx >> q0) & 1 == 0) & ((idx >> q1) & 1 == 0)]
+    for c in controls:
+        base = base[(base >> c) & 1 == 1]
+    grp = [base, base | (1 << q0), base | (1 << q1), base | (1 << q0) | (1 << q1)]
+    v = np.stack([state[g] for g in grp])
+    w = m @ v
+    for k in range(4):
+        out[grp[k]] = w[k]
+    return out
+
+
+@pytest.mark.parametrize("n,q0,q1,controls", [(2, 0, 1, ()), (5, 3, 1, ()), (10, 7, 2, (0,)),
+                                              (12, 0, 11, (5, 9)), (14, 13, 6, ())])
+def test_matrix2q_matches_numpy(qsim, gpu_ready, n, q0, q1, controls):
+    rng = np.random.default_rng(n + q0)
+    m = rng.normal(size=(4, 4)) + 1j * rng.normal(size=(4, 4))  # any matrix (not only unitary)
+    s0 = _rand_state(n, n)
+    sv = qsim.StateVector(n)
+    sv.fromHost(s0)
+    sv.applyMatrix2Q(q0, q1, m, controls)
+    np.testing.assert_allclose(sv.toHost(), _apply2(s0, n, m, q0, q1, controls), atol=1e-12, rtol=0)
+
+
+def test_matrix2q_cnot_and_errors(qsim, oracle, gpu_ready):
+    n = 6
+    s0 = _rand_state(n, 1)
+    cnot = np.eye(4)[[0, 3, 2, 1]]  # control q0, target q1 in the (b1 b0) basis
+    sv = qsim.StateVector(n)
+    sv.fromHost(s0)
+    sv.applyMatrix2Q(2, 4, cnot)
+    np.testing.assert_allclose(sv.toHost(), oracle.run_numpy(n, [(11, [2, 4], 0.0)], s0), atol=1e-12)
+    with pytest.raises(IndexError):
+        sv.applyMatrix2Q(0, n, cnot)
+    with pytest.raises(ValueError):
+        sv.applyMatrix2Q(1, 1, cnot)
+    with pytest.raises(ValueError):
+        sv.applyMatrix2Q(0, 1, cnot, [1])
+
+
+@pytest.mark.parametrize("n", [3, 12, 22])
+def test_diagonal_layer_matches_numpy(qsim, gpu_ready, n):
+    rng = np.random.default_rng(n)
+    params = rng.normal(size=(n, 4)) + 1j * rng.normal(size=(n, 4))
+    active = int(rng.integers(1, 1 << n))
+    s0 = _rand_state(n, n + 1)
+    sv = qsim.StateVector(n)
+    sv.fromHost(s0)
+    sv.applyDiagonalLayer(params, active)
+    idx = np.arange(1 << n)
+    want = s0.copy()
+    for q in range(n):
+        if (active >> q) & 1:
+            want = want * np.where((idx >> q) & 1, params[q, 3], params[q, 0])
+    np.testing.assert_allclose(sv.toHost(), want, atol=1e-12 * np.max(np.abs(want)) * 10, rtol=1e-12)
