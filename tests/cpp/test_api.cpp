@@ -3,6 +3,7 @@
 // mirrors.  Needs a GPU; the CPU oracle (tests only) is the header-only
 // oracle/cpu_simulator.hpp.
 #include <qsim/Circuit.hpp>
+#include <qsim/DensityMatrix.hpp>
 #include <qsim/NoiseModel.hpp>
 #include <qsim/Simulator.hpp>
 #include <qsim/StateVector.hpp>
@@ -328,6 +329,40 @@ TEST(StateVector, GeneralMatrixEqualsY) {  // test_optimized_gates.cu general-1Q
 }
 
 // ---- tests/test_noise.cu (batched, noise-free) ----------------------------------------------
+TEST(DensityMatrix, ReferenceSuite) {  // tests/test_density_matrix.cu:142-157, :251-265, :306-318
+    qsim::DensityMatrixSimulator bell(2);
+    bell.run(qsim::createBellCircuit());
+    auto p = bell.getProbabilities();
+    EXPECT_NEAR(p[0], 0.5, kTol);
+    EXPECT_NEAR(p[3], 0.5, kTol);
+    EXPECT_NEAR(bell.getPurity(), 1.0, kTol);
+    qsim::NoiseModel nm;
+    nm.addBitFlip(0.5);
+    qsim::DensityMatrixSimulator flip(1, nm);
+    qsim::Circuit x(1);
+    x.x(0);
+    flip.run(x);
+    EXPECT_NEAR(flip.getProbabilities()[0], 0.5, 0.1);
+    qsim::NoiseModel nm2;
+    nm2.addDepolarizing(0.1);
+    nm2.addAmplitudeDamping(0.05);
+    qsim::DensityMatrixSimulator tr(2, nm2);
+    qsim::Circuit c(2);
+    c.h(0).h(1).cnot(0, 1).rz(0, 0.5);
+    tr.run(c);
+    EXPECT_NEAR(tr.getTrace(), 1.0, 1e-6);
+    EXPECT_THROW(qsim::DensityMatrix(0), std::invalid_argument);
+}
+TEST(Noisy, BitFlipUndoesX) {  // tests/test_noise.cu:157-179
+    qsim::NoiseModel nm;
+    nm.addBitFlip({0}, 1.0);
+    qsim::NoisySimulator sim(1, nm);
+    sim.setSeed(42);
+    qsim::Circuit x(1);
+    x.x(0);
+    sim.run(x);
+    EXPECT_NEAR(sim.getProbabilities()[0], 1.0, kTol);
+}
 TEST(Batched, NoiseFreeBell) {  // :249-281, :313-339
     qsim::BatchedSimulator bs(2, 5);
     bs.run(qsim::createBellCircuit());
