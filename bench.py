@@ -53,6 +53,12 @@ def parse():
     p.add_argument("--noise", type=float, default=0.01)
     p.add_argument("--cpu-budget", type=float, default=12.0,
                    help="seconds of single-thread CPU oracle work for cpu_baseline (0 = skip)")
+    p.add_argument("--launch-timeout", type=float, default=1500.0,
+                   help="N > 1 without an external launcher: seconds before the rank processes "
+                        "are stopped")
+    p.add_argument("--dry-run", action="store_true",
+                   help="N-rank skeleton without the GPU: gloo bootstrap, the host remap planner "
+                        "per rank and step, barriers and max-over-ranks timing (CPU tests)")
     p.add_argument("--pmc-json", default=None,
                    help="per-launch HBM traffic measured by rocprofv3 --pmc (see profiles/)")
     return p.parse_args()
@@ -224,11 +230,17 @@ def run_batch(args):
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # No launcher around us: start the N rank processes ourselves (before anything here
+        # touches the GPU) and relay rank 0's JSON line (qsim_amd/launch.py).
+        from qsim_amd.launch import launch_ranks
+        sys.exit(launch_ranks(os.path.abspath(__file__), sys.argv[1:], args.gpus,
+                              timeout_s=args.launch_timeout))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if args.workload == "batch":
         run_batch(args)
         return
-    if world > 1 or args.gpus > 1:
+    if world > 1 or args.gpus > 1 or args.dry_run:
         from qsim_amd import dist_bench  # sharded strong-scaling path (RCCL over xGMI)
         dist_bench.run(args, METRIC, HBM_PEAK_GBPS)
     else:

@@ -344,7 +344,7 @@ int qsim_batch_run(qsim_batch* b, const qsim_gate* gates, size_t count,
                 QSIM_HIPCHK(hipGetLastError());
             }
             if (!fops.empty()) {
-                const Plan& plan = b->plans.get(fops, b->n);
+                const Plan& plan = b->plans.get(fops, b->n).plan;
                 b->ops.upload(plan.ops.data(), plan.ops.size() * sizeof(TileOp), b->stream);
                 b->stages.upload(plan.stages.data(), plan.stages.size() * sizeof(Stage), b->stream);
                 launch_fused(b->d, b->n, (uint64_t)b->batch, plan, (const TileOp*)b->ops.ptr,
@@ -405,6 +405,40 @@ int qsim_batch_traj_probabilities(qsim_batch* b, int traj, double* dst) {
         launch_probabilities(b->d + (uint64_t)traj * N, N, d_p, b->stream);
         QSIM_HIPCHK(hipMemcpyAsync(dst, d_p, N * sizeof(double), hipMemcpyDeviceToHost, b->stream));
         QSIM_HIPCHK(hipFreeAsync(d_p, b->stream));
+        QSIM_HIPCHK(hipStreamSynchronize(b->stream));
+    });
+}
+
+int qsim_batch_sample(qsim_batch* b, const double* uniforms, int shots, int64_t* out) {
+    return bguard([&] {
+        need(b);
+        if (shots < 0) fail(QSIM_ERR_INVALID_ARGUMENT, "n_shots must be non-negative");
+        if (shots > 0 && (!uniforms || !out)) fail(QSIM_ERR_INVALID_ARGUMENT, "null buffer");
+        sample_indices(b->d, b->n, (uint64_t)b->batch, uniforms, shots, out, b->stream);
+    });
+}
+
+int qsim_batch_histogram(qsim_batch* b, const double* uniforms, int shots, int64_t* hist) {
+    return bguard([&] {
+        need(b);
+        if (shots < 0) fail(QSIM_ERR_INVALID_ARGUMENT, "n_shots must be non-negative");
+        if (!hist || (shots > 0 && !uniforms)) fail(QSIM_ERR_INVALID_ARGUMENT, "null buffer");
+        const uint64_t N = 1ull << b->n, nshots = (uint64_t)shots * (uint64_t)b->batch;
+        std::vector<int64_t> idx(nshots);
+        sample_indices(b->d, b->n, (uint64_t)b->batch, uniforms, shots, idx.data(), b->stream);
+        int64_t* d_idx = nullptr;
+        unsigned long long* d_h = nullptr;
+        QSIM_HIPCHK(hipMallocAsync((void**)&d_idx, std::max<uint64_t>(1, nshots) * sizeof(int64_t), b->stream));
+        QSIM_HIPCHK(hipMallocAsync((void**)&d_h, N * sizeof(unsigned long long), b->stream));
+        QSIM_HIPCHK(hipMemsetAsync(d_h, 0, N * sizeof(unsigned long long), b->stream));
+        if (nshots) {
+            QSIM_HIPCHK(hipMemcpyAsync(d_idx, idx.data(), nshots * sizeof(int64_t),
+                                       hipMemcpyHostToDevice, b->stream));
+            launch_histogram(d_idx, nshots, N, d_h, b->stream);
+        }
+        QSIM_HIPCHK(hipMemcpyAsync(hist, d_h, N * sizeof(int64_t), hipMemcpyDeviceToHost, b->stream));
+        QSIM_HIPCHK(hipFreeAsync(d_idx, b->stream));
+        QSIM_HIPCHK(hipFreeAsync(d_h, b->stream));
         QSIM_HIPCHK(hipStreamSynchronize(b->stream));
     });
 }

@@ -154,6 +154,7 @@ struct qsim_state {
     DevBuf ops, stages;  // fused-plan descriptors, re-uploaded only when the plan changes
     PlanCache plans;
     Timer timer;
+    int last_passes = 0, last_jit_passes = 0;  // of the last fused run (qsim_state_last_run)
     ~qsim_state() {
         if (stream) (void)hipStreamSynchronize(stream);
         if (d) (void)hipFree(d);
@@ -180,17 +181,30 @@ static void check_state(const qsim_state* s) {
 }
 
 static void run_fused(qsim_state* s, const std::vector<Op>& ops) {
-    const Plan& plan = s->plans.get(ops, s->n);
-    const JitModule* jm = jit_for(s->plans.jit, plan, s->n);
+    PlanCache::Entry& pe = s->plans.get(ops, s->n);
+    const Plan& plan = pe.plan;
+    const JitModule* jm = jit_for(pe.jit, plan, s->n);
     s->ops.upload(plan.ops.data(), plan.ops.size() * sizeof(TileOp), s->stream);
     s->stages.upload(plan.stages.data(), plan.stages.size() * sizeof(Stage), s->stream);
     launch_fused(s->d, s->n, 1, plan, (const TileOp*)s->ops.ptr, (const Stage*)s->stages.ptr,
                  s->stream, &s->timer, jm);
+    s->last_passes = (int)plan.passes.size();
+    s->last_jit_passes = 0;
+    if (jm)
+        for (hipFunction_t f : jm->fn) s->last_jit_passes += f != nullptr;
 }
 
 extern "C" {
 
 const char* qsim_last_error(void) { return g_last_error.c_str(); }
+
+int qsim_state_last_run(qsim_state* s, int* passes, int* jit_passes) {
+    return guarded([&] {
+        check_state(s);
+        if (passes) *passes = s->last_passes;
+        if (jit_passes) *jit_passes = s->last_jit_passes;
+    });
+}
 int qsim_abi_version(void) { return QSIM_ABI_VERSION; }
 
 int qsim_device_count(int* count) {
@@ -566,7 +580,7 @@ int qsim_state_sample(qsim_state* s, const double* uniforms, int shots, int64_t*
         if (shots <= 0) fail(QSIM_ERR_INVALID_ARGUMENT, "n_shots must be positive");
         QSIM_REQUIRE(uniforms && out, QSIM_ERR_INVALID_ARGUMENT, "null buffer");
         DeviceGuard dg(s->device);
-        sample_indices(s->d, s->n, uniforms, shots, out, s->stream);
+        sample_indices(s->d, s->n, 1, uniforms, shots, out, s->stream);
     });
 }
 

@@ -18,6 +18,8 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
+#include <thread>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -315,10 +317,12 @@ __global__ __launch_bounds__(256) void k_exchange_copy(XArgs a, uint64_t lo, int
 
 }  // namespace qsim_hip
 
+// ncclInProgress is the normal return of a non-blocking communicator (the call is queued; the
+// communicator settles before the next use, comm_settle below).
 #define QSIM_NCCLCHK(call)                                                              \
     do {                                                                                \
         ncclResult_t r_ = (call);                                                       \
-        if (r_ != ncclSuccess)                                                          \
+        if (r_ != ncclSuccess && r_ != ncclInProgress)                                  \
             fail(QSIM_ERR_DEVICE, std::string("RCCL error: ") + ncclGetErrorString(r_)); \
     } while (0)
 
@@ -343,6 +347,7 @@ struct qsim_dist {
     hipStream_t comm_stream = nullptr;  // remap transfers (RCCL or, virtual, device copies)
     std::vector<hipEvent_t> events;     // remap pipeline: packed part p, transferred part p
     ncclComm_t comm = nullptr;
+    bool aborted = false;  // the communicator was aborted after an RCCL / HIP error or a timeout
     std::vector<int> perm;
     DevBuf ops, stages;
     // Plans of recent runs, keyed by (gate list, map at the start of the run): a repeated circuit
@@ -360,7 +365,19 @@ struct qsim_dist {
     ~qsim_dist() {
         (void)hipSetDevice(device);
         if (stream) (void)hipStreamSynchronize(stream);
-        if (comm) (void)ncclCommDestroy(comm);
+        if (comm) {  // flush, bounded wait (non-blocking comm), then destroy; abort on trouble
+            bool ok = ncclCommFinalize(comm) == ncclSuccess;
+            if (!ok) {
+                ncclResult_t st = ncclInProgress;
+                const auto t0 = std::chrono::steady_clock::now();
+                while (ncclCommGetAsyncError(comm, &st) == ncclSuccess && st == ncclInProgress &&
+                       std::chrono::steady_clock::now() - t0 < std::chrono::seconds(60))
+                    std::this_thread::yield();
+                ok = st == ncclSuccess;
+            }
+            if (ok) (void)ncclCommDestroy(comm);
+            else (void)ncclCommAbort(comm);
+        }
         for (Shard& s : shards)
             for (void* p : {(void*)s.d, (void*)s.sendbuf, (void*)s.recvbuf})
                 if (p) (void)hipFree(p);
@@ -390,6 +407,67 @@ int dguard(F&& f) {
 }
 void need(const qsim_dist* d) {
     if (!d) fail(QSIM_ERR_INVALID_ARGUMENT, "null dist handle");
+    if (d->aborted)
+        fail(QSIM_ERR_DEVICE, "distributed state unusable: its RCCL communicator was aborted "
+                              "after an earlier error");
+}
+// Entry points that touch the communicator: any RCCL / HIP failure (or a timeout) aborts it, so
+// peers blocked in a collective with this rank are released instead of hanging.
+template <typename F>
+int dguard_comm(qsim_dist* d, F&& f) {
+    const int rc = dguard(std::forward<F>(f));
+    if (rc == QSIM_ERR_DEVICE && d && d->comm && !d->aborted) {
+        (void)ncclCommAbort(d->comm);
+        d->comm = nullptr;
+        d->aborted = true;
+    }
+    return rc;
+}
+double env_seconds(const char* k, double dflt) {
+    const char* e = std::getenv(k);
+    const double v = e ? std::atof(e) : dflt;
+    return v > 0 ? v : dflt;
+}
+// Wait until a non-blocking communicator has finished queuing its last call (init, group end,
+// collective); a communicator error or QSIM_DIST_TIMEOUT seconds without progress fails (the
+// caller's dguard_comm then aborts the communicator).
+void comm_settle(ncclComm_t comm, const char* what, double timeout_s) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+        ncclResult_t st = ncclSuccess;
+        QSIM_NCCLCHK(ncclCommGetAsyncError(comm, &st));
+        if (st == ncclSuccess) return;
+        if (st != ncclInProgress)
+            fail(QSIM_ERR_DEVICE, std::string("RCCL error during ") + what + ": " + ncclGetErrorString(st));
+        if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > timeout_s)
+            fail(QSIM_ERR_DEVICE, std::string("RCCL timeout during ") + what);
+        std::this_thread::yield();
+    }
+}
+void comm_settle(qsim_dist* d, const char* what) {
+    if (!d->virt && d->comm) comm_settle(d->comm, what, env_seconds("QSIM_DIST_TIMEOUT", 600.0));
+}
+// hipStreamSynchronize with a watchdog: while the stream drains, a communicator error or
+// QSIM_DIST_TIMEOUT seconds fail (and abort the communicator) instead of blocking forever.
+void stream_wait(qsim_dist* d, hipStream_t s) {
+    if (d->virt || !d->comm) {
+        QSIM_HIPCHK(hipStreamSynchronize(s));
+        return;
+    }
+    const double timeout_s = env_seconds("QSIM_DIST_TIMEOUT", 600.0);
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+        const hipError_t q = hipStreamQuery(s);
+        if (q == hipSuccess) return;
+        if (q != hipErrorNotReady) QSIM_HIPCHK(q);
+        ncclResult_t st = ncclSuccess;
+        QSIM_NCCLCHK(ncclCommGetAsyncError(d->comm, &st));
+        if (st != ncclSuccess && st != ncclInProgress)
+            fail(QSIM_ERR_DEVICE, std::string("RCCL error while waiting: ") + ncclGetErrorString(st));
+        if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > timeout_s)
+            fail(QSIM_ERR_DEVICE, "timeout waiting for the distributed state's streams");
+        std::this_thread::sleep_for(std::chrono::microseconds(50));
+    }
 }
 int log2_exact(int w) {
     if (w < 1) fail(QSIM_ERR_INVALID_ARGUMENT, "world size must be positive");
@@ -517,6 +595,7 @@ void exchange(qsim_dist* d, const DStep& ex) {
                 QSIM_NCCLCHK(ncclRecv(sh.recvbuf + at, cnt, ncclDouble, x.peer_of[c], d->comm, d->comm_stream));
             }
             QSIM_NCCLCHK(ncclGroupEnd());
+            comm_settle(d, "remap send/recv");
         } else {  // shard r's slab c goes to shard peer(c), into that shard's slot my_c(r)
             for (size_t i = 0; i < d->shards.size(); ++i) {
                 const XPlan& x = xs[i];
@@ -545,15 +624,17 @@ double allreduce_sum(qsim_dist* d, double local) {
     if (d->virt) return local;
     QSIM_HIPCHK(hipMemcpyAsync(d->d_result, &local, sizeof(double), hipMemcpyHostToDevice, d->stream));
     QSIM_NCCLCHK(ncclAllReduce(d->d_result, d->d_result, 1, ncclDouble, ncclSum, d->comm, d->stream));
+    comm_settle(d, "all-reduce");
     double out = 0.0;
     QSIM_HIPCHK(hipMemcpyAsync(&out, d->d_result, sizeof(double), hipMemcpyDeviceToHost, d->stream));
-    QSIM_HIPCHK(hipStreamSynchronize(d->stream));
+    stream_wait(d, d->stream);
     return out;
 }
 void run_local(qsim_dist* d, Shard& sh, const std::vector<Op>& ops, int flags, PlanCache& pc) {
     if (flags & QSIM_RUN_FUSED) {
-        const Plan& plan = pc.get(ops, d->L);
-        const JitModule* jm = jit_for(pc.jit, plan, d->L);
+        PlanCache::Entry& pe = pc.get(ops, d->L);
+        const Plan& plan = pe.plan;
+        const JitModule* jm = jit_for(pe.jit, plan, d->L);
         d->ops.upload(plan.ops.data(), plan.ops.size() * sizeof(TileOp), d->stream);
         d->stages.upload(plan.stages.data(), plan.stages.size() * sizeof(Stage), d->stream);
         launch_fused(sh.d, d->L, 1, plan, (const TileOp*)d->ops.ptr, (const Stage*)d->stages.ptr,
@@ -627,7 +708,26 @@ int qsim_dist_create(int n_qubits, int rank, int world, const void* unique_id, i
         alloc_shards(d.get(), {rank});
         ncclUniqueId id;
         std::memcpy(&id, unique_id, sizeof(id));
-        QSIM_NCCLCHK(ncclCommInitRank(&d->comm, world, id, rank));
+        // Non-blocking communicator (QSIM_RCCL_BLOCKING=1 selects a blocking one): the init and
+        // every later call can then be bounded by a timeout and aborted, so a rank that never
+        // arrives (or dies) makes its peers fail instead of hanging.
+        const char* bl = std::getenv("QSIM_RCCL_BLOCKING");
+        const bool blocking = bl && std::atoi(bl) != 0;
+        ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+        cfg.blocking = blocking ? 1 : 0;
+        const ncclResult_t ir = ncclCommInitRankConfig(&d->comm, world, id, rank, &cfg);
+        if (ir != ncclSuccess && ir != ncclInProgress) {
+            if (d->comm) (void)ncclCommAbort(d->comm);
+            d->comm = nullptr;
+            fail(QSIM_ERR_DEVICE, std::string("RCCL error: ") + ncclGetErrorString(ir));
+        }
+        try {
+            comm_settle(d->comm, "communicator init", env_seconds("QSIM_DIST_INIT_TIMEOUT", 300.0));
+        } catch (...) {
+            (void)ncclCommAbort(d->comm);
+            d->comm = nullptr;
+            throw;
+        }
         init_zero(d.get());
         *out = d.release();
     });
@@ -664,7 +764,7 @@ int qsim_dist_destroy(qsim_dist* d) {
 }
 
 int qsim_dist_reset(qsim_dist* d) {
-    return dguard([&] {
+    return dguard_comm(d, [&] {
         need(d);
         QSIM_HIPCHK(hipSetDevice(d->device));
         init_zero(d);
@@ -672,7 +772,7 @@ int qsim_dist_reset(qsim_dist* d) {
 }
 
 int qsim_dist_run(qsim_dist* d, const qsim_gate* gates, size_t count, int flags) {
-    return dguard([&] {
+    return dguard_comm(d, [&] {
         need(d);
         if (!gates && count) fail(QSIM_ERR_INVALID_ARGUMENT, "null gate list");
         QSIM_HIPCHK(hipSetDevice(d->device));
@@ -699,10 +799,11 @@ int qsim_dist_run(qsim_dist* d, const qsim_gate* gates, size_t count, int flags)
 }
 
 int qsim_dist_sync(qsim_dist* d) {
-    return dguard([&] {
+    return dguard_comm(d, [&] {
         need(d);
         QSIM_HIPCHK(hipSetDevice(d->device));
-        QSIM_HIPCHK(hipStreamSynchronize(d->stream));
+        stream_wait(d, d->comm_stream);
+        stream_wait(d, d->stream);
     });
 }
 
@@ -714,7 +815,7 @@ int qsim_dist_perm(qsim_dist* d, int32_t* perm) {
 }
 
 int qsim_dist_local_state(qsim_dist* d, double* dst) {
-    return dguard([&] {
+    return dguard_comm(d, [&] {
         need(d);
         QSIM_HIPCHK(hipSetDevice(d->device));
         const size_t bytes = sizeof(double2) << d->L;
@@ -726,7 +827,7 @@ int qsim_dist_local_state(qsim_dist* d, double* dst) {
 }
 
 int qsim_dist_gather_state(qsim_dist* d, double* dst) {
-    return dguard([&] {
+    return dguard_comm(d, [&] {
         need(d);
         QSIM_HIPCHK(hipSetDevice(d->device));
         const uint64_t shard = 1ull << d->L;
@@ -748,8 +849,9 @@ int qsim_dist_gather_state(qsim_dist* d, double* dst) {
                 QSIM_NCCLCHK(ncclSend(d->shards[0].d, shard * 2, ncclDouble, 0, d->comm, d->stream));
             }
             QSIM_NCCLCHK(ncclGroupEnd());
+            comm_settle(d, "gather");
         }
-        QSIM_HIPCHK(hipStreamSynchronize(d->stream));
+        stream_wait(d, d->stream);
         if (root) {
             std::vector<double2> phys(1ull << d->n);
             QSIM_HIPCHK(hipMemcpy(phys.data(), all, sizeof(double2) << d->n, hipMemcpyDeviceToHost));
@@ -767,7 +869,7 @@ int qsim_dist_gather_state(qsim_dist* d, double* dst) {
 }
 
 int qsim_dist_total_probability(qsim_dist* d, double* out) {
-    return dguard([&] {
+    return dguard_comm(d, [&] {
         need(d);
         QSIM_HIPCHK(hipSetDevice(d->device));
         double local = 0.0;
@@ -778,7 +880,7 @@ int qsim_dist_total_probability(qsim_dist* d, double* out) {
 }
 
 int qsim_dist_prob_bit_zero(qsim_dist* d, int q, double* out) {
-    return dguard([&] {
+    return dguard_comm(d, [&] {
         need(d);
         if (q < 0 || q >= d->n) fail(QSIM_ERR_INVALID_ARGUMENT, "bit out of range");
         QSIM_HIPCHK(hipSetDevice(d->device));

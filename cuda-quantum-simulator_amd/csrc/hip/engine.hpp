@@ -146,6 +146,7 @@ Plan plan_fused(const std::vector<Op>& ops, int n, int hmax = -1);
 struct JitJob;
 struct JitModule {
     hipModule_t mod = nullptr;
+    int device = -1;                // unload waits for this device's queued kernels
     std::vector<hipFunction_t> fn;  // per plan pass; null = run by the interpreter
     ~JitModule();
 };
@@ -162,14 +163,21 @@ bool jit_compile(const std::string& src, std::vector<char>& code, std::string& l
 // The loaded module for `plan`, or null while it compiles / when JIT does not apply.
 const JitModule* jit_for(JitState& js, const Plan& plan, int n);
 
-// The last plan of one engine object: re-running the same circuit (the benchmark loop, repeated
-// trajectories) skips the host planning and, once compiled, runs the specialised kernels.
+// The last few plans of one engine object (LRU): re-running a circuit (the benchmark loop,
+// repeated trajectories, two circuits alternating on one state) skips the host planning and,
+// once compiled, runs the specialised kernels.
 struct PlanCache {
-    int n = -1;
-    std::vector<Op> key;
-    Plan plan;
-    JitState jit;
-    const Plan& get(const std::vector<Op>& ops, int n_qubits);
+    struct Entry {
+        int n = -1;
+        std::vector<Op> key;
+        Plan plan;
+        JitState jit;
+        uint64_t used = 0;
+    };
+    static constexpr size_t kEntries = 4;
+    std::vector<std::unique_ptr<Entry>> entries;
+    uint64_t clock = 0;
+    Entry& get(const std::vector<Op>& ops, int n_qubits);
 };
 // frames != null: batched noisy run under per-trajectory Pauli frames (FArgs::frames).
 void launch_fused(double2* st, int n, uint64_t batch, const Plan& plan, const TileOp* d_ops,
@@ -195,8 +203,10 @@ void launch_probabilities(const double2* st, uint64_t count, double* out, hipStr
 double reduce_norm(const double2* st, int n, int bit, double* d_partials, double* d_result,
                    hipStream_t s);
 void launch_collapse(double2* st, int n, int bit, int result, double scale, hipStream_t s);
-void sample_indices(const double2* st, int n, const double* uniforms, int shots, int64_t* out,
-                    hipStream_t s);
+void launch_histogram(const int64_t* d_idx, uint64_t count, uint64_t N, unsigned long long* d_hist,
+                      hipStream_t s);
+void sample_indices(const double2* st, int n, uint64_t batch, const double* uniforms, int shots,
+                    int64_t* out, hipStream_t s);
 // Average of |a|^2 over `batch` trajectories into out[2^n] (device).
 void launch_avg_probabilities(const double2* st, int n, uint64_t batch, double* out,
                               hipStream_t s);

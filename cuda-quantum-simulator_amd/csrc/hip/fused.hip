@@ -49,6 +49,8 @@ static TileOp make_tile_op(int kind, int sub, int b0, int b1, uint32_t cm, int d
     return t;
 }
 
+static constexpr int kMaxUnnormH = 512;
+
 // Group one pass's ops (tile bits) into register stages of at most `rb` target bits.
 static void plan_stages(std::vector<TileOp>& pass_ops, std::vector<int>& pass_src, int tile_bits,
                         int rb, Plan& plan, FusedPass& p) {
@@ -76,8 +78,11 @@ static void plan_stages(std::vector<TileOp>& pass_ops, std::vector<int>& pass_sr
     p.hu_count = 0;
     for (TileOp& t : ops) {
         if (t.kind == K_M1 && t.sub == S_H) {
-            if (t.cmask == 0) ++p.hu_count;  // unnormalized butterfly in the staged kernel
-            else t.sub = S_GEN;              // (no controlled H in the gate set; keep it exact)
+            // unnormalized butterfly in the staged kernel: each one scales the tile's 2-norm by
+            // exactly sqrt2, so at most kMaxUnnormH per pass bounds the growth to 2^(kMaxUnnormH/2)
+            // (no overflow for any state of norm < 2^700); further H run as the normalised matrix
+            if (t.cmask == 0 && p.hu_count < kMaxUnnormH) ++p.hu_count;
+            else t.sub = S_GEN;  // (also controlled H, not in the gate set; keep it exact)
         }
     }
     // The first stage is applied in registers straight after the HBM load and the last one
@@ -444,16 +449,28 @@ static bool same_op(const Op& a, const Op& b) {
     return true;
 }
 
-const Plan& PlanCache::get(const std::vector<Op>& ops, int n_qubits) {
-    bool hit = n == n_qubits && key.size() == ops.size();
-    for (size_t i = 0; hit && i < ops.size(); ++i) hit = same_op(key[i], ops[i]);
-    if (!hit) {
-        plan = plan_fused(ops, n_qubits);
-        key = ops;
-        n = n_qubits;
-        jit = JitState{};  // a new plan needs its own code object
+PlanCache::Entry& PlanCache::get(const std::vector<Op>& ops, int n_qubits) {
+    for (auto& e : entries) {
+        bool hit = e->n == n_qubits && e->key.size() == ops.size();
+        for (size_t i = 0; hit && i < ops.size(); ++i) hit = same_op(e->key[i], ops[i]);
+        if (hit) {
+            e->used = ++clock;
+            return *e;
+        }
     }
-    return plan;
+    if (entries.size() >= kEntries) {  // evict the least recently used plan (and its code object:
+                                       // ~JitModule waits for the device before unloading it)
+        auto lru = std::min_element(entries.begin(), entries.end(),
+                                    [](const auto& a, const auto& b) { return a->used < b->used; });
+        entries.erase(lru);
+    }
+    auto e = std::make_unique<Entry>();
+    e->plan = plan_fused(ops, n_qubits);
+    e->key = ops;
+    e->n = n_qubits;
+    e->used = ++clock;
+    entries.push_back(std::move(e));
+    return *entries.back();
 }
 
 static int env_int(const char* k, int d) {

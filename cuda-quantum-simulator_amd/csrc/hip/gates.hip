@@ -335,10 +335,77 @@ __global__ __launch_bounds__(256) void k_swap_ll(GArgs a) {
     }
 }
 
+// Any number of controls (M1 or DIAG): one thread per active pair / active amplitude, the index
+// built by zero insertion at every fixed position (target and controls, any height).  Used only
+// when the wave-item kernels' 3 fixed high positions do not suffice (e.g. applyMatrix with 3+
+// high controls); correctness path, the wave-item kernels carry the reference gate set.
+struct ManyArgs {
+    double2* st;
+    uint64_t units;
+    uint64_t setmask;
+    int nfix;
+    int fix[64];
+    int t0, kind, sub, d0_one;
+    double2 m0, m1, m2, m3;
+};
+
+__global__ __launch_bounds__(256) void k_op_many(ManyArgs a) {
+    const uint64_t step = (uint64_t)gridDim.x * blockDim.x;
+    const uint64_t tb = 1ull << a.t0;
+    for (uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; u < a.units; u += step) {
+        uint64_t i = u;
+        for (int k = 0; k < a.nfix; ++k) {
+            const uint64_t lo = i & ((1ull << a.fix[k]) - 1ull);
+            i = ((i ^ lo) << 1) | lo;
+        }
+        i |= a.setmask;
+        if (a.kind == K_M1) {
+            double2 v0 = a.st[i], v1 = a.st[i | tb];
+            m1_pair(a.sub, a.m0, a.m1, a.m2, a.m3, v0, v1);
+            a.st[i] = v0;
+            a.st[i | tb] = v1;
+        } else {
+            const int bit = (int)((i >> a.t0) & 1ull);
+            a.st[i] = diag_apply(a.sub, a.d0_one, a.m0, a.m1, bit, a.st[i]);
+        }
+    }
+}
+
+static void launch_op_many(double2* st, int n, uint64_t batch, const Op& op, hipStream_t s,
+                           Timer* tm, double bytes) {
+    ManyArgs a{};
+    a.t0 = op.t0;
+    a.kind = op.kind;
+    a.sub = op.sub;
+    a.d0_one = op.d0_one ? 1 : 0;
+    a.m0 = make_double2(op.m[0], op.m[1]);
+    a.m1 = make_double2(op.m[2], op.m[3]);
+    a.m2 = make_double2(op.m[4], op.m[5]);
+    a.m3 = make_double2(op.m[6], op.m[7]);
+    uint64_t fixmask = op.cmask;
+    a.setmask = op.cmask;
+    if (op.kind == K_M1) fixmask |= 1ull << op.t0;
+    if (op.kind == K_DIAG && op.d0_one) {
+        fixmask |= 1ull << op.t0;
+        a.setmask |= 1ull << op.t0;
+    }
+    for (int q = 0; q < n; ++q)
+        if ((fixmask >> q) & 1ull) a.fix[a.nfix++] = q;
+    TimedLaunch tl(tm, "op_many", bytes, s);
+    for (uint64_t b = 0; b < batch; ++b) {
+        a.st = st + (b << n);
+        a.units = 1ull << (n - a.nfix);
+        const uint64_t blocks = std::min<uint64_t>((a.units + 255) / 256, 256ull * 64);
+        hipLaunchKernelGGL(k_op_many, dim3((unsigned)blocks), dim3(256), 0, s, a);
+        QSIM_HIPCHK(hipGetLastError());
+    }
+}
+
 // ---------------------------------------------------------------------------------------
 // Host: launch
 // ---------------------------------------------------------------------------------------
 static void add_fix(GArgs& a, int pos) {
+    if (a.nfix >= 3) fail(QSIM_ERR_RUNTIME, "internal: more than 3 fixed high positions");
     int i = a.nfix++;
     a.fix[i] = pos;
     while (i > 0 && a.fix[i - 1] > a.fix[i]) {
@@ -380,6 +447,19 @@ static void go(K kernel, const GArgs& a, int U, hipStream_t s) {
 }
 
 void launch_op(double2* st, int n, uint64_t batch, const Op& op, hipStream_t s, Timer* tm) {
+    {
+        // fixed high positions the wave-item kernels would need: high controls + the target
+        // (M1 / one-sided DIAG with t0 >= 6) or both SWAP qubits; more than 3 -> general kernel
+        int high = __builtin_popcountll(op.cmask >> 6 << 6);
+        if ((op.kind == K_M1 || (op.kind == K_DIAG && op.d0_one)) && op.t0 >= 6) ++high;
+        if (op.kind == K_SWAP && op.cmask)
+            fail(QSIM_ERR_INVALID_ARGUMENT, "controlled SWAP is not supported");
+        if (high > 3 && op.kind != K_SWAP) {
+            launch_op_many(st, n, batch, op, s, tm,
+                           op_alg_bytes(op, std::ldexp(1.0, n) * (double)batch));
+            return;
+        }
+    }
     GArgs a{};
     a.st = st;
     a.stride = 1ull << n;

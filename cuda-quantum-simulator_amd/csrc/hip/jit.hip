@@ -398,7 +398,14 @@ private:
 }  // namespace
 
 JitModule::~JitModule() {
-    if (mod) (void)hipModuleUnload(mod);
+    if (!mod) return;
+    // kernels of this module may still be queued on the engine's stream: drain the device first
+    int cur = -1;
+    (void)hipGetDevice(&cur);
+    if (device >= 0 && device != cur) (void)hipSetDevice(device);
+    (void)hipDeviceSynchronize();
+    (void)hipModuleUnload(mod);
+    if (device >= 0 && device != cur && cur >= 0) (void)hipSetDevice(cur);
 }
 
 const JitModule* jit_for(JitState& js, const Plan& plan, int n) {
@@ -429,6 +436,7 @@ const JitModule* jit_for(JitState& js, const Plan& plan, int n) {
         return nullptr;
     }
     auto m = std::make_unique<JitModule>();
+    QSIM_HIPCHK(hipGetDevice(&m->device));
     QSIM_HIPCHK(hipModuleLoadData(&m->mod, js.job->code.data()));
     m->fn.assign(plan.passes.size(), nullptr);
     for (size_t i = 0; i < plan.passes.size(); ++i) {

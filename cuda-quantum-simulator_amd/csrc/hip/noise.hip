@@ -61,7 +61,7 @@ __global__ __launch_bounds__(256) void k_noise(NArgs a) {
         const uint64_t i0 = (idx & mask) | ((idx & ~mask) << 1);
         const uint64_t i1 = i0 | (1ull << a.target);
         if constexpr (TYPE == 0 || TYPE == 3 || TYPE == 4 || TYPE == 5) {  // Pauli flips
-            if (!(r1 < (float)a.p)) continue;
+            if (!((double)r1 < a.p)) continue;  // float draw vs double p, as the reference (:195)
             int pauli = TYPE == 3 ? 1 : (TYPE == 4 ? 3 : 2);  // 1 X, 2 Y, 3 Z
             if constexpr (TYPE == 0) {                         // depolarizing (:191-216)
                 const float r2 = nz_uniform(nz_mix(h ^ 0x5bd1e9955bd1e995ull));

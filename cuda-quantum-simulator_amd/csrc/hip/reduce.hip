@@ -143,7 +143,8 @@ __global__ __launch_bounds__(256) void k_chunk_sums(const double2* st, uint64_t 
     if (threadIdx.x == 0) sums[blockIdx.x] = (wsum[0] + wsum[1]) + (wsum[2] + wsum[3]);
 }
 
-// shot s: search chunk `chunk_of[s]` for the first i with prefix >= target[s]; -1 chunk -> N.
+// shot s: search chunk `chunk_of[s]` (global over the batch) for the first i with prefix >=
+// target[s], output the index within its trajectory; -1 chunk -> N (the reference's end()).
 __global__ __launch_bounds__(64) void k_chunk_search(const double2* st, uint64_t chunk,
                                                      const int64_t* chunk_of,
                                                      const double* target, int shots,
@@ -190,59 +191,99 @@ __global__ __launch_bounds__(64) void k_chunk_search(const double2* st, uint64_t
             }
         }
         if (found >= chunk) found = chunk - 1;
-        out[s] = (int64_t)(base + found);
+        out[s] = (int64_t)((base + found) & (total - 1));
     }
 }
 
-void sample_indices(const double2* st, int n, const double* uniforms, int shots, int64_t* out,
-                    hipStream_t s) {
+// Shots of `batch` trajectories (the single state is batch = 1).  uniforms / out are
+// trajectory-major: shot s of trajectory t at t * shots + s (the reference draws them in that
+// order, src/NoiseModel.cu:938-957).  The chunk prefix is accumulated with Neumaier's
+// compensation, so the device CDF is the exactly rounded one up to a few ulps; an index can
+// then differ from the reference's sequential partial_sum only where the uniform lies between
+// the exact and the sequentially rounded CDF at a step (tests/test_sampling_gpu.py checks that).
+void sample_indices(const double2* st, int n, uint64_t batch, const double* uniforms, int shots,
+                    int64_t* out, hipStream_t s) {
+    if (shots <= 0 || batch == 0) return;
     const uint64_t total = 1ull << n;
     const uint64_t chunk = 1ull << std::min(n, kChunkLog);
-    const uint64_t nchunks = total / chunk;
+    const uint64_t nchunks = total / chunk;  // per trajectory
+    const uint64_t all_chunks = nchunks * batch;
+    const uint64_t nshots = (uint64_t)shots * batch;
     double* d_sums = nullptr;
-    QSIM_HIPCHK(hipMallocAsync((void**)&d_sums, nchunks * sizeof(double), s));
-    hipLaunchKernelGGL(k_chunk_sums, dim3((unsigned)nchunks), dim3(256), 0, s, st, chunk, d_sums);
+    QSIM_HIPCHK(hipMallocAsync((void**)&d_sums, all_chunks * sizeof(double), s));
+    hipLaunchKernelGGL(k_chunk_sums, dim3((unsigned)all_chunks), dim3(256), 0, s, st, chunk, d_sums);
     QSIM_HIPCHK(hipGetLastError());
-    std::vector<double> sums(nchunks);
-    QSIM_HIPCHK(hipMemcpyAsync(sums.data(), d_sums, nchunks * sizeof(double),
+    std::vector<double> sums(all_chunks);
+    QSIM_HIPCHK(hipMemcpyAsync(sums.data(), d_sums, all_chunks * sizeof(double),
                                hipMemcpyDeviceToHost, s));
     QSIM_HIPCHK(hipStreamSynchronize(s));
     QSIM_HIPCHK(hipFreeAsync(d_sums, s));
-    std::vector<double> cdf(nchunks);
-    double run = 0.0;
-    for (uint64_t c = 0; c < nchunks; ++c) cdf[c] = (run += sums[c]);
-    std::vector<int64_t> chunk_of(shots);
-    std::vector<double> target(shots);
-    for (int i = 0; i < shots; ++i) {
-        const double r = uniforms[i];
-        auto it = std::lower_bound(cdf.begin(), cdf.end(), r);
-        if (it == cdf.end()) {
-            chunk_of[i] = -1;
-            target[i] = 0.0;
-        } else {
-            const int64_t c = it - cdf.begin();
-            chunk_of[i] = c;
-            target[i] = r - (c > 0 ? cdf[c - 1] : 0.0);
+    std::vector<double> cdf(nchunks), comp(nchunks);
+    std::vector<int64_t> chunk_of(nshots);
+    std::vector<double> target(nshots);
+    for (uint64_t t = 0; t < batch; ++t) {
+        double run = 0.0, c = 0.0;  // Neumaier: run + c is the prefix to ~1 ulp
+        for (uint64_t k = 0; k < nchunks; ++k) {
+            const double x = sums[t * nchunks + k];
+            const double y = run + x;
+            c += std::fabs(run) >= std::fabs(x) ? (run - y) + x : (x - y) + run;
+            run = y;
+            cdf[k] = run + c;
+            comp[k] = c - (cdf[k] - run);  // residual below cdf[k]
+        }
+        for (int i = 0; i < shots; ++i) {
+            const uint64_t j = t * (uint64_t)shots + (uint64_t)i;
+            const double r = uniforms[j];
+            auto it = std::lower_bound(cdf.begin(), cdf.end(), r);
+            if (it == cdf.end()) {
+                chunk_of[j] = -1;
+                target[j] = 0.0;
+            } else {
+                const int64_t k = it - cdf.begin();
+                chunk_of[j] = (int64_t)(t * nchunks) + k;
+                target[j] = k > 0 ? (r - cdf[k - 1]) - comp[k - 1] : r;
+            }
         }
     }
     int64_t* d_chunk = nullptr;
     double* d_target = nullptr;
     int64_t* d_out = nullptr;
-    QSIM_HIPCHK(hipMallocAsync((void**)&d_chunk, shots * sizeof(int64_t), s));
-    QSIM_HIPCHK(hipMallocAsync((void**)&d_target, shots * sizeof(double), s));
-    QSIM_HIPCHK(hipMallocAsync((void**)&d_out, shots * sizeof(int64_t), s));
-    QSIM_HIPCHK(hipMemcpyAsync(d_chunk, chunk_of.data(), shots * sizeof(int64_t),
+    QSIM_HIPCHK(hipMallocAsync((void**)&d_chunk, nshots * sizeof(int64_t), s));
+    QSIM_HIPCHK(hipMallocAsync((void**)&d_target, nshots * sizeof(double), s));
+    QSIM_HIPCHK(hipMallocAsync((void**)&d_out, nshots * sizeof(int64_t), s));
+    QSIM_HIPCHK(hipMemcpyAsync(d_chunk, chunk_of.data(), nshots * sizeof(int64_t),
                                hipMemcpyHostToDevice, s));
-    QSIM_HIPCHK(hipMemcpyAsync(d_target, target.data(), shots * sizeof(double),
+    QSIM_HIPCHK(hipMemcpyAsync(d_target, target.data(), nshots * sizeof(double),
                                hipMemcpyHostToDevice, s));
-    hipLaunchKernelGGL(k_chunk_search, dim3(shots), dim3(64), 0, s, st, chunk, d_chunk, d_target,
-                       shots, total, d_out);
-    QSIM_HIPCHK(hipGetLastError());
-    QSIM_HIPCHK(hipMemcpyAsync(out, d_out, shots * sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    for (uint64_t first = 0; first < nshots; first += 0x7fffffffull) {  // grid.x limit
+        const uint64_t cnt = std::min<uint64_t>(nshots - first, 0x7fffffffull);
+        hipLaunchKernelGGL(k_chunk_search, dim3((unsigned)cnt), dim3(64), 0, s, st, chunk,
+                           d_chunk + first, d_target + first, (int)cnt, total, d_out + first);
+        QSIM_HIPCHK(hipGetLastError());
+    }
+    QSIM_HIPCHK(hipMemcpyAsync(out, d_out, nshots * sizeof(int64_t), hipMemcpyDeviceToHost, s));
     QSIM_HIPCHK(hipStreamSynchronize(s));
     QSIM_HIPCHK(hipFreeAsync(d_chunk, s));
     QSIM_HIPCHK(hipFreeAsync(d_target, s));
     QSIM_HIPCHK(hipFreeAsync(d_out, s));
+}
+
+// Histogram of sampled outcomes; indices >= N (the reference's end()) are skipped, as in
+// BatchedSimulator::getHistogram (src/NoiseModel.cu:959-972).
+__global__ __launch_bounds__(256) void k_histogram(const int64_t* idx, uint64_t count, uint64_t N,
+                                                   unsigned long long* hist) {
+    const uint64_t step = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += step) {
+        const int64_t o = idx[i];
+        if (o >= 0 && (uint64_t)o < N) atomicAdd(hist + o, 1ull);
+    }
+}
+
+void launch_histogram(const int64_t* d_idx, uint64_t count, uint64_t N, unsigned long long* d_hist,
+                      hipStream_t s) {
+    const uint64_t blocks = std::min<uint64_t>((count + 255) / 256, 256 * 32);
+    hipLaunchKernelGGL(k_histogram, dim3((unsigned)blocks), dim3(256), 0, s, d_idx, count, N, d_hist);
+    QSIM_HIPCHK(hipGetLastError());
 }
 
 // out[i] = sum_b |a_{b,i}|^2 / B, accumulated in trajectory order like the reference loop.

@@ -82,12 +82,15 @@ void NoisySimulator::applyNoiseToQubit(NoiseType type, int qubit, double probabi
 }
 
 std::vector<int> NoisySimulator::sample(int n_shots) {
-    const std::vector<double> p = getProbabilities();
-    std::vector<double> cdf(p.size());
-    std::partial_sum(p.begin(), p.end(), cdf.begin());
+    // src/NoiseModel.cu:599-613: uniforms drawn in shot order; CDF + lower_bound on the device
     std::uniform_real_distribution<double> dist(0.0, 1.0);
     std::vector<int> out(n_shots > 0 ? n_shots : 0);
-    for (int& o : out) o = (int)(std::lower_bound(cdf.begin(), cdf.end(), dist(rng_)) - cdf.begin());
+    if (out.empty()) return out;
+    std::vector<double> u(out.size());
+    for (double& r : u) r = dist(rng_);
+    std::vector<int64_t> idx(out.size());
+    check(qsim_state_sample(state_.handle(), u.data(), n_shots, idx.data()));
+    for (size_t i = 0; i < out.size(); ++i) out[i] = static_cast<int>(idx[i]);
     return out;
 }
 
@@ -169,28 +172,32 @@ std::vector<double> BatchedSimulator::getProbabilities(int t) const {
     return p;
 }
 
+// Uniforms of src/NoiseModel.cu:944-954, in its order: trajectory-major, shot by shot.
+static std::vector<double> draw_uniforms(std::mt19937& rng, int batch, int n_shots) {
+    std::uniform_real_distribution<double> dist(0.0, 1.0);
+    std::vector<double> u((size_t)batch * (size_t)n_shots);
+    for (double& r : u) r = dist(rng);
+    return u;
+}
+
 std::vector<std::vector<int>> BatchedSimulator::sample(int n_shots) {
     if (n_shots < 0) throw std::invalid_argument("n_shots must be non-negative");
     std::vector<std::vector<int>> out(n_shots, std::vector<int>(batch_size_));
-    std::uniform_real_distribution<double> dist(0.0, 1.0);
-    for (int t = 0; t < batch_size_; ++t) {
-        const std::vector<double> p = getProbabilities(t);
-        std::vector<double> cdf(p.size());
-        std::partial_sum(p.begin(), p.end(), cdf.begin());
-        for (int s = 0; s < n_shots; ++s) {
-            const double r = dist(rng_);
-            out[s][t] = (int)(std::lower_bound(cdf.begin(), cdf.end(), r) - cdf.begin());
-        }
-    }
+    if (n_shots == 0) return out;
+    const std::vector<double> u = draw_uniforms(rng_, batch_size_, n_shots);
+    std::vector<int64_t> idx(u.size());
+    check(qsim_batch_sample(h_, u.data(), n_shots, idx.data()));  // per-trajectory device CDF
+    for (int t = 0; t < batch_size_; ++t)
+        for (int s = 0; s < n_shots; ++s) out[s][t] = static_cast<int>(idx[(size_t)t * n_shots + s]);
     return out;
 }
 
 std::vector<int> BatchedSimulator::getHistogram(int n_shots) {
-    std::vector<int> hist(size_t(1) << num_qubits_, 0);
-    for (const auto& shot : sample(n_shots))
-        for (int o : shot)
-            if (o < (int)hist.size()) ++hist[o];
-    return hist;
+    if (n_shots < 0) throw std::invalid_argument("n_shots must be non-negative");
+    const std::vector<double> u = draw_uniforms(rng_, batch_size_, n_shots);
+    std::vector<int64_t> h(size_t(1) << num_qubits_, 0);
+    check(qsim_batch_histogram(h_, u.data(), n_shots, h.data()));
+    return std::vector<int>(h.begin(), h.end());
 }
 
 }  // namespace qsim

@@ -1,9 +1,18 @@
 """bench.py's N > 1 leg: the sharded state over N GPUs of one node (strong scaling: the n-qubit
 circuit is fixed, each of the N ranks holds 2^n / N amplitudes).
 
-Launched one process per GPU by `torch.distributed.run`; torch.distributed (gloo, CPU only) is
-used for the bootstrap (broadcast of the RCCL unique id), the timing barriers and the max-over-
-ranks reduction.  All state traffic goes through the engine's RCCL communicator over xGMI.
+One process per GPU (device = LOCAL_RANK), started by `torch.distributed.run` or by bench.py's
+own launcher (`qsim_amd/launch.py`, when no WORLD_SIZE is set).  The host-side rendezvous —
+broadcast of the RCCL unique id, the timing barriers, the max-over-ranks wall time — goes through
+`qsim_amd.rendezvous.FileGroup` (single node; torch is deliberately not imported next to the
+engine, see that module), every wait bounded by QSIM_DIST_INIT_TIMEOUT.  All state traffic goes
+through the engine's RCCL communicator over xGMI (non-blocking communicator, aborted on error or
+timeout, csrc/hip/dist.hip).
+
+`--dry-run` runs the same skeleton without the GPU: rendezvous, the host remap planner of this
+rank once per step (its qubit map carried from step to step as in a real run), barriers and the
+max-over-ranks timing; the JSON line says "dry_run": true and its value is planner speed, not a
+measurement of the engine.
 """
 from __future__ import annotations
 
@@ -11,29 +20,72 @@ import json
 import os
 import time
 
+from .rendezvous import FileGroup
 
-def run(args, metric: str, peak_gbps: float) -> None:
-    from . import circuit as qc
-    from .dist import DistributedSimulator, unique_id
-    import torch
-    import torch.distributed as dist
 
+def _rank_world(args):
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", str(args.gpus)))
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
-    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-    os.environ.setdefault("MASTER_PORT", "29517")
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    return rank, world, local
+
+
+def _circuit(args):
+    from . import circuit as qc
     n = args.qubits
     if args.workload == "hc":
-        circuit = qc.createRandomHCCircuit(n, args.depth, args.seed)
-        wl = f"W-HC random H+CNOT depth-{args.depth} seed {args.seed}"
-    else:
-        circuit = qc.createScalingBenchmarkCircuit(n)
-        wl = "W-REF benchmark_scaling.cu:69-76 (100 H + 20 CNOT)"
-    obj = [unique_id() if rank == 0 else None]
-    dist.broadcast_object_list(obj, src=0)
-    sim = DistributedSimulator(n, rank, world, obj[0], device=local)
+        return (qc.createRandomHCCircuit(n, args.depth, args.seed),
+                f"W-HC random H+CNOT depth-{args.depth} seed {args.seed}")
+    return qc.createScalingBenchmarkCircuit(n), "W-REF benchmark_scaling.cu:69-76 (100 H + 20 CNOT)"
+
+
+def run_dry(args, metric: str) -> None:
+    from .dist import plan
+    rank, world, _ = _rank_world(args)
+    grp = FileGroup(rank, world)
+    circuit, wl = _circuit(args)
+    n = args.qubits
+    perm = list(range(n))
+    remaps = 0
+    for _ in range(args.warmup):
+        steps, perm = plan(circuit, world, rank, perm)
+    grp.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        steps, perm = plan(circuit, world, rank, perm)
+        remaps += sum(1 for s in steps if s["kind"] == "exchange")
+    t1 = time.perf_counter()
+    grp.barrier()
+    wall = max(grp.all_reduce_max(t1 - t0), 1e-9)
+    # every rank must plan the same exchange skeleton (the lockstep contract of qsim_dist_run)
+    if grp.all_reduce_min(remaps) != grp.all_reduce_max(remaps):
+        raise RuntimeError("ranks planned different numbers of remaps")
+    if rank == 0:
+        gates = circuit.getGateCount()
+        print(json.dumps({
+            "metric": metric, "value": round(gates * args.steps / wall, 2), "unit": "gates/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(wall / args.steps * 1e3, 3), "higher_is_better": True,
+            "scaling": "strong", "vs_baseline": None, "dtype": "c128 (complex<double>)",
+            "data": "synthetic", "dry_run": True,
+            "config": {"workload": wl, "qubits": n, "gates": gates,
+                       "remaps_per_step": remaps / max(1, args.steps),
+                       "parallelism": f"dry run: host planner on {world} ranks, no GPU"},
+            "roofline": None, "cpu_baseline": None}), flush=True)
+    grp.close()
+
+
+def run(args, metric: str, peak_gbps: float) -> None:
+    if getattr(args, "dry_run", False):
+        run_dry(args, metric)
+        return
+    from .dist import DistributedSimulator, unique_id
+    rank, world, local = _rank_world(args)
+    grp = FileGroup(rank, world)
+    n = args.qubits
+    circuit, wl = _circuit(args)
+    uid = grp.broadcast(unique_id() if rank == 0 else None, src=0)
+    sim = DistributedSimulator(n, rank, world, uid, device=local)
     fused = args.mode == "fused"
     jit = getattr(args, "jit", 2)
     from .plan import set_jit
@@ -50,16 +102,14 @@ def run(args, metric: str, peak_gbps: float) -> None:
         seen.add(p)
     sim.synchronize()
     sim.profile(True)
-    dist.barrier()
+    grp.barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         sim.run(circuit, fused=fused)
     sim.synchronize()
     t1 = time.perf_counter()
-    dist.barrier()
-    wall = torch.tensor([t1 - t0], dtype=torch.float64)
-    dist.all_reduce(wall, op=dist.ReduceOp.MAX)
-    wall = float(wall.item())
+    grp.barrier()
+    wall = grp.all_reduce_max(t1 - t0)
     stats = sim.profileStats()
     gates = circuit.getGateCount()
     if rank == 0:
@@ -86,7 +136,6 @@ def run(args, metric: str, peak_gbps: float) -> None:
                        "parallelism": f"state sharded by high qubits over {world} GPUs (RCCL all-to-all remaps)"},
             "roofline": roof, "kernels_rank0": stats, "cpu_baseline": None,
         }
-        print(json.dumps(out))
+        print(json.dumps(out), flush=True)
     sim.close()
-    dist.barrier()
-    dist.destroy_process_group()
+    grp.close()

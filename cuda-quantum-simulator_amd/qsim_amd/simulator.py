@@ -212,6 +212,12 @@ class StateVector:
     def profileReset(self) -> None:
         _lib.check(_lib.hip.qsim_state_profile_reset(self._h))
 
+    def lastRunInfo(self):
+        """(tile passes, passes run by circuit-specialised kernels) of the last fused run."""
+        p, j = _c.c_int(0), _c.c_int(0)
+        _lib.check(_lib.hip.qsim_state_last_run(self._h, _c.byref(p), _c.byref(j)))
+        return p.value, j.value
+
     def profileStats(self):
         n = _c.c_int(0)
         _lib.check(_lib.hip.qsim_state_profile_count(self._h, _c.byref(n)))
@@ -390,9 +396,10 @@ class NoisySimulator:
     def getProbabilities(self) -> np.ndarray: return self._state.getProbabilities()
 
     def sample(self, n_shots: int) -> np.ndarray:
-        """Host CDF + lower_bound like the reference (src/NoiseModel.cu:599-613)."""
-        cdf = np.cumsum(self.getProbabilities())
-        return np.searchsorted(cdf, self._rng.random(n_shots), side="left").astype(np.int64)
+        """CDF + lower_bound like the reference (src/NoiseModel.cu:599-613), on the device."""
+        if n_shots <= 0:
+            return np.empty(0, dtype=np.int64)
+        return self._state.sampleWith(self._rng.random(n_shots))
 
     def measureQubit(self, qubit: int) -> int:
         p0 = self._state.probBitZero(qubit)
@@ -472,18 +479,34 @@ class BatchedSimulator:
         _lib.check(_lib.hip.qsim_batch_traj_state(self._h, t, _ptr(out)))
         return out
 
-    def sample(self, n_shots: int) -> np.ndarray:
-        """[shot][trajectory] outcomes: per-trajectory CDF + lower_bound (NoiseModel.cu:938-957)."""
-        out = np.empty((n_shots, self._b), dtype=np.int64)
-        for t in range(self._b):
-            cdf = np.cumsum(self.getProbabilities(t))
-            out[:, t] = np.searchsorted(cdf, self._rng.random(n_shots), side="left")
+    def sampleWith(self, uniforms: np.ndarray) -> np.ndarray:
+        """Device sampling with given uniforms, shape (B, shots) trajectory-major; returns the
+        (B, shots) outcomes (lower_bound over each trajectory's CDF, 2^n past its end)."""
+        u = np.ascontiguousarray(uniforms, dtype=np.float64)
+        if u.ndim != 2 or u.shape[0] != self._b:
+            raise ValueError("uniforms must have shape (batch_size, shots)")
+        out = np.empty(u.shape, dtype=np.int64)
+        _lib.check(_lib.hip.qsim_batch_sample(self._h, _ptr(u), int(u.shape[1]), _ptr(out)))
         return out
 
+    def _draw(self, n_shots: int) -> np.ndarray:
+        if n_shots < 0:
+            raise ValueError("n_shots must be non-negative")
+        # the reference draws shot by shot inside the trajectory loop (NoiseModel.cu:944-954)
+        return self._rng.random((self._b, n_shots))
+
+    def sample(self, n_shots: int) -> np.ndarray:
+        """[shot][trajectory] outcomes: per-trajectory CDF + lower_bound (NoiseModel.cu:938-957),
+        on the device."""
+        return np.ascontiguousarray(self.sampleWith(self._draw(n_shots)).T)
+
     def getHistogram(self, n_shots: int) -> np.ndarray:
-        s = self.sample(n_shots).ravel()
-        s = s[s < (1 << self._n)]
-        return np.bincount(s, minlength=1 << self._n).astype(np.int64)
+        """Counts over every trajectory and shot, out-of-range outcomes skipped
+        (NoiseModel.cu:959-972); sampling and counting on the device."""
+        u = np.ascontiguousarray(self._draw(n_shots))
+        hist = np.empty(1 << self._n, dtype=np.int64)
+        _lib.check(_lib.hip.qsim_batch_histogram(self._h, _ptr(u), int(n_shots), _ptr(hist)))
+        return hist
 
     def getNumQubits(self) -> int: return self._n
     def getBatchSize(self) -> int: return self._b

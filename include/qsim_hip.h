@@ -158,6 +158,9 @@ int qsim_state_profile_count(qsim_state* s, int* n);
 int qsim_state_profile_get(qsim_state* s, int i, char* name, size_t name_len,
                            double* total_ms, int64_t* launches, double* alg_bytes);
 int qsim_state_profile_reset(qsim_state* s);
+/* Introspection of the last fused qsim_run on this state: tile passes planned and how many ran
+ * as circuit-specialised (hipRTC) kernels rather than the pass interpreter. */
+int qsim_state_last_run(qsim_state* s, int* passes, int* jit_passes);
 
 /* ---- batched trajectories (BatchedSimulator, include/NoiseModel.cuh:231-297) ---- */
 /* Noise channel on one qubit, NoiseType numbering == reference enum (NoiseModel.cuh:49-56). */
@@ -183,6 +186,13 @@ int qsim_batch_run(qsim_batch* b, const qsim_gate* gates, size_t count,
 int qsim_batch_avg_probabilities(qsim_batch* b, double* dst);           /* 2^n */
 int qsim_batch_traj_probabilities(qsim_batch* b, int traj, double* dst);  /* 2^n */
 int qsim_batch_traj_state(qsim_batch* b, int traj, double* dst);          /* 2*2^n */
+/* BatchedSimulator::sample (src/NoiseModel.cu:938-957) on the device: uniforms and out are
+ * trajectory-major, B x shots (shot s of trajectory t at t*shots + s — the reference's draw
+ * order); out = lower_bound of the uniform over the trajectory's CDF, 2^n when past its end. */
+int qsim_batch_sample(qsim_batch* b, const double* uniforms, int shots, int64_t* out);
+/* BatchedSimulator::getHistogram (src/NoiseModel.cu:959-972): counts of the sampled outcomes
+ * over every trajectory and shot, out-of-range outcomes skipped; hist has 2^n entries. */
+int qsim_batch_histogram(qsim_batch* b, const double* uniforms, int shots, int64_t* hist);
 int qsim_batch_device_ptr(qsim_batch* b, void** dptr);
 int qsim_batch_sync(qsim_batch* b);
 int qsim_batch_profile(qsim_batch* b, int enable);

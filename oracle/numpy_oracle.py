@@ -221,7 +221,7 @@ def noise_pass(state, n, ntype, q, p, seed, counter):
     i1 = i0 | (1 << q)
     a0, a1 = s[i0].copy(), s[i1].copy()
     if ntype in (0, 3, 4, 5):
-        fire = r1 < np.float32(p)
+        fire = r1.astype(np.float64) < float(p)  # float draw promoted to double (NoiseModel.cu:195)
         if ntype == 0:
             r2 = _uniform(_mix_np(h ^ np.uint64(0x5bd1e9955bd1e995)))
             pauli = np.where(r2 < np.float32(1.0) / np.float32(3.0), 1,

@@ -1,0 +1,10 @@
+#!/bin/bash
+# Quick GPU check: the -m gpu parity suite and the default bench line.
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+O=$R/gpurun_out/check
+mkdir -p $O
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1; rc=$?
+tail -3 $O/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python bench.py --cpu-budget 2 > $O/bench30.json 2> $O/bench30.err || exit 1
+cat $O/bench30.json

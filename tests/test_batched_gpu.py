@@ -101,3 +101,59 @@ def test_frames_noise_actually_applied(qsim, gpu_ready):
     ideal.applyGate(qsim.GateOp(qsim.GateType.X, [0]))
     for t in range(B):
         np.testing.assert_allclose(s.getStateVector(t), ideal.getStateVector(), atol=1e-12, rtol=0)
+
+
+# ---- BASELINE config 4: 16 qubits x 1024 trajectories ("config 4 has no GPU test")
+def test_config4_noise_free_matches_oracle(qsim, oracle, gpu_ready):
+    """16q x 1024 trajectories (1 GiB of states), W-HC depth 100: a fixed sample of 64
+    trajectories (first, last and 62 spread between) equals the oracle state at 1e-12."""
+    n, B = 16, 1024
+    c = qsim.createRandomHCCircuit(n, 100, 42)
+    s = qsim.BatchedSimulator(n, B)
+    s.run(c)
+    ref = oracle.run_cpu(n, oracle.gates_of(c))
+    for t in sorted({0, B - 1, *np.linspace(0, B - 1, 62).astype(int).tolist()}):
+        np.testing.assert_allclose(s.getStateVector(t), ref, atol=1e-12, rtol=0)
+    np.testing.assert_allclose(s.getAverageProbabilities(), np.abs(ref) ** 2, atol=1e-12)
+
+
+def test_config4_noisy_frames_equal_per_gate(qsim, gpu_ready):
+    """16q, depolarizing 0.01 on every qubit after every gate (W-BATCH's noise), 64 trajectories:
+    the fused Pauli-frame execution == one kernel per gate + one Pauli pass per step."""
+    n, B = 16, 64
+    c = qsim.createRandomHCCircuit(n, 100, 42)
+    nm = qsim.NoiseModel()
+    nm.addDepolarizingAll(n, 0.01)
+    fused, ref = qsim.BatchedSimulator(n, B, nm), qsim.BatchedSimulator(n, B, nm)
+    fused.setSeed(42)
+    ref.setSeed(42)
+    fused.run(c)
+    ref.run(c, per_gate=True)
+    differ = 0
+    ideal = qsim.BatchedSimulator(n, 1)
+    ideal.run(c)
+    psi = ideal.getStateVector(0)
+    for t in range(B):
+        a = fused.getStateVector(t)
+        np.testing.assert_allclose(a, ref.getStateVector(t), atol=1e-12, rtol=0)
+        differ += np.max(np.abs(a - psi)) > 1e-9
+    # 16 x 100 channels at p = 0.01: a trajectory stays error-free with prob ~1e-7
+    assert differ >= B - 2
+
+
+def test_config4_full_size_noisy_run(qsim, gpu_ready):
+    """The W-BATCH configuration itself (16q x 1024, depolarizing 0.01 everywhere): every
+    trajectory stays normalised and the average distribution is a distribution."""
+    n, B = 16, 1024
+    c = qsim.createRandomHCCircuit(n, 100, 42)
+    nm = qsim.NoiseModel()
+    nm.addDepolarizingAll(n, 0.01)
+    s = qsim.BatchedSimulator(n, B, nm)
+    s.setSeed(42)
+    s.run(c)
+    avg = s.getAverageProbabilities()
+    assert abs(avg.sum() - 1.0) < 1e-10 and avg.min() >= 0
+    for t in (0, 511, 1023):
+        assert abs(np.sum(np.abs(s.getStateVector(t)) ** 2) - 1.0) < 1e-10
+    h = s.getHistogram(4)
+    assert h.sum() == 4 * B

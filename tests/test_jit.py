@@ -137,3 +137,34 @@ def test_full_size_paths_agree(qsim, gpu_ready, n):
         set_jit(1, 20)
     np.testing.assert_allclose(states[1], states[0], atol=1e-12, rtol=0)
     np.testing.assert_allclose(states[2], states[0], atol=1e-12, rtol=0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("jit", [0, 2])
+def test_many_h_in_one_pass_stay_finite(qsim, gpu_ready, jit):
+    """a pass runs uncontrolled H as unnormalised butterflies (norm x sqrt2 each) and
+    rescales at the store; the planner caps them per pass (the rest run as the normalised
+    matrix), so 4000 H on a 12-qubit state (one tile, one pass) stay finite: H.H pairs = identity."""
+    from qsim_amd.plan import set_jit
+    n = 12
+    rng = np.random.default_rng(4)
+    c = qsim.Circuit(n)
+    for _ in range(2000):
+        q = int(rng.integers(0, n))
+        c.h(q).h(q)
+    psi = rng.normal(size=1 << n) + 1j * rng.normal(size=1 << n)
+    psi /= np.linalg.norm(psi)
+    try:
+        set_jit(jit, 0)
+        sim = qsim.Simulator(n, mode=qsim.RunMode.Fused)
+        sim.state.fromHost(psi)
+        sim.run(c)
+        got = sim.getStateVector()
+    finally:
+        set_jit(1, 20)
+    assert np.all(np.isfinite(got))
+    np.testing.assert_allclose(got, psi, atol=1e-11, rtol=0)
+    zero = qsim.Simulator(n, mode=qsim.RunMode.Fused)
+    zero.run(c)
+    p = zero.getProbabilities()
+    assert abs(p[0] - 1.0) < 1e-10

@@ -1,0 +1,89 @@
+"""CPU: bench.py's N-rank launch contract (no GPU).
+
+* `bench.py --gpus N --dry-run` with no WORLD_SIZE self-launches N rank processes
+  (qsim_amd/launch.py), runs the sharded bench skeleton (rendezvous, per-rank host remap planner,
+  barriers, max-over-ranks timing) and prints exactly ONE JSON line from rank 0.
+* A failing rank makes the launcher stop its peers and exit non-zero; a rank that never arrives
+  makes the rendezvous raise instead of hanging.
+"""
+import json
+import os
+import subprocess
+import sys
+import tempfile
+import time
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BENCH = os.path.join(ROOT, "bench.py")
+
+
+def _env():
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT", "QSIM_RDZV_KEY"):
+        env.pop(k, None)
+    return env
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_dry_run_launch_prints_one_json_line(world):
+    r = subprocess.run([sys.executable, BENCH, "--gpus", str(world), "--dry-run", "--steps", "2",
+                        "--warmup", "1", "--qubits", "24"], capture_output=True, text=True,
+                       timeout=300, env=_env())
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == world and out["dry_run"] is True
+    assert out["steps"] == 2 and out["value"] > 0 and out["scaling"] == "strong"
+    assert out["config"]["remaps_per_step"] >= 1  # W-HC at 24q needs at least one remap per run
+
+
+def test_failing_rank_stops_launch():
+    sys.path.insert(0, os.path.join(ROOT, "cuda-quantum-simulator_amd"))
+    from qsim_amd.launch import launch_ranks
+    with tempfile.TemporaryDirectory() as d:
+        script = os.path.join(d, "rank.py")
+        with open(script, "w") as f:
+            f.write("import os, sys, time\n"
+                    "r = int(os.environ['RANK'])\n"
+                    "if r == 1: sys.exit(3)\n"
+                    "time.sleep(120)\n")
+        t0 = time.time()
+        rc = launch_ranks(script, [], 3, timeout_s=100)
+        assert rc == 3
+        assert time.time() - t0 < 60  # the sleeping ranks were stopped, not waited for
+
+
+def test_rendezvous_times_out_on_missing_rank():
+    sys.path.insert(0, os.path.join(ROOT, "cuda-quantum-simulator_amd"))
+    from qsim_amd.rendezvous import FileGroup
+    with tempfile.TemporaryDirectory() as d:
+        g = FileGroup(0, 2, key="t", timeout_s=0.5, root=d)
+        with pytest.raises(TimeoutError):
+            g.barrier()
+
+
+def test_rendezvous_collectives_in_process():
+    sys.path.insert(0, os.path.join(ROOT, "cuda-quantum-simulator_amd"))
+    from qsim_amd.rendezvous import FileGroup
+    import threading
+    with tempfile.TemporaryDirectory() as d:
+        res = {}
+
+        def rank(r):
+            g = FileGroup(r, 3, key="c", timeout_s=30, root=d)
+            uid = g.broadcast(b"id-bytes" if r == 0 else None)
+            m = g.all_reduce_max(float(r) * 1.5)
+            lo = g.all_reduce_min(float(r) + 2)
+            g.close()
+            res[r] = (uid, m, lo)
+
+        ts = [threading.Thread(target=rank, args=(r,)) for r in range(3)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join(60)
+        assert res == {r: (b"id-bytes", 3.0, 2.0) for r in range(3)}
+        assert not os.path.exists(os.path.join(d, "qsim_rdzv_c"))

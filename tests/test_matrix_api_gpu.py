@@ -71,3 +71,35 @@ def test_diagonal_layer_matches_numpy(qsim, gpu_ready, n):
         if (active >> q) & 1:
             want = want * np.where((idx >> q) & 1, params[q, 3], params[q, 0])
     np.testing.assert_allclose(sv.toHost(), want, atol=1e-12 * np.max(np.abs(want)) * 10, rtol=1e-12)
+
+
+def _numpy_controlled_1q(state, n, target, m, controls):
+    out = state.copy()
+    idx = np.arange(1 << n)
+    sel = np.ones(1 << n, bool)
+    for c in controls:
+        sel &= ((idx >> c) & 1) == 1
+    i0 = idx[sel & (((idx >> target) & 1) == 0)]
+    i1 = i0 | (1 << target)
+    a0, a1 = state[i0], state[i1]
+    out[i0] = m[0, 0] * a0 + m[0, 1] * a1
+    out[i1] = m[1, 0] * a0 + m[1, 1] * a1
+    return out
+
+
+@pytest.mark.parametrize("target,controls", [(7, [6, 8, 9]), (2, [6, 7, 8, 9]), (9, [0, 6, 7, 8]),
+                                             (11, [6, 7, 8, 9, 10]), (3, [0, 1, 6, 7, 8, 10, 11])])
+def test_matrix1q_many_high_controls(qsim, gpu_ready, target, controls):
+    """more fixed high positions than the wave-item kernels hold (3) -> general
+    kernel; checked against numpy on a random state."""
+    n = 12
+    rng = np.random.default_rng(target * 31 + len(controls))
+    psi = rng.normal(size=1 << n) + 1j * rng.normal(size=1 << n)
+    psi /= np.linalg.norm(psi)
+    a = rng.normal(size=(2, 2)) + 1j * rng.normal(size=(2, 2))
+    u, _ = np.linalg.qr(a)
+    sv = qsim.StateVector(n)
+    sv.fromHost(psi)
+    sv.applyMatrix1Q(target, u, controls)
+    np.testing.assert_allclose(sv.toHost(), _numpy_controlled_1q(psi, n, target, u, controls),
+                               atol=1e-12, rtol=0)
