@@ -193,6 +193,7 @@ struct qsim_batch {
     DevBuf ops, stages;             // fused-plan descriptors
     PlanCache plans;
     Timer timer;
+    Scratch scratch, scratch2;
     ~qsim_batch() {
         if (stream) (void)hipStreamSynchronize(stream);
         if (d) (void)hipFree(d);
@@ -344,7 +345,7 @@ int qsim_batch_run(qsim_batch* b, const qsim_gate* gates, size_t count,
                 QSIM_HIPCHK(hipGetLastError());
             }
             if (!fops.empty()) {
-                const Plan& plan = b->plans.get(fops, b->n).plan;
+                const Plan& plan = b->plans.get(fops, b->n, b->stream).plan;
                 b->ops.upload(plan.ops.data(), plan.ops.size() * sizeof(TileOp), b->stream);
                 b->stages.upload(plan.stages.data(), plan.stages.size() * sizeof(Stage), b->stream);
                 launch_fused(b->d, b->n, (uint64_t)b->batch, plan, (const TileOp*)b->ops.ptr,
@@ -386,11 +387,9 @@ int qsim_batch_avg_probabilities(qsim_batch* b, double* dst) {
     return bguard([&] {
         need(b);
         const uint64_t N = 1ull << b->n;
-        double* d_p = nullptr;
-        QSIM_HIPCHK(hipMallocAsync((void**)&d_p, N * sizeof(double), b->stream));
+        double* d_p = (double*)b->scratch.get(N * sizeof(double), b->stream);
         launch_avg_probabilities(b->d, b->n, (uint64_t)b->batch, d_p, b->stream);
         QSIM_HIPCHK(hipMemcpyAsync(dst, d_p, N * sizeof(double), hipMemcpyDeviceToHost, b->stream));
-        QSIM_HIPCHK(hipFreeAsync(d_p, b->stream));
         QSIM_HIPCHK(hipStreamSynchronize(b->stream));
     });
 }
@@ -400,11 +399,9 @@ int qsim_batch_traj_probabilities(qsim_batch* b, int traj, double* dst) {
         need(b);
         if (traj < 0 || traj >= b->batch) fail(QSIM_ERR_OUT_OF_RANGE, "Invalid trajectory index");
         const uint64_t N = 1ull << b->n;
-        double* d_p = nullptr;
-        QSIM_HIPCHK(hipMallocAsync((void**)&d_p, N * sizeof(double), b->stream));
+        double* d_p = (double*)b->scratch.get(N * sizeof(double), b->stream);
         launch_probabilities(b->d + (uint64_t)traj * N, N, d_p, b->stream);
         QSIM_HIPCHK(hipMemcpyAsync(dst, d_p, N * sizeof(double), hipMemcpyDeviceToHost, b->stream));
-        QSIM_HIPCHK(hipFreeAsync(d_p, b->stream));
         QSIM_HIPCHK(hipStreamSynchronize(b->stream));
     });
 }
@@ -414,7 +411,7 @@ int qsim_batch_sample(qsim_batch* b, const double* uniforms, int shots, int64_t*
         need(b);
         if (shots < 0) fail(QSIM_ERR_INVALID_ARGUMENT, "n_shots must be non-negative");
         if (shots > 0 && (!uniforms || !out)) fail(QSIM_ERR_INVALID_ARGUMENT, "null buffer");
-        sample_indices(b->d, b->n, (uint64_t)b->batch, uniforms, shots, out, b->stream);
+        sample_indices(b->d, b->n, (uint64_t)b->batch, uniforms, shots, out, b->stream, b->scratch);
     });
 }
 
@@ -425,11 +422,12 @@ int qsim_batch_histogram(qsim_batch* b, const double* uniforms, int shots, int64
         if (!hist || (shots > 0 && !uniforms)) fail(QSIM_ERR_INVALID_ARGUMENT, "null buffer");
         const uint64_t N = 1ull << b->n, nshots = (uint64_t)shots * (uint64_t)b->batch;
         std::vector<int64_t> idx(nshots);
-        sample_indices(b->d, b->n, (uint64_t)b->batch, uniforms, shots, idx.data(), b->stream);
-        int64_t* d_idx = nullptr;
-        unsigned long long* d_h = nullptr;
-        QSIM_HIPCHK(hipMallocAsync((void**)&d_idx, std::max<uint64_t>(1, nshots) * sizeof(int64_t), b->stream));
-        QSIM_HIPCHK(hipMallocAsync((void**)&d_h, N * sizeof(unsigned long long), b->stream));
+        sample_indices(b->d, b->n, (uint64_t)b->batch, uniforms, shots, idx.data(), b->stream,
+                       b->scratch);
+        // counts on the device: scratch2 = [hist N x u64][indices nshots x i64]
+        char* base = (char*)b->scratch2.get(N * 8 + std::max<uint64_t>(1, nshots) * 8, b->stream);
+        unsigned long long* d_h = (unsigned long long*)base;
+        int64_t* d_idx = (int64_t*)(base + N * 8);
         QSIM_HIPCHK(hipMemsetAsync(d_h, 0, N * sizeof(unsigned long long), b->stream));
         if (nshots) {
             QSIM_HIPCHK(hipMemcpyAsync(d_idx, idx.data(), nshots * sizeof(int64_t),
@@ -437,8 +435,6 @@ int qsim_batch_histogram(qsim_batch* b, const double* uniforms, int shots, int64
             launch_histogram(d_idx, nshots, N, d_h, b->stream);
         }
         QSIM_HIPCHK(hipMemcpyAsync(hist, d_h, N * sizeof(int64_t), hipMemcpyDeviceToHost, b->stream));
-        QSIM_HIPCHK(hipFreeAsync(d_idx, b->stream));
-        QSIM_HIPCHK(hipFreeAsync(d_h, b->stream));
         QSIM_HIPCHK(hipStreamSynchronize(b->stream));
     });
 }

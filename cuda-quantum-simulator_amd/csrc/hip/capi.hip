@@ -116,6 +116,23 @@ void DevBuf::upload(const void* src, size_t bytes, hipStream_t s) {
     if (!copied) QSIM_HIPCHK(hipEventCreateWithFlags(&copied, hipEventDisableTiming));
     QSIM_HIPCHK(hipEventRecord(copied, s));
 }
+void* Scratch::get(size_t bytes, hipStream_t s) {
+    bytes = std::max<size_t>(bytes, 256);
+    if (bytes > cap) {
+        if (ptr) {
+            QSIM_HIPCHK(hipStreamSynchronize(s));
+            QSIM_HIPCHK(hipFree(ptr));
+            ptr = nullptr;
+            cap = 0;
+        }
+        QSIM_HIPCHK(hipMalloc(&ptr, bytes));
+        cap = bytes;
+    }
+    return ptr;
+}
+Scratch::~Scratch() {
+    if (ptr) (void)hipFree(ptr);
+}
 DevBuf::~DevBuf() {
     if (copied) {
         (void)hipEventSynchronize(copied);
@@ -155,6 +172,7 @@ struct qsim_state {
     PlanCache plans;
     Timer timer;
     int last_passes = 0, last_jit_passes = 0;  // of the last fused run (qsim_state_last_run)
+    Scratch scratch;
     ~qsim_state() {
         if (stream) (void)hipStreamSynchronize(stream);
         if (d) (void)hipFree(d);
@@ -181,7 +199,7 @@ static void check_state(const qsim_state* s) {
 }
 
 static void run_fused(qsim_state* s, const std::vector<Op>& ops) {
-    PlanCache::Entry& pe = s->plans.get(ops, s->n);
+    PlanCache::Entry& pe = s->plans.get(ops, s->n, s->stream);
     const Plan& plan = pe.plan;
     const JitModule* jm = jit_for(pe.jit, plan, s->n);
     s->ops.upload(plan.ops.data(), plan.ops.size() * sizeof(TileOp), s->stream);
@@ -535,11 +553,9 @@ int qsim_state_probabilities(qsim_state* s, double* dst) {
         QSIM_REQUIRE(dst, QSIM_ERR_INVALID_ARGUMENT, "null destination");
         DeviceGuard dg(s->device);
         const uint64_t N = 1ull << s->n;
-        double* d_p = nullptr;
-        QSIM_HIPCHK(hipMallocAsync((void**)&d_p, N * sizeof(double), s->stream));
+        double* d_p = (double*)s->scratch.get(N * sizeof(double), s->stream);
         launch_probabilities(s->d, N, d_p, s->stream);
         QSIM_HIPCHK(hipMemcpyAsync(dst, d_p, N * sizeof(double), hipMemcpyDeviceToHost, s->stream));
-        QSIM_HIPCHK(hipFreeAsync(d_p, s->stream));
         QSIM_HIPCHK(hipStreamSynchronize(s->stream));
     });
 }
@@ -580,7 +596,7 @@ int qsim_state_sample(qsim_state* s, const double* uniforms, int shots, int64_t*
         if (shots <= 0) fail(QSIM_ERR_INVALID_ARGUMENT, "n_shots must be positive");
         QSIM_REQUIRE(uniforms && out, QSIM_ERR_INVALID_ARGUMENT, "null buffer");
         DeviceGuard dg(s->device);
-        sample_indices(s->d, s->n, 1, uniforms, shots, out, s->stream);
+        sample_indices(s->d, s->n, 1, uniforms, shots, out, s->stream, s->scratch);
     });
 }
 
@@ -663,11 +679,9 @@ int qsim_dm_diagonal(qsim_state* s, int n, double* dst) {
         check_dm(s, n);
         QSIM_REQUIRE(dst, QSIM_ERR_INVALID_ARGUMENT, "null destination");
         DeviceGuard dg(s->device);
-        double* d_p = nullptr;
-        QSIM_HIPCHK(hipMallocAsync((void**)&d_p, sizeof(double) << n, s->stream));
+        double* d_p = (double*)s->scratch.get(sizeof(double) << n, s->stream);
         launch_dm_diag(s->d, n, d_p, s->stream);
         QSIM_HIPCHK(hipMemcpyAsync(dst, d_p, sizeof(double) << n, hipMemcpyDeviceToHost, s->stream));
-        QSIM_HIPCHK(hipFreeAsync(d_p, s->stream));
         QSIM_HIPCHK(hipStreamSynchronize(s->stream));
     });
 }
@@ -677,11 +691,9 @@ int qsim_dm_init_pure(qsim_state* s, int n, const double* psi) {
         check_dm(s, n);
         QSIM_REQUIRE(psi, QSIM_ERR_INVALID_ARGUMENT, "null state");
         DeviceGuard dg(s->device);
-        double2* d_psi = nullptr;
-        QSIM_HIPCHK(hipMallocAsync((void**)&d_psi, sizeof(double2) << n, s->stream));
+        double2* d_psi = (double2*)s->scratch.get(sizeof(double2) << n, s->stream);
         QSIM_HIPCHK(hipMemcpyAsync(d_psi, psi, sizeof(double2) << n, hipMemcpyHostToDevice, s->stream));
         launch_dm_init(s->d, d_psi, n, s->stream);
-        QSIM_HIPCHK(hipFreeAsync(d_psi, s->stream));
         QSIM_HIPCHK(hipStreamSynchronize(s->stream));
     });
 }

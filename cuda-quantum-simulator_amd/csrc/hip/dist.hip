@@ -632,7 +632,7 @@ double allreduce_sum(qsim_dist* d, double local) {
 }
 void run_local(qsim_dist* d, Shard& sh, const std::vector<Op>& ops, int flags, PlanCache& pc) {
     if (flags & QSIM_RUN_FUSED) {
-        PlanCache::Entry& pe = pc.get(ops, d->L);
+        PlanCache::Entry& pe = pc.get(ops, d->L, d->stream);
         const Plan& plan = pe.plan;
         const JitModule* jm = jit_for(pe.jit, plan, d->L);
         d->ops.upload(plan.ops.data(), plan.ops.size() * sizeof(TileOp), d->stream);
@@ -666,6 +666,7 @@ qsim_dist::RunPlan& run_plan(qsim_dist* d, const qsim_gate* gates, size_t count)
     if (d->run_plans.size() >= 8) {
         auto lru = std::min_element(d->run_plans.begin(), d->run_plans.end(),
                                     [](const auto& a, const auto& b) { return a->used < b->used; });
+        QSIM_HIPCHK(hipStreamSynchronize(d->stream));  // its compiled kernels may still be queued
         d->run_plans.erase(lru);
     }
     d->run_plans.push_back(std::move(rp));

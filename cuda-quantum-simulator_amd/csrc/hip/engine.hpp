@@ -146,7 +146,6 @@ Plan plan_fused(const std::vector<Op>& ops, int n, int hmax = -1);
 struct JitJob;
 struct JitModule {
     hipModule_t mod = nullptr;
-    int device = -1;                // unload waits for this device's queued kernels
     std::vector<hipFunction_t> fn;  // per plan pass; null = run by the interpreter
     ~JitModule();
 };
@@ -177,7 +176,8 @@ struct PlanCache {
     static constexpr size_t kEntries = 4;
     std::vector<std::unique_ptr<Entry>> entries;
     uint64_t clock = 0;
-    Entry& get(const std::vector<Op>& ops, int n_qubits);
+    // stream: where the owner runs this cache's plans (drained before a plan is evicted)
+    Entry& get(const std::vector<Op>& ops, int n_qubits, hipStream_t stream);
 };
 // frames != null: batched noisy run under per-trajectory Pauli frames (FArgs::frames).
 void launch_fused(double2* st, int n, uint64_t batch, const Plan& plan, const TileOp* d_ops,
@@ -203,10 +203,11 @@ void launch_probabilities(const double2* st, uint64_t count, double* out, hipStr
 double reduce_norm(const double2* st, int n, int bit, double* d_partials, double* d_result,
                    hipStream_t s);
 void launch_collapse(double2* st, int n, int bit, int result, double scale, hipStream_t s);
+struct Scratch;
 void launch_histogram(const int64_t* d_idx, uint64_t count, uint64_t N, unsigned long long* d_hist,
                       hipStream_t s);
 void sample_indices(const double2* st, int n, uint64_t batch, const double* uniforms, int shots,
-                    int64_t* out, hipStream_t s);
+                    int64_t* out, hipStream_t s, Scratch& scratch);
 // Average of |a|^2 over `batch` trajectories into out[2^n] (device).
 void launch_avg_probabilities(const double2* st, int n, uint64_t batch, double* out,
                               hipStream_t s);
@@ -239,6 +240,17 @@ struct DevBuf {
     hipEvent_t copied = nullptr;
     void upload(const void* src, size_t bytes, hipStream_t s);
     ~DevBuf();
+};
+
+// Grow-only device scratch of one engine object (readback / sampling temporaries).  Every user
+// synchronises its stream before returning, so the next user may reuse the memory; growing
+// waits for the stream before the old block is freed.  (Plain hipMalloc memory: the
+// stream-ordered pool is not used for buffers that pageable host copies read or write.)
+struct Scratch {
+    void* ptr = nullptr;
+    size_t cap = 0;
+    void* get(size_t bytes, hipStream_t s);
+    ~Scratch();
 };
 
 // RAII scope used around each launch.

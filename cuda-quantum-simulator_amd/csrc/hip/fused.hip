@@ -449,7 +449,7 @@ static bool same_op(const Op& a, const Op& b) {
     return true;
 }
 
-PlanCache::Entry& PlanCache::get(const std::vector<Op>& ops, int n_qubits) {
+PlanCache::Entry& PlanCache::get(const std::vector<Op>& ops, int n_qubits, hipStream_t stream) {
     for (auto& e : entries) {
         bool hit = e->n == n_qubits && e->key.size() == ops.size();
         for (size_t i = 0; hit && i < ops.size(); ++i) hit = same_op(e->key[i], ops[i]);
@@ -462,6 +462,7 @@ PlanCache::Entry& PlanCache::get(const std::vector<Op>& ops, int n_qubits) {
                                        // ~JitModule waits for the device before unloading it)
         auto lru = std::min_element(entries.begin(), entries.end(),
                                     [](const auto& a, const auto& b) { return a->used < b->used; });
+        if ((*lru)->jit.mod) QSIM_HIPCHK(hipStreamSynchronize(stream));  // its kernels may be queued
         entries.erase(lru);
     }
     auto e = std::make_unique<Entry>();

@@ -300,14 +300,42 @@ void gen_pass(std::ostringstream& out, const Plan& plan, const FusedPass& p, int
 
 }  // namespace
 
-bool jit_pass_eligible(const FusedPass& p) { return p.single < 0 && p.h >= 4; }
+// Passes with very many ops stay on the interpreter: straight-line code grows with every op
+// (each expanded over its register pairs) and hipRTC time with it; past ~kJitMaxOps ops the
+// pass is VALU-heavy anyway and the per-op dispatch of the interpreter matters less.
+constexpr int kJitMaxOps = 192;
+static int pass_ops(const Plan& plan, const FusedPass& p) {
+    int ops = 0;
+    for (int k = p.stage_begin; k < p.stage_end; ++k) ops += plan.stages[k].op_end - plan.stages[k].op_begin;
+    return ops;
+}
+static bool jit_pass_eligible(const Plan& plan, const FusedPass& p) {
+    return p.single < 0 && p.h >= 4 && pass_ops(plan, p) <= kJitMaxOps;
+}
+// The passes one code object specialises: eligible passes in plan order while the module stays
+// within kJitModuleOps ops (bounds hipRTC time — also for the background worker, which a
+// process exit waits for); later passes run on the interpreter.
+constexpr int kJitModuleOps = 2048;
+static std::vector<char> jit_selection(const Plan& plan) {
+    std::vector<char> sel(plan.passes.size(), 0);
+    int budget = kJitModuleOps;
+    for (size_t i = 0; i < plan.passes.size(); ++i) {
+        if (!jit_pass_eligible(plan, plan.passes[i])) continue;
+        const int ops = pass_ops(plan, plan.passes[i]);
+        if (ops > budget) break;
+        budget -= ops;
+        sel[i] = 1;
+    }
+    return sel;
+}
 
 std::string jit_source(const Plan& plan) {
     std::ostringstream out;
     bool any = false;
     out << kPrelude;
+    const std::vector<char> sel = jit_selection(plan);
     for (size_t i = 0; i < plan.passes.size(); ++i) {
-        if (!jit_pass_eligible(plan.passes[i])) continue;
+        if (!sel[i]) continue;
         gen_pass(out, plan, plan.passes[i], (int)i);
         any = true;
     }
@@ -398,14 +426,9 @@ private:
 }  // namespace
 
 JitModule::~JitModule() {
-    if (!mod) return;
-    // kernels of this module may still be queued on the engine's stream: drain the device first
-    int cur = -1;
-    (void)hipGetDevice(&cur);
-    if (device >= 0 && device != cur) (void)hipSetDevice(device);
-    (void)hipDeviceSynchronize();
-    (void)hipModuleUnload(mod);
-    if (device >= 0 && device != cur && cur >= 0) (void)hipSetDevice(cur);
+    // the owner has drained the stream that ran this module's kernels (engine destructors
+    // synchronise first; PlanCache::get synchronises before it evicts a plan)
+    if (mod) (void)hipModuleUnload(mod);
 }
 
 const JitModule* jit_for(JitState& js, const Plan& plan, int n) {
@@ -436,11 +459,11 @@ const JitModule* jit_for(JitState& js, const Plan& plan, int n) {
         return nullptr;
     }
     auto m = std::make_unique<JitModule>();
-    QSIM_HIPCHK(hipGetDevice(&m->device));
     QSIM_HIPCHK(hipModuleLoadData(&m->mod, js.job->code.data()));
     m->fn.assign(plan.passes.size(), nullptr);
+    const std::vector<char> sel = jit_selection(plan);
     for (size_t i = 0; i < plan.passes.size(); ++i) {
-        if (!jit_pass_eligible(plan.passes[i])) continue;
+        if (!sel[i]) continue;
         const std::string name = "qk" + std::to_string(i);
         QSIM_HIPCHK(hipModuleGetFunction(&m->fn[i], m->mod, name.c_str()));
     }

@@ -202,22 +202,25 @@ __global__ __launch_bounds__(64) void k_chunk_search(const double2* st, uint64_t
 // then differ from the reference's sequential partial_sum only where the uniform lies between
 // the exact and the sequentially rounded CDF at a step (tests/test_sampling_gpu.py checks that).
 void sample_indices(const double2* st, int n, uint64_t batch, const double* uniforms, int shots,
-                    int64_t* out, hipStream_t s) {
+                    int64_t* out, hipStream_t s, Scratch& scratch) {
     if (shots <= 0 || batch == 0) return;
     const uint64_t total = 1ull << n;
     const uint64_t chunk = 1ull << std::min(n, kChunkLog);
     const uint64_t nchunks = total / chunk;  // per trajectory
     const uint64_t all_chunks = nchunks * batch;
     const uint64_t nshots = (uint64_t)shots * batch;
-    double* d_sums = nullptr;
-    QSIM_HIPCHK(hipMallocAsync((void**)&d_sums, all_chunks * sizeof(double), s));
+    // scratch = [chunk sums][chunk of shot][target of shot][index of shot], 8 B each
+    char* base = (char*)scratch.get((all_chunks + 3 * nshots) * 8, s);
+    double* d_sums = (double*)base;
+    int64_t* d_chunk = (int64_t*)(base + all_chunks * 8);
+    double* d_target = (double*)(base + (all_chunks + nshots) * 8);
+    int64_t* d_out = (int64_t*)(base + (all_chunks + 2 * nshots) * 8);
     hipLaunchKernelGGL(k_chunk_sums, dim3((unsigned)all_chunks), dim3(256), 0, s, st, chunk, d_sums);
     QSIM_HIPCHK(hipGetLastError());
     std::vector<double> sums(all_chunks);
     QSIM_HIPCHK(hipMemcpyAsync(sums.data(), d_sums, all_chunks * sizeof(double),
                                hipMemcpyDeviceToHost, s));
     QSIM_HIPCHK(hipStreamSynchronize(s));
-    QSIM_HIPCHK(hipFreeAsync(d_sums, s));
     std::vector<double> cdf(nchunks), comp(nchunks);
     std::vector<int64_t> chunk_of(nshots);
     std::vector<double> target(nshots);
@@ -245,12 +248,6 @@ void sample_indices(const double2* st, int n, uint64_t batch, const double* unif
             }
         }
     }
-    int64_t* d_chunk = nullptr;
-    double* d_target = nullptr;
-    int64_t* d_out = nullptr;
-    QSIM_HIPCHK(hipMallocAsync((void**)&d_chunk, nshots * sizeof(int64_t), s));
-    QSIM_HIPCHK(hipMallocAsync((void**)&d_target, nshots * sizeof(double), s));
-    QSIM_HIPCHK(hipMallocAsync((void**)&d_out, nshots * sizeof(int64_t), s));
     QSIM_HIPCHK(hipMemcpyAsync(d_chunk, chunk_of.data(), nshots * sizeof(int64_t),
                                hipMemcpyHostToDevice, s));
     QSIM_HIPCHK(hipMemcpyAsync(d_target, target.data(), nshots * sizeof(double),
@@ -263,9 +260,6 @@ void sample_indices(const double2* st, int n, uint64_t batch, const double* unif
     }
     QSIM_HIPCHK(hipMemcpyAsync(out, d_out, nshots * sizeof(int64_t), hipMemcpyDeviceToHost, s));
     QSIM_HIPCHK(hipStreamSynchronize(s));
-    QSIM_HIPCHK(hipFreeAsync(d_chunk, s));
-    QSIM_HIPCHK(hipFreeAsync(d_target, s));
-    QSIM_HIPCHK(hipFreeAsync(d_out, s));
 }
 
 // Histogram of sampled outcomes; indices >= N (the reference's end()) are skipped, as in

@@ -51,8 +51,9 @@ def test_state_sampling_matches_sequential_cdf(qsim, oracle, gpu_ready, n):
     u = u[(u > 0) & (u < 1)]
     got = sim.state.sampleWith(u)
     exp = oracle.sample_cpu(n, st, u)
-    nbad = _assert_tie_only(probs, u, got, exp)
-    assert nbad <= 0.01 * u.size
+    _assert_tie_only(probs, u, got, exp)
+    # uniform shots (not aimed at steps) essentially never land in such a gap
+    assert np.count_nonzero(got[:20000] != exp[:20000]) <= 2
 
 
 def test_sampling_past_the_end(qsim, gpu_ready):
