@@ -183,6 +183,7 @@ struct qsim_batch {
     double2* d = nullptr;
     hipStream_t stream = nullptr;
     uint64_t seed = 0, step = 0;
+    uint64_t ncounter = 0;  // per-pair noise passes so far (QSIM_BATCH_REFERENCE_NOISE)
     uint64_t* d_xz = nullptr;
     int* d_e = nullptr;
     DevChannel* d_ch = nullptr;
@@ -267,6 +268,7 @@ int qsim_batch_set_seed(qsim_batch* b, uint64_t seed) {
         need(b);
         b->seed = seed;
         b->step = 0;
+        b->ncounter = 0;
     });
 }
 
@@ -308,6 +310,23 @@ int qsim_batch_run(qsim_batch* b, const qsim_gate* gates, size_t count,
         }
         const uint64_t N = 1ull << b->n;
         const uint64_t items_per_traj = N / 2 > 0 ? N / 2 : 1;
+        if (flags & QSIM_BATCH_REFERENCE_NOISE) {
+            // The reference's process (src/NoiseModel.cu:815-892): each gate, then for every
+            // Depolarizing channel entry (the only type batched mode applies, F5) one pass over
+            // all B x 2^(n-1) amplitude pairs; every pair draws its own uniform (counter hash of
+            // (seed, pass, global pair index) in place of its curandState) and, below p, a second
+            // one picks X / Y / Z at 1/3, 2/3 — applied to that pair only (F7).
+            std::vector<const qsim_noise_channel*> dep;
+            for (size_t i = 0; i < n_channels; ++i)
+                if (channels[i].type == 0) dep.push_back(&channels[i]);
+            for (const Op& op : ops) {
+                if (op.kind >= 0) launch_op(b->d, b->n, (uint64_t)b->batch, op, b->stream, &b->timer);
+                for (const qsim_noise_channel* c : dep)
+                    launch_noise(b->d, b->n, 0, c->qubit, c->probability, b->seed, b->ncounter++,
+                                 b->stream, &b->timer, (uint64_t)b->batch);
+            }
+            return;
+        }
         static const bool fused_env = [] {
             const char* e = std::getenv("QSIM_BATCH_FUSED");
             return e == nullptr || std::atoi(e) != 0;

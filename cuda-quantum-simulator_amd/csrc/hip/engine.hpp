@@ -187,7 +187,7 @@ void launch_fused(double2* st, int n, uint64_t batch, const Plan& plan, const Ti
 // Single-trajectory Monte-Carlo noise (noise.hip): one per-pair pass of channel `type`
 // (reference NoiseType numbering) on `qubit`, uniforms from the hash of (seed, counter, pair).
 void launch_noise(double2* st, int n, int type, int qubit, double p, uint64_t seed,
-                  uint64_t counter, hipStream_t s, Timer* tm);
+                  uint64_t counter, hipStream_t s, Timer* tm, uint64_t batch = 1);
 
 // Density matrices as 2n-index-bit states (density.hip).
 void dm_lower(int n, const qsim_gate* gates, size_t count, const qsim_noise_channel* ch,

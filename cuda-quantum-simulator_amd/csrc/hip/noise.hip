@@ -45,7 +45,8 @@ __device__ __forceinline__ float nz_uniform(uint64_t h) {
 
 struct NArgs {
     double2* st;
-    uint64_t pairs;  // 2^(n-1)
+    uint64_t pairs;  // B x 2^(n-1): pair idx of trajectory t is t * 2^(n-1) + its index in t
+    int log_ppt;     // n - 1
     uint64_t key;    // noise_key(seed, counter)
     int target;
     double p;
@@ -58,7 +59,9 @@ __global__ __launch_bounds__(256) void k_noise(NArgs a) {
     for (uint64_t idx = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < a.pairs; idx += stride) {
         const uint64_t h = nz_mix(a.key ^ nz_mix(idx));
         const float r1 = nz_uniform(h);
-        const uint64_t i0 = (idx & mask) | ((idx & ~mask) << 1);
+        // reference idx -> (traj, pair_idx) split (src/NoiseModel.cu:843-856); batch 1: traj 0
+        const uint64_t traj = idx >> a.log_ppt, pr = idx & ((1ull << a.log_ppt) - 1ull);
+        const uint64_t i0 = (traj << (a.log_ppt + 1)) | (pr & mask) | ((pr & ~mask) << 1);
         const uint64_t i1 = i0 | (1ull << a.target);
         if constexpr (TYPE == 0 || TYPE == 3 || TYPE == 4 || TYPE == 5) {  // Pauli flips
             if (!((double)r1 < a.p)) continue;  // float draw vs double p, as the reference (:195)
@@ -129,14 +132,15 @@ uint64_t noise_key(uint64_t seed, uint64_t counter) {
 }
 
 void launch_noise(double2* st, int n, int type, int qubit, double p, uint64_t seed,
-                  uint64_t counter, hipStream_t s, Timer* tm) {
+                  uint64_t counter, hipStream_t s, Timer* tm, uint64_t batch) {
     if (type < 0 || type > 5) fail(QSIM_ERR_INVALID_ARGUMENT, "unknown noise type");
     if (qubit < 0 || qubit >= n)
         fail(QSIM_ERR_OUT_OF_RANGE, "Qubit index " + std::to_string(qubit) + " out of range");
     if (!std::isfinite(p)) fail(QSIM_ERR_INVALID_ARGUMENT, "noise probability must be finite");
     NArgs a{};
     a.st = st;
-    a.pairs = 1ull << (n - 1);
+    a.pairs = batch << (n - 1);
+    a.log_ppt = n - 1;
     a.key = noise_key(seed, counter);
     a.target = qubit;
     a.p = p;

@@ -155,8 +155,9 @@ void BatchedSimulator::run(const Circuit& circuit) {
     for (const NoiseChannel& c : noise_model_.getChannels())
         for (int q : c.qubits) ch.push_back(qsim_noise_channel{static_cast<int>(c.type), q, c.probability});
     check(qsim_batch_run(h_, gates.data(), gates.size(), ch.data(), ch.size(),
-                         gate_set_ == BatchedGateSet::Reference ? QSIM_BATCH_REFERENCE_GATESET
-                                                                : QSIM_BATCH_FULL_GATESET));
+                         (gate_set_ == BatchedGateSet::Reference ? QSIM_BATCH_REFERENCE_GATESET
+                                                                 : QSIM_BATCH_FULL_GATESET) |
+                             (noise_ == BatchedNoise::Reference ? QSIM_BATCH_REFERENCE_NOISE : 0)));
 }
 
 std::vector<double> BatchedSimulator::getAverageProbabilities() const {

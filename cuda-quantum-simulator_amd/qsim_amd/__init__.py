@@ -7,7 +7,7 @@ from . import _lib
 from .circuit import (Circuit, GateOp, GateType, MAX_QUBITS, MIN_QUBITS, createBellCircuit,
                       createGHZCircuit, createRandomCircuit, createRandomHCCircuit,
                       createScalingBenchmarkCircuit, is_valid_qubit_count)
-from .simulator import (BatchedGateSet, BatchedSimulator, NoiseChannel, NoiseModel, NoiseType,
+from .simulator import (BatchedGateSet, BatchedNoise, BatchedSimulator, NoiseChannel, NoiseModel, NoiseType,
                         NoisySimulator, RunMode, Simulator, StateVector, device_count, device_info)
 from .density import DensityMatrix, DensityMatrixSimulator
 
@@ -15,7 +15,7 @@ __all__ = [
     "DensityMatrix", "DensityMatrixSimulator",
     "Circuit", "GateOp", "GateType", "MAX_QUBITS", "MIN_QUBITS", "createBellCircuit",
     "createGHZCircuit", "createRandomCircuit", "createRandomHCCircuit",
-    "createScalingBenchmarkCircuit", "is_valid_qubit_count", "BatchedGateSet",
+    "createScalingBenchmarkCircuit", "is_valid_qubit_count", "BatchedGateSet", "BatchedNoise",
     "BatchedSimulator", "NoiseChannel", "NoiseModel", "NoiseType", "NoisySimulator", "RunMode", "Simulator",
     "StateVector", "device_count", "device_info",
 ]

@@ -26,6 +26,7 @@ QSIM_RUN_FUSED = 1
 QSIM_BATCH_FULL_GATESET = 0
 QSIM_BATCH_REFERENCE_GATESET = 1
 QSIM_BATCH_PER_GATE = 2
+QSIM_BATCH_REFERENCE_NOISE = 4
 
 QSIM_CIRCUIT_BELL = 0
 QSIM_CIRCUIT_GHZ = 1

@@ -418,16 +418,26 @@ class BatchedGateSet(enum.IntEnum):
     Reference = _lib.QSIM_BATCH_REFERENCE_GATESET
 
 
+class BatchedNoise(enum.IntEnum):
+    """Physical: one draw per trajectory, channel and gate (the Kraus channel on a pure-state
+    trajectory).  Reference: the reference's per-amplitude-pair depolarizing process
+    (src/NoiseModel.cu:834-892; Depolarizing entries only)."""
+    Physical = 0
+    Reference = _lib.QSIM_BATCH_REFERENCE_NOISE
+
+
 class BatchedSimulator:
     """Reference BatchedSimulator (src/NoiseModel.cu:653-972)."""
 
     def __init__(self, num_qubits: int, batch_size: int, noise_model: Optional[NoiseModel] = None,
-                 gate_set: BatchedGateSet = BatchedGateSet.Full):
+                 gate_set: BatchedGateSet = BatchedGateSet.Full,
+                 noise: BatchedNoise = BatchedNoise.Physical):
         self._h = _c.c_void_p()
         _lib.check(_lib.hip.qsim_batch_create(num_qubits, batch_size, _c.byref(self._h)))
         self._n, self._b = num_qubits, batch_size
         self._noise = noise_model or NoiseModel()
         self._gate_set = BatchedGateSet(gate_set)
+        self._noise_sem = BatchedNoise(noise)
         self._rng = np.random.default_rng()
 
     def __del__(self):
@@ -441,6 +451,12 @@ class BatchedSimulator:
 
     def setNoiseModel(self, nm: NoiseModel) -> None: self._noise = nm
     def setGateSet(self, g: BatchedGateSet) -> None: self._gate_set = BatchedGateSet(g)
+    def setNoiseSemantics(self, m: BatchedNoise) -> None: self._noise_sem = BatchedNoise(m)
+
+    def setReferenceCompatible(self) -> None:
+        """Both reference behaviours: gate set X/Y/Z/H/CNOT and per-pair depolarizing noise."""
+        self._gate_set = BatchedGateSet.Reference
+        self._noise_sem = BatchedNoise.Reference
 
     def setSeed(self, seed: int) -> None:
         self._rng = np.random.default_rng(seed)
@@ -455,7 +471,8 @@ class BatchedSimulator:
             raise ValueError("Circuit qubit count doesn't match simulator")
         g, ng = circuit.to_abi()
         ch, nch = self._noise.to_abi()
-        flags = int(self._gate_set) | (_lib.QSIM_BATCH_PER_GATE if per_gate else 0)
+        flags = int(self._gate_set) | int(self._noise_sem) | \
+            (_lib.QSIM_BATCH_PER_GATE if per_gate else 0)
         _lib.check(_lib.hip.qsim_batch_run(self._h, g, ng, ch, nch, flags))
 
     def synchronize(self) -> None: _lib.check(_lib.hip.qsim_batch_sync(self._h))

@@ -103,6 +103,12 @@ private:
 // silently skipped (src/NoiseModel.cu:742-763, 808-812).  Full: every GateType.
 enum class BatchedGateSet { Full, Reference };
 
+// Noise process of the batched trajectories.  Physical (default): one draw per trajectory, channel
+// and gate — the Kraus channel on a pure-state trajectory, all four Pauli channel types.
+// Reference: the reference's per-amplitude-pair process — Depolarizing entries only, one draw
+// per pair per pass (applyBatchedDepolarizingKernel, src/NoiseModel.cu:834-892).
+enum class BatchedNoise { Physical, Reference };
+
 class BatchedSimulator {
 public:
     BatchedSimulator(int num_qubits, int batch_size);
@@ -128,6 +134,12 @@ public:
     size_t getTotalMemoryBytes() const { return (size_t)batch_size_ * (1ULL << num_qubits_) * 16u; }
 
     void setGateSet(BatchedGateSet g) { gate_set_ = g; }
+    void setNoiseSemantics(BatchedNoise m) { noise_ = m; }
+    // Both reference behaviours at once (gate set X/Y/Z/H/CNOT, per-pair depolarizing noise).
+    void setReferenceCompatible() {
+        gate_set_ = BatchedGateSet::Reference;
+        noise_ = BatchedNoise::Reference;
+    }
     qsim_batch* handle() const { return h_; }
 
 private:
@@ -136,6 +148,7 @@ private:
     qsim_batch* h_ = nullptr;
     NoiseModel noise_model_;
     BatchedGateSet gate_set_ = BatchedGateSet::Full;
+    BatchedNoise noise_ = BatchedNoise::Physical;
     std::mt19937 rng_;  // host sampling stream (reference rng_, src/NoiseModel.cu:661)
 };
 

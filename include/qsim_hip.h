@@ -180,7 +180,15 @@ int qsim_batch_set_seed(qsim_batch* b, uint64_t seed);
  * For n >= 10 the gates run as fused tile passes with the noise carried as per-trajectory Pauli
  * frames (same draws, same trajectories); QSIM_BATCH_PER_GATE forces one kernel per gate plus
  * one Pauli pass per noisy step (the reference's structure). */
-enum { QSIM_BATCH_FULL_GATESET = 0, QSIM_BATCH_REFERENCE_GATESET = 1, QSIM_BATCH_PER_GATE = 2 };
+enum { QSIM_BATCH_FULL_GATESET = 0, QSIM_BATCH_REFERENCE_GATESET = 1, QSIM_BATCH_PER_GATE = 2,
+       QSIM_BATCH_REFERENCE_NOISE = 4 };
+/* QSIM_BATCH_REFERENCE_NOISE: the reference's noise process instead of the physical channel —
+ * after every gate, one pass per Depolarizing channel entry (other types are ignored, as the
+ * reference's batched mode does) over all B x 2^(n-1) amplitude pairs; each pair draws its own
+ * uniform (float, compared with the double probability) and below p picks X/Y/Z at float
+ * thresholds 1/3, 2/3 with a second draw, applied to that pair only
+ * (applyBatchedDepolarizingKernel, src/NoiseModel.cu:834-892).  The draws come from the counter
+ * hash of qsim_noise_apply keyed by (seed, pass counter, global pair index t*2^(n-1) + pair). */
 int qsim_batch_run(qsim_batch* b, const qsim_gate* gates, size_t count,
                    const qsim_noise_channel* channels, size_t n_channels, int flags);
 int qsim_batch_avg_probabilities(qsim_batch* b, double* dst);           /* 2^n */

@@ -272,6 +272,60 @@ def noisy_run(n, gates, channels, seed, counter=0, state=None):
 # rho' = U rho U^dag with textbook matrices, channels per the reference kernels
 # src/DensityMatrix.cu:978-1122 (depolarizing: off-diagonal x (1 - 4p/3) only; bit-phase flip =
 # phase flip, :343-356; amplitude damping with the pre-channel rho11).
+# ---- BatchedSimulator, reference noise process (test infrastructure) ---------------------
+# Restates run() + applyBatchedNoise() + applyBatchedDepolarizingKernel
+# (src/NoiseModel.cu:815-892): after EVERY circuit gate (also gates the reference gate set
+# skips), one pass per Depolarizing channel entry in order; pass idx covers all B x 2^(n-1)
+# pairs (traj = idx / n_pairs, pair = idx % n_pairs, :843-856); a pair fires when its float
+# uniform < p (promoted to double), then a second float uniform picks X (< 1/3f), Y (< 2/3f),
+# else Z, applied to that pair of that trajectory only.  Draws: the engine's documented counter
+# hash keyed by (seed, pass counter, idx) in place of curandState[idx] (parity unpinned vs cuRAND).
+_REF_BATCH_GATES = {0, 1, 2, 3, 11}  # src/NoiseModel.cu:742-763 (X/Y/Z/H), :808-812 (CNOT)
+
+
+def batched_depolarizing_pass(states, n, q, p, seed, counter):
+    """states: (B, 2^n) complex, modified copy returned."""
+    s = np.array(states, dtype=complex)
+    B = s.shape[0]
+    npairs = 1 << (n - 1)
+    idx = np.arange(B * npairs, dtype=np.uint64)
+    h = _mix_np(np.uint64(noise_key(seed, counter)) ^ _mix_np(idx))
+    fire = _uniform(h).astype(np.float64) < float(p)
+    r2 = _uniform(_mix_np(h ^ np.uint64(0x5bd1e9955bd1e995)))
+    pauli = np.where(r2 < np.float32(1.0) / np.float32(3.0), 1,
+                     np.where(r2 < np.float32(2.0) / np.float32(3.0), 2, 3))
+    traj = (idx // np.uint64(npairs)).astype(np.int64)
+    pr = (idx % np.uint64(npairs)).astype(np.int64)
+    mask = (1 << q) - 1
+    i0 = (pr & mask) | ((pr & ~mask) << 1)
+    i1 = i0 | (1 << q)
+    flat = s.reshape(-1)
+    o0, o1 = traj * (1 << n) + i0, traj * (1 << n) + i1
+    a0, a1 = flat[o0].copy(), flat[o1].copy()
+    x, y, z = fire & (pauli == 1), fire & (pauli == 2), fire & (pauli == 3)
+    flat[o0[x]], flat[o1[x]] = a1[x], a0[x]
+    flat[o0[y]], flat[o1[y]] = -1j * a1[y], 1j * a0[y]
+    flat[o1[z]] = -a1[z]
+    return s
+
+
+def batched_reference_run(n, B, gates, channels, seed, reference_gateset=False, states=None,
+                          counter=0):
+    """channels: (type, qubit, p) entries in order; returns (states (B, 2^n), next counter)."""
+    st = np.zeros((B, 1 << n), complex) if states is None else np.array(states, dtype=complex)
+    if states is None:
+        st[:, 0] = 1.0
+    dep = [(q, p) for (t, q, p) in channels if t == 0]
+    for g in gates:
+        if not reference_gateset or g[0] in _REF_BATCH_GATES:
+            for b in range(B):
+                st[b] = run_cpu(n, [g], st[b])
+        for q, p in dep:
+            st = batched_depolarizing_pass(st, n, q, p, seed, counter)
+            counter += 1
+    return st, counter
+
+
 def dm_apply_gate(rho, n, gate):
     t, qubits, th = gate
     if t in (13, 14, 16):

@@ -1,0 +1,110 @@
+"""BatchedSimulator under the reference's noise process (QSIM_BATCH_REFERENCE_NOISE; VERDICT r1
+"reference-semantics batched noise").
+
+The reference applies, after every gate, one applyBatchedDepolarizingKernel pass per
+Depolarizing channel entry: every amplitude PAIR of every trajectory draws its own uniform and,
+below p, a second one picks X/Y/Z applied to that pair only (src/NoiseModel.cu:815-892, SURVEY
+F5/F7).  The engine runs that process with a counter hash in place of the per-pair curandState;
+the oracle restates it with the same hash (oracle/numpy_oracle.py: batched_reference_run), so
+the GPU trajectories are compared exactly (1e-12).  cuRAND's own stream is parity-unpinned; the
+statistics test checks the process against its closed form.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _circuit(q, n, depth, seed):
+    rng = np.random.default_rng(seed)
+    c = q.Circuit(n)
+    for _ in range(depth):
+        a, b, d = (int(x) for x in rng.choice(n, 3, replace=False))
+        k = int(rng.integers(0, 9))
+        if k < 4:
+            (c.x, c.y, c.z, c.h)[k](a)
+        elif k == 4:
+            c.cnot(a, b)
+        elif k == 5:
+            c.rx(a, float(rng.uniform(-3, 3)))
+        elif k == 6:
+            c.cz(a, b)
+        elif k == 7:
+            c.toffoli(a, b, d)
+        else:
+            c.swap(a, b)
+    return c
+
+
+def _entries(n, p_dep, p_flip):
+    # NoiseModel order: addDepolarizingAll(n, p_dep) then addBitFlip([0, n-1], p_flip)
+    return [(0, q, p_dep) for q in range(n)] + [(3, 0, p_flip), (3, n - 1, p_flip)]
+
+
+@pytest.mark.parametrize("n,B,seed,refgates", [(6, 8, 1, False), (9, 4, 2, True), (11, 3, 3, False)])
+def test_reference_noise_matches_oracle(qsim, oracle, gpu_ready, n, B, seed, refgates):
+    c = _circuit(qsim, n, 25, seed)
+    nm = qsim.NoiseModel()
+    nm.addDepolarizingAll(n, 0.15)
+    nm.addBitFlip([0, n - 1], 0.3)  # not a Depolarizing channel: the reference ignores it
+    s = qsim.BatchedSimulator(n, B, nm, noise=qsim.BatchedNoise.Reference,
+                              gate_set=qsim.BatchedGateSet.Reference if refgates
+                              else qsim.BatchedGateSet.Full)
+    s.setSeed(seed)
+    ref, counter = None, 0
+    for _ in range(2):  # the second run continues the pass counter
+        s.run(c)
+        ref, counter = oracle.batched_reference_run(n, B, oracle.gates_of(c), _entries(n, 0.15, 0.3),
+                                                    seed, refgates, states=ref, counter=counter)
+    for t in range(B):
+        np.testing.assert_allclose(s.getStateVector(t), ref[t], atol=1e-12, rtol=0)
+    # per-pair flips act on a random subset of pairs: trajectories differ and stay normalised
+    # (X/Y/Z on a pair preserve the norm)
+    assert abs(np.sum(np.abs(s.getStateVector(0)) ** 2) - 1.0) < 1e-10
+
+
+def test_reference_noise_statistics(qsim, gpu_ready):
+    """n = 1: one pair per trajectory, so the per-pair process equals the channel: after X,
+    P(|0>) = 2p/3 (X or Y flips back, Z keeps |1>)."""
+    n, B, p = 1, 20000, 0.3
+    nm = qsim.NoiseModel()
+    nm.addDepolarizing([0], p)
+    b = qsim.BatchedSimulator(n, B, nm, noise=qsim.BatchedNoise.Reference)
+    b.setSeed(42)
+    c = qsim.Circuit(1)
+    c.x(0)
+    b.run(c)
+    avg = b.getAverageProbabilities()
+    assert abs(avg[0] - 2 * p / 3) < 0.015
+
+
+def test_reference_noise_per_pair_subset(qsim, gpu_ready):
+    """F7: the reference flips a random SUBSET of pairs — with p = 0.5 on qubit 0 of |+>^n the
+    trajectory is no longer a product state, unlike any Pauli-channel realisation."""
+    n, B = 8, 4
+    nm = qsim.NoiseModel()
+    nm.addDepolarizing([0], 0.5)
+    c = qsim.Circuit(n)
+    for q in range(n):
+        c.z(q) if q == 0 else c.h(q)
+    b = qsim.BatchedSimulator(n, B, nm, noise=qsim.BatchedNoise.Reference)
+    b.setSeed(1)
+    b.run(c)
+    psi = b.getStateVector(0).reshape(-1, 2)  # row k: the qubit-0 pair (a0, a1) of pair k
+    mag = 1 / np.sqrt(psi.shape[0])
+    one = np.abs(psi[:, 1]) > 0.5 * mag
+    # every pair holds its amplitude on exactly one side, with its magnitude unchanged ...
+    np.testing.assert_allclose(np.abs(psi).max(axis=1), mag, atol=1e-12)
+    np.testing.assert_allclose(np.abs(psi).min(axis=1), 0, atol=1e-12)
+    # ... and which side differs from pair to pair (8 passes at p = 0.5 over 128 pairs)
+    assert 0 < np.count_nonzero(one) < psi.shape[0]
+
+
+def test_reference_compatible_profile_cpp_names(qsim, gpu_ready):
+    b = qsim.BatchedSimulator(3, 2)
+    b.setReferenceCompatible()
+    c = qsim.Circuit(3)
+    c.h(0).s(1).cnot(0, 1)  # S ignored by the reference gate set
+    b.run(c)
+    p = b.getAverageProbabilities()
+    np.testing.assert_allclose(p, [0.5, 0, 0, 0.5, 0, 0, 0, 0], atol=1e-12)
