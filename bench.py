@@ -50,6 +50,12 @@ def parse():
                         "circuit on --trajectories noisy trajectories (depolarizing on every "
                         "qubit after every gate, SURVEY §8(d))")
     p.add_argument("--trajectories", type=int, default=1024)
+    p.add_argument("--batch-noise", choices=["physical", "reference"], default="physical",
+                   help="W-BATCH noise process: physical (one draw per trajectory, channel and "
+                        "gate; Pauli frames) or reference (per-pair draws after every gate, "
+                        "src/NoiseModel.cu:834-892)")
+    p.add_argument("--no-1q28", action="store_true",
+                   help="skip the W-1Q 28q single-qubit roofline object of the default line")
     p.add_argument("--noise", type=float, default=0.01)
     p.add_argument("--cpu-budget", type=float, default=12.0,
                    help="seconds of single-thread CPU oracle work for cpu_baseline (0 = skip)")
@@ -171,11 +177,46 @@ def run_single(args):
         "effective_GBps": round(eff, 1),
         "kernels": stats,
     }
+    del sim
+    if args.workload == "hc" and not args.no_1q28:
+        out["roofline_1q28"] = roofline_1q28(q)
     if args.cpu_budget > 0:
         out["cpu_baseline"] = cpu_baseline(circuit, n, args.cpu_budget)
     else:
         out["cpu_baseline"] = None
     print(json.dumps(out))
+
+
+def roofline_1q28(q, steps=3):
+    """north_star's single-qubit target, measured in the same run: W-1Q at 28 qubits (BASELINE
+    configs[2], 4 GiB state) — 100 H gates on targets i % 28, one kernel per gate, unfused —
+    per-launch HIP events on the state's stream; algorithmic bytes 32 B x 2^28 per gate."""
+    n = 28
+    c = q.Circuit(n)
+    for i in range(100):
+        c.h(i % n)
+    sim = q.Simulator(n, mode=q.RunMode.PerGate)
+    sim.run(c)
+    sim.synchronize()
+    sim.state.profile(True)
+    sim.state.profileReset()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        sim.run(c)
+    sim.synchronize()
+    wall = time.perf_counter() - t0
+    stats = sim.state.profileStats()
+    sim.state.profile(False)
+    launches = sum(s["launches"] for s in stats)
+    ms = sum(s["ms"] for s in stats)
+    by = sum(s["alg_bytes"] for s in stats)
+    achieved = by / (ms / 1e3) / 1e9
+    return {"workload": "W-1Q 100 unfused H gates on targets i % 28, 28 qubits",
+            "kernels": sorted({s["name"] for s in stats}), "launches": launches,
+            "avg_launch_ms": round(ms / launches, 4), "alg_bytes_per_launch": by / launches,
+            "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBPS, 4),
+            "gates_per_s": round(100 * steps / wall, 1), "target_frac": 0.70}
 
 
 def run_batch(args):
@@ -189,7 +230,8 @@ def run_batch(args):
     circuit = q.createRandomHCCircuit(n, args.depth, args.seed)
     nm = q.NoiseModel()
     nm.addDepolarizingAll(n, args.noise)
-    sim = q.BatchedSimulator(n, B, nm)
+    sem = q.BatchedNoise.Reference if args.batch_noise == "reference" else q.BatchedNoise.Physical
+    sim = q.BatchedSimulator(n, B, nm, noise=sem)
     sim.setSeed(args.seed)
     for _ in range(args.warmup):
         sim.run(circuit)
@@ -222,6 +264,11 @@ def run_batch(args):
         "scaling": "weak", "vs_baseline": None, "dtype": "c128 (complex<double>)", "data": "synthetic",
         "config": {"workload": f"W-BATCH {n}q x {B} trajectories, depolarizing {args.noise} on all "
                                f"qubits after every gate, W-HC depth {args.depth} seed {args.seed}",
+                   "noise_process": ("reference: per-pair draws, one pass per channel entry "
+                                     "after every gate (src/NoiseModel.cu:834-892)"
+                                     if args.batch_noise == "reference" else
+                                     "physical: one draw per trajectory, channel and gate "
+                                     "(Pauli frames)"),
                    "qubits": n, "trajectories": B, "gates": gates, "state_bytes": (16 << n) * B},
         "roofline": roof, "kernels": stats, "cpu_baseline": None,
     }
