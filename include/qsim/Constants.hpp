@@ -31,6 +31,18 @@ constexpr int MAX_QUBITS = 30;
 constexpr int MIN_QUBITS = 1;
 }  // namespace device_config
 
+// Source compatibility with code written against the reference (include/Constants.hpp:56-75):
+// `qsim::cuda_config::MAX_QUBITS`, `DEFAULT_BLOCK_SIZE`, ... keep compiling.  The values are the
+// MI355X ones (a block of 256 threads is 4 wave64s); TARGET_CC_* name the gfx950 target.
+namespace cuda_config {
+constexpr int DEFAULT_BLOCK_SIZE = device_config::DEFAULT_BLOCK_SIZE;
+constexpr int REDUCTION_BLOCK_SIZE = device_config::DEFAULT_BLOCK_SIZE;
+constexpr int MAX_QUBITS = device_config::MAX_QUBITS;
+constexpr int MIN_QUBITS = device_config::MIN_QUBITS;
+constexpr int TARGET_CC_MAJOR = 9;  // gfx950: GFX9 family (CDNA4)
+constexpr int TARGET_CC_MINOR = 50;
+}  // namespace cuda_config
+
 inline bool isValidQubit(int qubit, int num_qubits) { return qubit >= 0 && qubit < num_qubits; }
 inline bool isValidQubitCount(int num_qubits) {
     return num_qubits >= device_config::MIN_QUBITS && num_qubits <= device_config::MAX_QUBITS;

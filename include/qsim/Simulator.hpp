@@ -4,11 +4,17 @@
 // measurement signatures and exception types.  run() is asynchronous like the reference
 // (src/Simulator.cu:95-97); every readout synchronizes.  By default run() hands the whole circuit
 // to the engine's fused-pass planner (RunMode::Fused); RunMode::PerGate reproduces the
-// reference's one-launch-per-gate execution.  The reference's CPUSimulator is the parity oracle
-// and lives in oracle/ (test infrastructure), not in this library.
+// reference's one-launch-per-gate execution.
+//
+// CPUSimulator (reference include/Simulator.hpp:91-112, src/Simulator.cu:195-345) is this
+// library's own host implementation (csrc/host/CPUSimulator.cpp: gate table + thread pool over
+// the amplitude pairs), kept for code that compares against the CPU (benchmark_scaling.cu:85).
+// It is not the parity oracle (oracle/ is test infrastructure and is never linked here).
 #pragma once
 
 #include <complex>
+#include <cstdint>
+#include <random>
 #include <vector>
 
 #include "Circuit.hpp"
@@ -45,6 +51,41 @@ public:
 private:
     StateVector state_;
     RunMode mode_ = RunMode::Fused;
+};
+
+// Which gates CPUSimulator::applyGate acts on.  Reference: exactly the reference CPU path —
+// every 1-qubit gate, CNOT, CZ and SWAP; CRY, CRZ and Toffoli are silent no-ops
+// (src/Simulator.cu:214-220, 313-314).  Full: CRY / CRZ / Toffoli as the GPU kernels
+// define them (src/Gates.cu:322-410), so CPU and GPU agree on every circuit.
+enum class CpuGateSet { Reference, Full };
+
+class CPUSimulator {
+public:
+    explicit CPUSimulator(int num_qubits, CpuGateSet gates = CpuGateSet::Reference);
+
+    void reset();
+    void run(const Circuit& circuit);  // std::invalid_argument on qubit-count mismatch
+    void applyGate(const GateOp& gate);
+
+    std::vector<std::complex<double>> getStateVector() const { return state_; }
+    std::vector<double> getProbabilities() const;
+    std::vector<int> sample(int n_shots);
+
+    int getNumQubits() const { return num_qubits_; }
+    size_t getStateSize() const { return state_.size(); }
+
+    // Worker threads for the pair loops (default: hardware concurrency, capped at 64; states
+    // below 2^14 amplitudes always run on the calling thread).  1 = the reference's single core.
+    void setThreads(int threads);
+    int getThreads() const { return threads_; }
+    void setSeed(unsigned int seed) { rng_.seed(seed); }
+
+private:
+    int num_qubits_;
+    CpuGateSet gate_set_;
+    int threads_;
+    std::vector<std::complex<double>> state_;
+    std::mt19937 rng_;
 };
 
 }  // namespace qsim

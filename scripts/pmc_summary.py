@@ -78,10 +78,33 @@ def main():
             for k in ("fetch_bytes_per_launch", "write_bytes_per_launch", "hbm_bytes_per_launch"):
                 agg[k] = (agg[k] * n0 + ent[k] * n1) / (n0 + n1)
             agg["launches"] = n0 + n1
+    # further passes (p3, p4, ...): every other counter, averaged per launch of each kernel
+    other = {}
+    for pdir in sorted(glob.glob(os.path.join(src, "p[0-9]*"))):
+        if os.path.basename(pdir) in ("p1", "p2"):
+            continue
+        for path in glob.glob(os.path.join(pdir, "**", "*counter_collection.csv"), recursive=True):
+            with open(path) as f:
+                acc = {}
+                for r in csv.DictReader(f):
+                    key = (r["Kernel_Name"], r["Counter_Name"], int(r["Dispatch_Id"]))
+                    acc[key] = acc.get(key, 0.0) + float(r["Counter_Value"])
+            for (kname, cname, _), v in acc.items():
+                lab = label_of(kname)
+                for k in ([kname] + ([lab] if lab else [])):
+                    d = other.setdefault(k, {}).setdefault(cname, [0.0, 0])
+                    d[0] += v
+                    d[1] += 1
+    for k, cs in other.items():
+        tgt = per.setdefault(k, {})
+        tgt["counters_per_launch"] = {c: v[0] / v[1] for c, v in sorted(cs.items())}
     with open(out, "w") as f:
         json.dump({"source": src, "fetch_correction": 2.0, "unit": "bytes", "kernels": per}, f, indent=1)
     for k, v in per.items():
-        print(f"{k[:60]:60s} {v['launches']:5d} {v['hbm_bytes_per_launch'] / 2**30:8.3f} GiB/launch")
+        if "hbm_bytes_per_launch" in v:
+            print(f"{k[:60]:60s} {v['launches']:5d} {v['hbm_bytes_per_launch'] / 2**30:8.3f} GiB/launch")
+        for c, x in v.get("counters_per_launch", {}).items():
+            print(f"    {c:28s} {x:16.1f}")
 
 
 if __name__ == "__main__":

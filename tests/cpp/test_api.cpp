@@ -390,4 +390,21 @@ TEST(Batched, DepolarizingKeepsNormalization) {  // :283-311, :449-462
     EXPECT_NEAR(std::accumulate(avg.begin(), avg.end(), 0.0), 1.0, 1e-10);
 }
 
+// benchmarks/benchmark_scaling.cu:69-90 (benchmarkGPUvsCPU): the W-REF circuit through the GPU
+// Simulator and the API's CPUSimulator at n = 10..22 — the states agree at 1e-12.
+TEST(Scaling, GpuMatchesCpuSimulator) {
+    for (int n = 10; n <= 22; n += 2) {
+        qsim::Circuit c(n);
+        for (int i = 0; i < 100; ++i) {
+            c.h(i % n);
+            if (n > 1 && i % 5 == 0) c.cnot(i % n, (i + 1) % n);
+        }
+        qsim::Simulator gpu_sim(n);
+        gpu_sim.run(c);
+        qsim::CPUSimulator cpu_sim(n);
+        cpu_sim.run(c);
+        expect_state(gpu_sim.getStateVector(), cpu_sim.getStateVector(), kEquivTol);
+    }
+}
+
 TH_MAIN

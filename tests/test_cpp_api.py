@@ -28,3 +28,13 @@ def test_cpp_api_suite():
     print(r.stdout[-4000:])
     assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-4000:]
     assert " 0 failed" in r.stdout
+
+
+def test_cpu_simulator_suite():
+    """CPU-only: the product qsim::CPUSimulator (libqsim.so) against the test oracle, thread
+    invariance, sampling, errors and the cuda_config alias (tests/cpp/test_cpu_api.cpp)."""
+    _build()
+    exe = os.path.join(CPP, "build", "test_cpu_api")
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-4000:]
+    assert " 0 failed" in r.stdout
