@@ -230,10 +230,12 @@ def run_batch(args):
     circuit = q.createRandomHCCircuit(n, args.depth, args.seed)
     nm = q.NoiseModel()
     nm.addDepolarizingAll(n, args.noise)
+    from qsim_amd.plan import set_jit
+    set_jit(args.jit, -1)  # specialised pass kernels, compiled during the first warmup run
     sem = q.BatchedNoise.Reference if args.batch_noise == "reference" else q.BatchedNoise.Physical
     sim = q.BatchedSimulator(n, B, nm, noise=sem)
     sim.setSeed(args.seed)
-    for _ in range(args.warmup):
+    for _ in range(max(1, args.warmup) if args.jit else args.warmup):
         sim.run(circuit)
     sim.synchronize()
     sim.profile(True)
@@ -244,6 +246,7 @@ def run_batch(args):
     wall = time.perf_counter() - t0
     stats = sim.profileStats()
     sim.profile(False)
+    passes, jit_passes = sim.lastRunInfo()
     gates = circuit.getGateCount()
     gate_stats = [s for s in stats if s["alg_bytes"] > 0]  # (noise kernels carry no byte count)
     dom = max(gate_stats, key=lambda s: s["ms"]) if gate_stats else None
@@ -252,8 +255,16 @@ def run_batch(args):
         per = dom["alg_bytes"] / dom["launches"]
         avg_s = dom["ms"] / dom["launches"] / 1e3
         ach = per / avg_s / 1e9
+        traffic, traffic_src = None, None
+        pmc_path = args.pmc_json or os.path.join(ROOT, "profiles", f"pmc_batch_{n}q.json")
+        if os.path.exists(pmc_path) and args.batch_noise == "physical":
+            with open(pmc_path) as f:
+                ent = json.load(f).get("kernels", {}).get(dom["name"], {})
+            traffic = ent.get("hbm_bytes_per_launch")
+            traffic_src = os.path.relpath(pmc_path, ROOT) if traffic is not None else None
         roof = {"bound": "hbm", "kernel": dom["name"], "achieved": round(ach, 1), "peak": HBM_PEAK_GBPS,
-                "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBPS, 4), "traffic": None,
+                "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBPS, 4), "traffic": traffic,
+                "traffic_source": traffic_src,
                 "alg_bytes_per_launch": per, "avg_launch_ms": round(avg_s * 1e3, 4),
                 "launches": dom["launches"]}
     out = {
@@ -269,7 +280,8 @@ def run_batch(args):
                                      if args.batch_noise == "reference" else
                                      "physical: one draw per trajectory, channel and gate "
                                      "(Pauli frames)"),
-                   "qubits": n, "trajectories": B, "gates": gates, "state_bytes": (16 << n) * B},
+                   "qubits": n, "trajectories": B, "gates": gates, "state_bytes": (16 << n) * B,
+                   "tile_passes": passes, "jit_passes": jit_passes},
         "roofline": roof, "kernels": stats, "cpu_baseline": None,
     }
     print(json.dumps(out))

@@ -114,8 +114,58 @@ __global__ void k_draw_steps(const DevChannel* ch, int nch, uint64_t seed, uint6
     ephase[i] = e;
 }
 
+// Clifford gates move the frame instead of being conjugated by it (Pauli-frame propagation):
+// for a Clifford U, U Phi = (U Phi U^dag) U, so U runs on the stored vector unchanged and the
+// frame becomes U Phi U^dag — again a Pauli.  Per step: {code, q0, q1}; code 0 = not Clifford (the
+// gate is conjugated by the frame in the pass kernels instead).  Rules for Phi = i^E X^F Z^G:
+//   X_q: E += 2 G_q            Z_q: E += 2 F_q              Y_q: E += 2 (F_q ^ G_q)
+//   H_q: swap F_q, G_q; E += 2 (F_q & G_q)
+//   S_q: G_q ^= F_q; E += F_q   Sdag_q: G_q ^= F_q; E += 3 F_q
+//   CNOT(c, t): F_t ^= F_c; G_c ^= G_t      CZ(a, b): G_a ^= F_b; G_b ^= F_a; E += 2 (F_a & F_b)
+//   SWAP(a, b): exchange bits a and b of F and of G.
+enum CliffordCode : int { CL_NONE = 0, CL_X, CL_Y, CL_Z, CL_H, CL_S, CL_SDG, CL_CNOT, CL_CZ, CL_SWAP };
+struct StepClifford {
+    int code, q0, q1, _pad;
+};
+
+__device__ __forceinline__ void clifford_update(const StepClifford& c, uint64_t& F, uint64_t& G, int& E) {
+    const uint64_t a = 1ull << c.q0, bm = 1ull << (c.q1 < 0 ? 0 : c.q1);
+    const int fa = (F & a) != 0, ga = (G & a) != 0;
+    switch (c.code) {
+        case CL_X: E += 2 * ga; break;
+        case CL_Z: E += 2 * fa; break;
+        case CL_Y: E += 2 * (fa ^ ga); break;
+        case CL_H:
+            E += 2 * (fa & ga);
+            F = (F & ~a) | (ga ? a : 0ull);
+            G = (G & ~a) | (fa ? a : 0ull);
+            break;
+        case CL_S: E += fa; if (fa) G ^= a; break;
+        case CL_SDG: E += 3 * fa; if (fa) G ^= a; break;
+        case CL_CNOT: {  // q0 control, q1 target
+            if (fa) F ^= bm;
+            if (G & bm) G ^= a;
+            break;
+        }
+        case CL_CZ: {
+            const int fb = (F & bm) != 0;
+            E += 2 * (fa & fb);
+            if (fb) G ^= a;
+            if (fa) G ^= bm;
+            break;
+        }
+        case CL_SWAP: {
+            const int fb = (F & bm) != 0, gb = (G & bm) != 0;
+            F = (F & ~(a | bm)) | (fb ? a : 0ull) | (fa ? bm : 0ull);
+            G = (G & ~(a | bm)) | (gb ? a : 0ull) | (ga ? bm : 0ull);
+            break;
+        }
+        default: break;
+    }
+}
+
 __global__ void k_frame_build(int count, int batch, uint64_t* frames, const int* ephase,
-                              uint64_t* fin_xz, int* fin_e) {
+                              const StepClifford* cl, uint64_t* fin_xz, int* fin_e) {
     const int b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= batch) return;
     uint64_t F = 0, G = 0;
@@ -124,9 +174,10 @@ __global__ void k_frame_build(int count, int batch, uint64_t* frames, const int*
         const uint64_t i = (uint64_t)s * batch + b;
         uint64_t* fr = frames + 2 * i;
         const uint64_t x = fr[0], z = fr[1];
-        fr[0] = F;
+        fr[0] = F;  // the frame gate s is conjugated by (when it is not Clifford)
         fr[1] = G;
-        E += ephase[i] + ((__popcll(z & F) & 1) ? 2 : 0);
+        clifford_update(cl[s], F, G, E);
+        E += ephase[i] + ((__popcll(z & F) & 1) ? 2 : 0);  // then this step's noise: P Phi
         F ^= x;
         G ^= z;
     }
@@ -192,9 +243,11 @@ struct qsim_batch {
     int* d_fe = nullptr;           // per-(step, trajectory) draw phases (frame build scratch)
     size_t frames_cap = 0;
     DevBuf ops, stages;             // fused-plan descriptors
+    DevBuf cliff;                   // per-step Clifford codes of the current run (frame build)
     PlanCache plans;
     Timer timer;
     Scratch scratch, scratch2;
+    int last_passes = 0, last_jit_passes = 0;
     ~qsim_batch() {
         if (stream) (void)hipStreamSynchronize(stream);
         if (d) (void)hipFree(d);
@@ -335,13 +388,22 @@ int qsim_batch_run(qsim_batch* b, const qsim_gate* gates, size_t count,
             // Fused tile passes over all trajectories (a tile never straddles two).  Noise is
             // carried as per-trajectory Pauli frames: no noise kernel per gate, one frame build
             // before and one materialising Pauli pass after the circuit.
+            const bool noisy = !ch.empty() && count > 0;
             std::vector<Op> fops;
+            std::vector<StepClifford> cl(count, StepClifford{CL_NONE, 0, -1, 0});
             for (size_t i = 0; i < ops.size(); ++i) {
                 if (ops[i].kind < 0) continue;  // ignored by the reference gate set
+                const qsim_gate& g = gates[i];
+                static const int code_of[QSIM_GATE_COUNT] = {
+                    CL_X, CL_Y, CL_Z, CL_H, CL_S, CL_NONE /*T*/, CL_SDG, CL_NONE /*Tdag*/,
+                    CL_NONE, CL_NONE, CL_NONE /*Rx Ry Rz*/, CL_CNOT, CL_CZ, CL_NONE, CL_NONE /*CRY CRZ*/,
+                    CL_SWAP, CL_NONE /*Toffoli*/};
+                cl[i] = StepClifford{code_of[g.type], g.qubits[0], g.nqubits > 1 ? g.qubits[1] : -1, 0};
                 fops.push_back(ops[i]);
-                fops.back().src = (int)i;       // circuit step (frame index)
+                // circuit step = frame index for ops conjugated by the frame; Clifford gates move
+                // the frame instead and run unconjugated (src -1)
+                fops.back().src = (noisy && cl[i].code == CL_NONE) ? (int)i : -1;
             }
-            const bool noisy = !ch.empty() && count > 0;
             if (noisy) {
                 const size_t need_frames = 2 * count * (size_t)b->batch;
                 if (need_frames > b->frames_cap) {
@@ -359,17 +421,29 @@ int qsim_batch_run(qsim_batch* b, const qsim_gate* gates, size_t count,
                 hipLaunchKernelGGL(k_draw_steps, dim3((unsigned)((draws + 255) / 256)), dim3(256), 0,
                                    b->stream, b->d_ch, (int)ch.size(), b->seed, b->step, (int)count,
                                    b->batch, b->d_frames, b->d_fe);
+                b->cliff.upload(cl.data(), cl.size() * sizeof(StepClifford), b->stream);
                 hipLaunchKernelGGL(k_frame_build, dim3((b->batch + 63) / 64), dim3(64), 0, b->stream,
-                                   (int)count, b->batch, b->d_frames, b->d_fe, b->d_xz, b->d_e);
+                                   (int)count, b->batch, b->d_frames, b->d_fe,
+                                   (const StepClifford*)b->cliff.ptr, b->d_xz, b->d_e);
                 QSIM_HIPCHK(hipGetLastError());
             }
             if (!fops.empty()) {
-                const Plan& plan = b->plans.get(fops, b->n, b->stream).plan;
+                PlanCache::Entry& pe = b->plans.get(fops, b->n, b->stream);
+                const Plan& plan = pe.plan;
+                // circuit-specialised kernels for the passes no frame conjugation reaches (all of
+                // them for a Clifford circuit); the JIT threshold counts the whole batch
+                int eff = b->n;
+                while ((1ll << (eff - b->n)) < (long long)b->batch) ++eff;
+                const JitModule* jm = jit_for(pe.jit, plan, eff);
                 b->ops.upload(plan.ops.data(), plan.ops.size() * sizeof(TileOp), b->stream);
                 b->stages.upload(plan.stages.data(), plan.stages.size() * sizeof(Stage), b->stream);
                 launch_fused(b->d, b->n, (uint64_t)b->batch, plan, (const TileOp*)b->ops.ptr,
-                             (const Stage*)b->stages.ptr, b->stream, &b->timer, nullptr,
+                             (const Stage*)b->stages.ptr, b->stream, &b->timer, jm,
                              noisy ? b->d_frames : nullptr);
+                b->last_passes = (int)plan.passes.size();
+                b->last_jit_passes = 0;
+                if (jm)
+                    for (hipFunction_t f : jm->fn) b->last_jit_passes += f != nullptr;
             }
             if (noisy) {
                 b->step += count;
@@ -473,6 +547,14 @@ int qsim_batch_device_ptr(qsim_batch* b, void** dptr) {
     return bguard([&] {
         need(b);
         *dptr = b->d;
+    });
+}
+
+int qsim_batch_last_run(qsim_batch* b, int* passes, int* jit_passes) {
+    return bguard([&] {
+        need(b);
+        if (passes) *passes = b->last_passes;
+        if (jit_passes) *jit_passes = b->last_jit_passes;
     });
 }
 

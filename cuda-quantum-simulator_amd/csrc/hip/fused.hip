@@ -998,8 +998,11 @@ __global__ __launch_bounds__(256, 2) void k_fused_staged(FArgs a) {  // 2 WGs/CU
         }
         if constexpr (FR) {
             const uint64_t traj = tile_id >> a.log_tpt;
-            for (int o = sg.op_begin; o < sg.op_end; ++o)
-                stage_op_frame<RB>(v, jb, ldc(a.ops, o), a.frames, a.nbatch, traj);
+            for (int o = sg.op_begin; o < sg.op_end; ++o) {
+                const TileOp op = ldc(a.ops, o);
+                if (op.step < 0) stage_op<RB>(v, jb, op);  // Clifford: moved the frame instead
+                else stage_op_frame<RB>(v, jb, op, a.frames, a.nbatch, traj);
+            }
         } else {
             for (int o = sg.op_begin; o < sg.op_end; ++o) stage_op<RB>(v, jb, ldc(a.ops, o));
         }
@@ -1058,10 +1061,14 @@ void launch_fused(double2* st, int n, uint64_t batch, const Plan& plan, const Ti
         a.tpt_mask = (1ull << lt) - 1ull;
         const uint64_t blocks = batch << lt;
         TimedLaunch tl(tm, "fused_tile", pass_bytes * (p.alg_bpa / 32.0), s);
-        if (frames) {  // batched noisy run: general arms under the trajectory's Pauli frame
+        bool framed = false;  // does any op of this pass run conjugated by the Pauli frame?
+        if (frames)
+            for (int k = p.stage_begin; k < p.stage_end && !framed; ++k)
+                for (int o = plan.stages[k].op_begin; o < plan.stages[k].op_end; ++o)
+                    if (plan.ops[o].step >= 0) framed = true;
+        if (framed) {  // batched noisy run: non-Clifford ops under the trajectory's Pauli frame
             a.frames = frames;
             a.nbatch = (int)batch;
-            a.scale = 1.0;  // H runs as its normalised matrix here
             switch (p.h) {
                 case 4: hipLaunchKernelGGL((k_fused_staged<4, true, true>), dim3((unsigned)blocks), dim3(256), 0, s, a); break;
                 case 5: hipLaunchKernelGGL((k_fused_staged<5, true, true>), dim3((unsigned)blocks), dim3(256), 0, s, a); break;

@@ -114,6 +114,7 @@ _sig(hip, "qsim_batch_traj_probabilities", [_P, c_int, _P])
 _sig(hip, "qsim_batch_traj_state", [_P, c_int, _P])
 _sig(hip, "qsim_batch_sample", [_P, _P, c_int, _P])
 _sig(hip, "qsim_state_last_run", [_P, _P, _P])
+_sig(hip, "qsim_batch_last_run", [_P, _P, _P])
 _sig(hip, "qsim_batch_histogram", [_P, _P, c_int, _P])
 _sig(hip, "qsim_batch_device_ptr", [_P, POINTER(_P)])
 _sig(hip, "qsim_batch_sync", [_P])

@@ -529,6 +529,12 @@ class BatchedSimulator:
     def getBatchSize(self) -> int: return self._b
     def getTotalMemoryBytes(self) -> int: return self._b * (1 << self._n) * 16
 
+    def lastRunInfo(self):
+        """(tile passes, passes run by circuit-specialised kernels) of the last fused run."""
+        p, j = _c.c_int(0), _c.c_int(0)
+        _lib.check(_lib.hip.qsim_batch_last_run(self._h, _c.byref(p), _c.byref(j)))
+        return p.value, j.value
+
     def profile(self, enable: bool = True) -> None:
         _lib.check(_lib.hip.qsim_batch_profile(self._h, 1 if enable else 0))
 

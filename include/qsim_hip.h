@@ -203,6 +203,8 @@ int qsim_batch_sample(qsim_batch* b, const double* uniforms, int shots, int64_t*
 int qsim_batch_histogram(qsim_batch* b, const double* uniforms, int shots, int64_t* hist);
 int qsim_batch_device_ptr(qsim_batch* b, void** dptr);
 int qsim_batch_sync(qsim_batch* b);
+/* Last fused batched run: tile passes and how many ran as circuit-specialised kernels. */
+int qsim_batch_last_run(qsim_batch* b, int* passes, int* jit_passes);
 int qsim_batch_profile(qsim_batch* b, int enable);
 int qsim_batch_profile_count(qsim_batch* b, int* n);
 int qsim_batch_profile_get(qsim_batch* b, int i, char* name, size_t name_len,
