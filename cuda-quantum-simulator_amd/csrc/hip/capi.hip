@@ -409,6 +409,78 @@ int qsim_apply_matrix2q(qsim_state* s, int q0, int q1, const double m[32], const
     });
 }
 
+int qsim_apply_matrix(qsim_state* s, const int* targets, int k, const double* m,
+                      const int* controls, int n_controls) {
+    return guarded([&] {
+        check_state(s);
+        QSIM_REQUIRE(m && targets, QSIM_ERR_INVALID_ARGUMENT, "null matrix or targets");
+        QSIM_REQUIRE(controls || n_controls == 0, QSIM_ERR_INVALID_ARGUMENT, "null controls");
+        if (k < 1 || k > 8) fail(QSIM_ERR_INVALID_ARGUMENT, "matrix must act on 1 to 8 qubits");
+        uint64_t used = 0, cm = 0;
+        for (int j = 0; j < k; ++j) {
+            const int q = targets[j];
+            if (q < 0 || q >= s->n) fail(QSIM_ERR_OUT_OF_RANGE, "Qubit index " + std::to_string(q) + " out of range");
+            if ((used >> q) & 1ull) fail(QSIM_ERR_INVALID_ARGUMENT, "target qubits must be distinct");
+            used |= 1ull << q;
+        }
+        for (int i = 0; i < n_controls; ++i) {
+            const int c = controls[i];
+            if (c < 0 || c >= s->n) fail(QSIM_ERR_OUT_OF_RANGE, "Qubit index " + std::to_string(c) + " out of range");
+            if ((used >> c) & 1ull)
+                fail(QSIM_ERR_INVALID_ARGUMENT, "control qubits must be distinct from the targets");
+            used |= 1ull << c;
+            cm |= 1ull << c;
+        }
+        DeviceGuard dg(s->device);
+        const int dim = 1 << k;
+        std::vector<double> mt(2 * (size_t)dim * dim);  // transpose: mt[c][r] = M[r][c]
+        for (int r = 0; r < dim; ++r)
+            for (int c = 0; c < dim; ++c) {
+                mt[2 * ((size_t)c * dim + r)] = m[2 * ((size_t)r * dim + c)];
+                mt[2 * ((size_t)c * dim + r) + 1] = m[2 * ((size_t)r * dim + c) + 1];
+            }
+        double2* d_mt = (double2*)s->scratch.get(mt.size() * sizeof(double), s->stream);
+        QSIM_HIPCHK(hipMemcpyAsync(d_mt, mt.data(), mt.size() * sizeof(double), hipMemcpyHostToDevice,
+                                   s->stream));
+        launch_matrixk(s->d, s->n, targets, k, d_mt, cm, s->stream, &s->timer);
+        // the matrix lives in the state's scratch: wait before the next user may reuse it
+        QSIM_HIPCHK(hipStreamSynchronize(s->stream));
+    });
+}
+
+int qsim_apply_hadamard_optimized(void* dstate, int n_qubits, int target, void* stream) {
+    qsim_gate g{};
+    g.type = QSIM_GATE_H;
+    g.nqubits = 1;
+    g.qubits[0] = target;
+    return qsim_apply_gate_raw(dstate, n_qubits, &g, stream);
+}
+
+int qsim_apply_cnot_optimized(void* dstate, int n_qubits, int control, int target, void* stream) {
+    qsim_gate g{};
+    g.type = QSIM_GATE_CNOT;
+    g.nqubits = 2;
+    g.qubits[0] = control;
+    g.qubits[1] = target;
+    return qsim_apply_gate_raw(dstate, n_qubits, &g, stream);
+}
+
+int qsim_apply_matrix1q_raw(void* dstate, int n_qubits, int target, const double m[8], void* stream) {
+    return guarded([&] {
+        QSIM_REQUIRE(dstate && m, QSIM_ERR_INVALID_ARGUMENT, "null argument");
+        if (n_qubits < 1 || n_qubits > QSIM_MAX_QUBITS_SINGLE)
+            fail(QSIM_ERR_INVALID_ARGUMENT, "Number of qubits must be between 1 and 30");
+        if (target < 0 || target >= n_qubits)
+            fail(QSIM_ERR_OUT_OF_RANGE, "Qubit index " + std::to_string(target) + " out of range");
+        Op op;
+        op.kind = K_M1;
+        op.sub = S_GEN;
+        op.t0 = target;
+        for (int i = 0; i < 8; ++i) op.m[i] = m[i];
+        launch_op((double2*)dstate, n_qubits, 1, op, (hipStream_t)stream, nullptr);
+    });
+}
+
 int qsim_apply_diagonal_layer(qsim_state* s, const double* gp, uint64_t active) {
     return guarded([&] {
         check_state(s);

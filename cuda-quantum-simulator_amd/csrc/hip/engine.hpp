@@ -85,6 +85,10 @@ struct Timer;  // per-launch HIP-event attribution (capi.hip)
 // Apply one op to `batch` contiguous trajectories of 2^n amplitudes each.
 void launch_op(double2* st, int n, uint64_t batch, const Op& op, hipStream_t s, Timer* tm);
 
+// General 2^k x 2^k matrix (k <= 8) on `targets` (matrix-index bit j = targets[j]), d_mt the
+// device copy of the transposed matrix, controlled on cmask.
+void launch_matrixk(double2* st, int n, const int* targets, int k, const double2* d_mt,
+                    uint64_t cmask, hipStream_t s, Timer* tm);
 // General 4x4 on qubits (q0, q1) (m row-major over (b1 << 1) | b0, re/im interleaved), controlled.
 void launch_matrix2q(double2* st, int n, int q0, int q1, const double* m, uint64_t cmask,
                      hipStream_t s, Timer* tm);

@@ -615,4 +615,79 @@ void launch_matrix2q(double2* st, int n, int q0, int q1, const double* m, uint64
     QSIM_HIPCHK(hipGetLastError());
 }
 
+// ---------------------------------------------------------------------------------------
+// General k-qubit matrix, k <= 8 (SURVEY §8(f) rank 3 "k-qubit unitary with controls"; the
+// reference stops at the 2x2 applyGate1Q_opt, src/OptimizedGates.cu:165-183).  A workgroup of 256
+// threads holds 256 / 2^k groups of 2^k amplitudes in LDS; thread (group, r) loads amplitude r of
+// its group, then computes output row r = sum_c M[r][c] v[c] from LDS (broadcast reads) and the
+// transposed matrix mt[c][r] (consecutive lanes read consecutive entries; the matrix stays in
+// L2), and stores it in place.  Each group is the control == 1 subspace of one assignment of the
+// other qubits (zero insertion at the sorted target + control positions).
+// ---------------------------------------------------------------------------------------
+struct MkArgs {
+    double2* st;
+    const double2* mt;   // transposed matrix: mt[c * 2^k + r] = M[r][c]
+    uint64_t groups;
+    uint64_t setmask;    // control bits forced to 1
+    int k, nfix;
+    int fix[64];         // ascending target + control positions
+    int tq[8];           // target qubit of matrix-index bit j
+};
+
+__global__ __launch_bounds__(256) void k_mk(MkArgs a) {
+    __shared__ double2 v[256];
+    const int dim = 1 << a.k;
+    const int gpb = 256 >> a.k;  // groups per block
+    const int t = threadIdx.x;
+    const int lg = t >> a.k, r = t & (dim - 1);
+    for (uint64_t g0 = (uint64_t)blockIdx.x * gpb; g0 < a.groups; g0 += (uint64_t)gridDim.x * gpb) {
+        const uint64_t g = g0 + (uint64_t)lg;
+        const bool live = g < a.groups;
+        uint64_t idx = 0;
+        if (live) {
+            uint64_t i = g;
+            for (int q = 0; q < a.nfix; ++q) {
+                const uint64_t lo = i & ((1ull << a.fix[q]) - 1ull);
+                i = ((i ^ lo) << 1) | lo;
+            }
+            idx = i | a.setmask;
+            for (int j = 0; j < a.k; ++j)
+                if ((r >> j) & 1) idx |= 1ull << a.tq[j];
+            v[t] = a.st[idx];
+        }
+        __syncthreads();
+        if (live) {
+            double2 acc = make_double2(0.0, 0.0);
+            const double2* grp = v + (lg << a.k);
+            for (int c = 0; c < dim; ++c) acc = cadd(acc, cmul(a.mt[(uint64_t)c * dim + r], grp[c]));
+            a.st[idx] = acc;
+        }
+        __syncthreads();
+    }
+}
+
+void launch_matrixk(double2* st, int n, const int* targets, int k, const double2* d_mt,
+                    uint64_t cmask, hipStream_t s, Timer* tm) {
+    if (k < 1 || k > 8) fail(QSIM_ERR_INVALID_ARGUMENT, "matrix must act on 1 to 8 qubits");
+    MkArgs a{};
+    a.st = st;
+    a.mt = d_mt;
+    a.k = k;
+    a.setmask = cmask;
+    uint64_t fixed = cmask;
+    for (int j = 0; j < k; ++j) {
+        a.tq[j] = targets[j];
+        fixed |= 1ull << targets[j];
+    }
+    for (int q = 0; q < n; ++q)
+        if ((fixed >> q) & 1ull) a.fix[a.nfix++] = q;
+    if (a.nfix > n) fail(QSIM_ERR_INVALID_ARGUMENT, "too many fixed qubits");
+    a.groups = 1ull << (n - a.nfix);
+    const uint64_t gpb = 256ull >> k;
+    const uint64_t blocks = std::min<uint64_t>((a.groups + gpb - 1) / gpb, 256ull * 64);
+    TimedLaunch tl(tm, "matrixk", 32.0 * (double)(a.groups << k), s);
+    hipLaunchKernelGGL(k_mk, dim3((unsigned)blocks), dim3(256), 0, s, a);
+    QSIM_HIPCHK(hipGetLastError());
+}
+
 }  // namespace qsim_hip

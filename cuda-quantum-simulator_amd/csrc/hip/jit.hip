@@ -77,7 +77,9 @@ std::string hexu(uint64_t x) {
     return b;
 }
 
-const char* kPrelude = R"(
+// HBM access of the generated passes: non-temporal by default (a pass touches every amplitude
+// once); QSIM_JIT_NT=0 uses the default cache policy (Infinity Cache residency experiments).
+const char* kPreludeNT = R"(
 typedef double qdv2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ double2 qld(const double2* p) {
   const qdv2 t = __builtin_nontemporal_load(reinterpret_cast<const qdv2*>(p));
@@ -87,6 +89,12 @@ __device__ __forceinline__ void qst(double2* p, double2 v) {
   qdv2 t; t.x = v.x; t.y = v.y;
   __builtin_nontemporal_store(t, reinterpret_cast<qdv2*>(p));
 }
+)";
+const char* kPreludeT = R"(
+__device__ __forceinline__ double2 qld(const double2* p) { return *p; }
+__device__ __forceinline__ void qst(double2* p, double2 v) { *p = v; }
+)";
+const char* kPrelude = R"(
 __device__ __forceinline__ double2 qsel(bool c, double2 a, double2 b) {
   return make_double2(c ? a.x : b.x, c ? a.y : b.y);
 }
@@ -332,7 +340,7 @@ static std::vector<char> jit_selection(const Plan& plan) {
 std::string jit_source(const Plan& plan) {
     std::ostringstream out;
     bool any = false;
-    out << kPrelude;
+    out << (env_or("QSIM_JIT_NT", 1) ? kPreludeNT : kPreludeT) << kPrelude;
     const std::vector<char> sel = jit_selection(plan);
     for (size_t i = 0; i < plan.passes.size(); ++i) {
         if (!sel[i]) continue;

@@ -63,6 +63,20 @@ void StateVector::applyMatrix1Q(int target, const std::complex<double> (&m)[4],
                               (int)controls.size()));
 }
 
+void StateVector::applyMatrix(const std::vector<int>& targets, const std::vector<std::complex<double>>& m,
+                              const std::vector<int>& controls) {
+    const size_t dim = size_t(1) << targets.size();
+    if (targets.empty() || targets.size() > 8 || m.size() != dim * dim)
+        throw std::invalid_argument("matrix must be 2^k x 2^k for 1 <= k <= 8 targets");
+    std::vector<double> mm(2 * m.size());
+    for (size_t i = 0; i < m.size(); ++i) {
+        mm[2 * i] = m[i].real();
+        mm[2 * i + 1] = m[i].imag();
+    }
+    check(qsim_apply_matrix(h_, targets.data(), (int)targets.size(), mm.data(),
+                            controls.empty() ? nullptr : controls.data(), (int)controls.size()));
+}
+
 void StateVector::initializeZero() { check(qsim_state_init_zero(h_)); }
 
 void StateVector::initializeBasis(size_t basis_idx) {

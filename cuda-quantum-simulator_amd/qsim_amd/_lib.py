@@ -83,6 +83,10 @@ _sig(hip, "qsim_apply_gate", [_P, POINTER(qsim_gate)])
 _sig(hip, "qsim_run", [_P, POINTER(qsim_gate), c_size_t, c_int])
 _sig(hip, "qsim_apply_matrix1q", [_P, c_int, POINTER(c_double), POINTER(c_int), c_int])
 _sig(hip, "qsim_apply_matrix2q", [_P, c_int, c_int, POINTER(c_double), POINTER(c_int), c_int])
+_sig(hip, "qsim_apply_matrix", [_P, POINTER(c_int), c_int, POINTER(c_double), POINTER(c_int), c_int])
+_sig(hip, "qsim_apply_hadamard_optimized", [_P, c_int, c_int, _P])
+_sig(hip, "qsim_apply_cnot_optimized", [_P, c_int, c_int, c_int, _P])
+_sig(hip, "qsim_apply_matrix1q_raw", [_P, c_int, c_int, POINTER(c_double), _P])
 _sig(hip, "qsim_apply_diagonal_layer", [_P, POINTER(c_double), c_uint64])
 _sig(hip, "qsim_apply_gate_raw", [_P, c_int, POINTER(qsim_gate), _P])
 _sig(hip, "qsim_plan_fused", [c_int, POINTER(qsim_gate), c_size_t, c_int, _P, _P,

@@ -191,6 +191,20 @@ class StateVector:
         ctl = (_c.c_int * max(1, len(controls)))(*controls)
         _lib.check(_lib.hip.qsim_apply_matrix2q(self._h, q0, q1, buf, ctl, len(controls)))
 
+    def applyMatrix(self, targets: Sequence[int], m, controls: Sequence[int] = ()) -> None:
+        """General 2^k x 2^k matrix, k = len(targets) <= 8, row-major; matrix-index bit j is
+        qubit targets[j]; applied on the control == 1 subspace (qsim_apply_matrix)."""
+        k = len(targets)
+        mm = np.asarray(m, dtype=np.complex128)
+        if k < 1 or k > 8 or mm.size != (1 << k) ** 2:
+            raise ValueError("matrix must be 2^k x 2^k for 1 <= k <= 8 targets")
+        buf = np.ascontiguousarray(mm.reshape(-1)).view(np.float64)
+        tg = (_c.c_int * k)(*targets)
+        ctl = (_c.c_int * max(1, len(controls)))(*controls)
+        _lib.check(_lib.hip.qsim_apply_matrix(self._h, tg, k,
+                                              buf.ctypes.data_as(_c.POINTER(_c.c_double)),
+                                              ctl, len(controls)))
+
     def applyDiagonalLayer(self, gate_params, active_qubits: int) -> None:
         """applyFusedSingleQubitLayer (src/OptimizedGates.cu:344-382): gate_params[q][0] / [q][3]
         scale the bit-q = 0 / 1 amplitudes of every active qubit."""

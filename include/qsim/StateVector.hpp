@@ -44,6 +44,10 @@ public:
     // applyGate1Q_coalesced, plus controls); std::out_of_range / std::invalid_argument on bad qubits.
     void applyMatrix1Q(int target, const std::complex<double> (&m)[4],
                        const std::vector<int>& controls = {});
+    // General 2^k x 2^k matrix (row-major, k = targets.size() <= 8; matrix-index bit j = qubit
+    // targets[j]) on the control == 1 subspace (qsim_apply_matrix).
+    void applyMatrix(const std::vector<int>& targets, const std::vector<std::complex<double>>& m,
+                     const std::vector<int>& controls = {});
 
     std::vector<std::complex<double>> toHost() const;
     void fromHost(const std::vector<std::complex<double>>& amplitudes);

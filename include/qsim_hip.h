@@ -110,6 +110,19 @@ int qsim_apply_matrix1q(qsim_state* s, int target, const double m[8],
  * optionally controlled (the k = 2 applyMatrix of SURVEY §8(f) rank 3).  Asynchronous. */
 int qsim_apply_matrix2q(qsim_state* s, int q0, int q1, const double m[32], const int* controls,
                         int n_controls);
+/* General 2^k x 2^k complex matrix on k <= 8 target qubits (generalises
+ * applyGate1Q_opt, src/OptimizedGates.cu:165-183, and cuStateVec's applyMatrix used by
+ * benchmarks/benchmark_custatevec.cu:131-135): m row-major, re/im interleaved, matrix-index bit j
+ * = bit targets[j] of the amplitude index; applied on the control == 1 subspace of `controls`.
+ * Asynchronous; synchronises before returning (the matrix is staged in device scratch). */
+int qsim_apply_matrix(qsim_state* s, const int* targets, int k, const double* m,
+                      const int* controls, int n_controls);
+/* Named dispatchers of the reference (src/OptimizedGates.cu:388-413, declared in
+ * include/OptimizedGates.cuh:161-166) on a raw device pointer and stream, routed to this build's
+ * per-gate kernels; applyGate1Q_opt's general 2x2 as qsim_apply_matrix1q_raw. */
+int qsim_apply_hadamard_optimized(void* dstate, int n_qubits, int target, void* stream);
+int qsim_apply_cnot_optimized(void* dstate, int n_qubits, int control, int target, void* stream);
+int qsim_apply_matrix1q_raw(void* dstate, int n_qubits, int target, const double m[8], void* stream);
 /* applyFusedSingleQubitLayer (src/OptimizedGates.cu:344-382): for every qubit q in `active`,
  * amplitudes with bit q = 0 are scaled by gate_params[q*4+0] and those with bit q = 1 by
  * gate_params[q*4+3] (complex, re/im interleaved: 8 doubles per qubit).  Runs as fused passes. */

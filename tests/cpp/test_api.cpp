@@ -5,6 +5,7 @@
 #include <qsim/Circuit.hpp>
 #include <qsim/DensityMatrix.hpp>
 #include <qsim/NoiseModel.hpp>
+#include <qsim/OptimizedGates.hpp>
 #include <qsim/Simulator.hpp>
 #include <qsim/StateVector.hpp>
 
@@ -405,6 +406,45 @@ TEST(Scaling, GpuMatchesCpuSimulator) {
         cpu_sim.run(c);
         expect_state(gpu_sim.getStateVector(), cpu_sim.getStateVector(), kEquivTol);
     }
+}
+
+// src/OptimizedGates.cu:388-413 named dispatchers on StateVector::devicePtr() (the reference's
+// tests/test_optimized_gates.cu drive them the same way) == the same gates via the simulator.
+TEST(OptimizedGates, NamedDispatchers) {
+    const int n = 9;
+    qsim::StateVector sv(n);
+    qsim::applyHadamardOptimized(sv.devicePtr(), n, 2);
+    qsim::applyCNOTOptimized(sv.devicePtr(), n, 2, 7);
+    const std::complex<double> x[4] = {0.0, 1.0, 1.0, 0.0};
+    qsim::applyGate1QOptimized(sv.devicePtr(), n, 5, x);
+    qsim::StateVector ref(n);
+    qsim::Circuit c(n);
+    c.h(2).cnot(2, 7).x(5);
+    qsim::Simulator sim(n);
+    sim.run(c);
+    expect_state(sv.toHost(), sim.getStateVector(), kEquivTol);
+}
+
+// qsim_apply_matrix (k-qubit general matrix): a 3-qubit permutation matrix == the gates it encodes.
+TEST(StateVector, GeneralMatrixK3) {
+    const int n = 8;
+    qsim::StateVector sv(n);
+    qsim::Circuit prep(n);
+    prep.h(0).h(3).h(5).ry(6, 0.3);
+    qsim::Simulator sim(n);
+    sim.run(prep);
+    sv.fromHost(sim.getStateVector());
+    // Toffoli(c1 = qubit 5 (bit 0), c2 = qubit 3 (bit 1), target = qubit 6 (bit 2)) as an 8x8
+    std::vector<std::complex<double>> m(64, 0.0);
+    for (int r = 0; r < 8; ++r) {
+        const int c = (r & 3) == 3 ? r ^ 4 : r;
+        m[r * 8 + c] = 1.0;
+    }
+    sv.applyMatrix({5, 3, 6}, m);
+    qsim::Circuit t(n);
+    t.toffoli(5, 3, 6);
+    sim.applyGate(t.getGates()[0]);
+    expect_state(sv.toHost(), sim.getStateVector(), kEquivTol);
 }
 
 TH_MAIN

@@ -103,3 +103,75 @@ def test_matrix1q_many_high_controls(qsim, gpu_ready, target, controls):
     sv.applyMatrix1Q(target, u, controls)
     np.testing.assert_allclose(sv.toHost(), _numpy_controlled_1q(psi, n, target, u, controls),
                                atol=1e-12, rtol=0)
+
+
+def _numpy_apply_k(state, n, targets, m, controls=()):
+    """Dense reference: out[i] = sum_c M[r(i)][c] psi[i with target bits = c] on control == 1."""
+    out = state.copy()
+    k = len(targets)
+    idx = np.arange(1 << n)
+    sel = np.ones(1 << n, bool)
+    for c in controls:
+        sel &= ((idx >> c) & 1) == 1
+    for t in targets:
+        sel &= ((idx >> t) & 1) == 0
+    base = idx[sel]
+    cols = []
+    for c in range(1 << k):
+        off = 0
+        for j, t in enumerate(targets):
+            if (c >> j) & 1:
+                off |= 1 << t
+        cols.append(base | off)
+    vec = np.stack([state[ci] for ci in cols])  # (2^k, groups)
+    res = m @ vec
+    for r, ci in enumerate(cols):
+        out[ci] = res[r]
+    return out
+
+
+@pytest.mark.parametrize("targets,controls", [([3], []), ([0, 7], [2]), ([1, 5, 9], []),
+                                              ([11, 2, 6], [0, 8]), ([0, 1, 2, 3], [10]),
+                                              ([4, 9, 1, 7, 11], []), ([2, 3, 4, 5, 6, 7, 8, 9], [11])])
+def test_matrix_k_qubits(qsim, gpu_ready, targets, controls):
+    """General k-qubit matrix (qsim_apply_matrix, k <= 8) vs dense numpy on a random state."""
+    n = 12
+    rng = np.random.default_rng(len(targets) * 13 + len(controls))
+    psi = _rand_state(n, 40 + len(targets))
+    d = 1 << len(targets)
+    a = rng.normal(size=(d, d)) + 1j * rng.normal(size=(d, d))
+    u, _ = np.linalg.qr(a)
+    sv = qsim.StateVector(n)
+    sv.fromHost(psi)
+    sv.applyMatrix(targets, u, controls)
+    np.testing.assert_allclose(sv.toHost(), _numpy_apply_k(psi, n, targets, u, controls),
+                               atol=1e-12, rtol=0)
+
+
+def test_matrix_k_rejects_bad_input(qsim, gpu_ready):
+    sv = qsim.StateVector(6)
+    with pytest.raises(ValueError):
+        sv.applyMatrix([1, 1], np.eye(4))
+    with pytest.raises(IndexError):
+        sv.applyMatrix([6], np.eye(2))
+    with pytest.raises(ValueError):
+        sv.applyMatrix([0, 1], np.eye(4), controls=[1])
+
+
+def test_named_optimized_dispatchers(qsim, oracle, gpu_ready):
+    """applyHadamardOptimized / applyCNOTOptimized / applyGate1Q_opt (src/OptimizedGates.cu:
+    388-413) on a raw device pointer == the same gates through the simulator."""
+    import ctypes
+    from qsim_amd import _lib
+    n = 10
+    psi = _rand_state(n, 77)
+    sv = qsim.StateVector(n)
+    sv.fromHost(psi)
+    ptr, stream = sv.devicePtr(), ctypes.c_void_p(sv.stream())
+    _lib.check(_lib.hip.qsim_apply_hadamard_optimized(ptr, n, 3, stream))
+    _lib.check(_lib.hip.qsim_apply_cnot_optimized(ptr, n, 3, 8, stream))
+    ry = oracle.gate_matrix(9, [0], 0.7)[0]
+    buf = (ctypes.c_double * 8)(*[v for z in ry.reshape(4) for v in (z.real, z.imag)])
+    _lib.check(_lib.hip.qsim_apply_matrix1q_raw(ptr, n, 6, buf, stream))
+    ref = oracle.run_cpu(n, [(3, [3], 0.0), (11, [3, 8], 0.0), (9, [6], 0.7)], state=psi)
+    np.testing.assert_allclose(sv.toHost(), ref, atol=1e-12, rtol=0)
