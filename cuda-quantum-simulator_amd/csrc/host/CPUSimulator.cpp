@@ -6,10 +6,13 @@
 //     so results agree to the last bit for X/Y/Z/H/S/T/S†/T†/CNOT/CZ/SWAP) or a 2x2 complex
 //     matrix for the rotations — with its controls as forced-1 bits of the pair index, so only
 //     the control == 1 subspace is visited (the reference scans all 2^n indices for CNOT);
-//   * the pair range is split into contiguous blocks over worker threads (std::thread; states
-//     below 2^14 amplitudes stay on the calling thread).
+//   * the pair range is split into contiguous blocks over a persistent worker pool (states below
+//     2^17 amplitudes stay on the calling thread).
 #include <algorithm>
 #include <cmath>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
 #include <numeric>
 #include <stdexcept>
 #include <string>
@@ -94,24 +97,83 @@ inline uint64_t insert_zeros(uint64_t k, const int* pos, int npos) {
     return k;
 }
 
-template <typename F>
-void parallel_blocks(uint64_t units, int threads, F&& body) {
-    if (threads <= 1 || units < (1ull << 13)) {
+constexpr uint64_t kSerialUnits = 1ull << 16;  // below this many pairs: the calling thread
+
+}  // namespace
+
+// Persistent worker pool: `run(parts, fn)` calls fn(part) for part in [0, parts) on the workers
+// and the calling thread, and returns when all are done.  Waking parked threads costs a few
+// microseconds, not the tens of a thread spawn per gate.
+struct CPUSimulator::Pool {
+    explicit Pool(int n) {
+        for (int i = 1; i < n; ++i) workers.emplace_back([this, i] { loop(i); });
+        size = n;
+    }
+    ~Pool() {
+        {
+            std::lock_guard<std::mutex> l(mu);
+            stop = true;
+            ++gen;
+        }
+        cv.notify_all();
+        for (auto& t : workers) t.join();
+    }
+    template <typename F>
+    void run(int parts, F&& fn) {
+        std::lock_guard<std::mutex> serial(run_mu);  // copies of one simulator share the pool
+        {
+            std::lock_guard<std::mutex> l(mu);
+            job = [&fn](int p) { fn(p); };
+            nparts = std::min(parts, size);
+            pending = nparts - 1;
+            ++gen;
+        }
+        cv.notify_all();
+        fn(0);
+        std::unique_lock<std::mutex> l(mu);
+        done_cv.wait(l, [&] { return pending == 0; });
+        job = nullptr;
+    }
+    void loop(int id) {
+        uint64_t seen = 0;
+        for (;;) {
+            std::function<void(int)> j;
+            {
+                std::unique_lock<std::mutex> l(mu);
+                cv.wait(l, [&] { return gen != seen; });
+                seen = gen;
+                if (stop) return;
+                if (id >= nparts) continue;
+                j = job;
+            }
+            j(id);
+            std::lock_guard<std::mutex> l(mu);
+            if (--pending == 0) done_cv.notify_one();
+        }
+    }
+    std::vector<std::thread> workers;
+    std::mutex mu, run_mu;
+    std::condition_variable cv, done_cv;
+    std::function<void(int)> job;
+    uint64_t gen = 0;
+    int size = 1, nparts = 0, pending = 0;
+    bool stop = false;
+};
+
+namespace {
+template <typename P, typename F>
+void parallel_blocks(P* pool, uint64_t units, F&& body) {
+    if (!pool || pool->size <= 1 || units < kSerialUnits) {
         body(0, units);
         return;
     }
-    const int t = (int)std::min<uint64_t>((uint64_t)threads, units >> 12);
-    std::vector<std::thread> pool;
-    pool.reserve(t - 1);
-    const uint64_t per = (units + t - 1) / t;
-    for (int i = 1; i < t; ++i) {
-        const uint64_t b = per * i, e = std::min(units, b + per);
-        if (b < e) pool.emplace_back([&body, b, e] { body(b, e); });
-    }
-    body(0, std::min(units, per));
-    for (auto& th : pool) th.join();
+    const int parts = pool->size;
+    const uint64_t per = (units + parts - 1) / parts;
+    pool->run(parts, [&](int p) {
+        const uint64_t b = per * (uint64_t)p, e = std::min(units, b + per);
+        if (b < e) body(b, e);
+    });
 }
-
 }  // namespace
 
 CPUSimulator::CPUSimulator(int num_qubits, CpuGateSet gates)
@@ -121,13 +183,16 @@ CPUSimulator::CPUSimulator(int num_qubits, CpuGateSet gates)
                                     std::to_string(device_config::MIN_QUBITS) + " and " +
                                     std::to_string(device_config::MAX_QUBITS));
     const unsigned hc = std::thread::hardware_concurrency();
-    threads_ = (int)std::max(1u, std::min(64u, hc));
+    setThreads((int)std::max(1u, std::min(16u, hc)));
     state_.assign(size_t(1) << num_qubits, cplx(0.0, 0.0));
     reset();
     rng_.seed(std::random_device{}());  // the reference seeds sample() from random_device
 }
 
-void CPUSimulator::setThreads(int threads) { threads_ = std::max(1, threads); }
+void CPUSimulator::setThreads(int threads) {
+    threads_ = std::max(1, std::min(256, threads));
+    pool_ = threads_ > 1 ? std::make_shared<Pool>(threads_) : nullptr;
+}
 
 void CPUSimulator::reset() {
     std::fill(state_.begin(), state_.end(), cplx(0.0, 0.0));
@@ -192,14 +257,14 @@ void CPUSimulator::applyGate(const GateOp& gate) {
             }
         }
     };
-    parallel_blocks(units, threads_, body);
+    parallel_blocks(pool_.get(), units, body);
 }
 
 std::vector<double> CPUSimulator::getProbabilities() const {
     std::vector<double> p(state_.size());
     const cplx* st = state_.data();
     double* out = p.data();
-    parallel_blocks(p.size(), threads_, [&](uint64_t b, uint64_t e) {
+    parallel_blocks(pool_.get(), p.size(), [&](uint64_t b, uint64_t e) {
         for (uint64_t i = b; i < e; ++i) out[i] = std::norm(st[i]);
     });
     return p;

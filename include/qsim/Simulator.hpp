@@ -14,6 +14,7 @@
 
 #include <complex>
 #include <cstdint>
+#include <memory>
 #include <random>
 #include <vector>
 
@@ -74,8 +75,9 @@ public:
     int getNumQubits() const { return num_qubits_; }
     size_t getStateSize() const { return state_.size(); }
 
-    // Worker threads for the pair loops (default: hardware concurrency, capped at 64; states
-    // below 2^14 amplitudes always run on the calling thread).  1 = the reference's single core.
+    // Worker threads for the pair loops (a persistent pool; default min(hardware threads, 16);
+    // states below 2^17 amplitudes always run on the calling thread).  1 = the reference's single
+    // core.
     void setThreads(int threads);
     int getThreads() const { return threads_; }
     void setSeed(unsigned int seed) { rng_.seed(seed); }
@@ -86,6 +88,8 @@ private:
     int threads_;
     std::vector<std::complex<double>> state_;
     std::mt19937 rng_;
+    struct Pool;
+    std::shared_ptr<Pool> pool_;
 };
 
 }  // namespace qsim
