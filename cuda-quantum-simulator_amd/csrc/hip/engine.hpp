@@ -126,13 +126,28 @@ struct TileOp {            // an Op re-expressed in tile-index bits
 // Register r of a stage holds tile element jb | offs(r), offs(r) = r spread over fix[].  Both
 // address maps are XOR-linear in the element index, so their per-register parts are
 // precomputed here and the kernel combines them with the thread part by one OR / XOR.
+// LDS layout between two stages: element j lives at slot sigma(j) = j ^ sum_i parity(j & trow[i])
+// << i (trow[i] only holds tile bits above i: triangular, so sigma is a bijection).  The planner
+// picks trow per stage transition so that both the writes of the stage before (ds_write_b128:
+// 8 groups of 8 lanes, slot mod 8) and the reads of the stage after (ds_read_b128: 4 groups of
+// 16 lanes, slot mod 16) are bank-conflict-free (MI355X_MICROARCH.md §LDS); the fixed
+// j ^ ((j >> 4) & 15) is 2-way conflicted whenever a stage's lanes span bits 0-3 and 4-7 unevenly.
 struct Stage {
     uint64_t goff[16];     // HBM amplitude offset of offs(r) (its bits >= 6 spread over hpos)
-    uint32_t lds[16];      // LDS byte offset of offs(r) after the XOR swizzle (16 * sw(offs(r)))
+    uint32_t lds[16];      // LDS byte offset 16 * sigma_in(offs(r)): this stage's reads
+    uint32_t lds_w[16];    // LDS byte offset 16 * sigma_out(offs(r)): this stage's writes
+    uint32_t trow_in[4], trow_out[4];  // the two layouts' sigma rows (see above)
     int fix[4];            // ascending stage tile bits
     int op_begin, op_end;
     int _pad[2];
 };
+// sigma of a layout (host and device)
+__host__ __device__ __forceinline__ uint32_t lds_sigma(uint32_t j, const uint32_t* trow) {
+    uint32_t s = j;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) s ^= (uint32_t)(__builtin_popcount(j & trow[i]) & 1) << i;
+    return s;
+}
 struct Plan {
     std::vector<FusedPass> passes;
     std::vector<TileOp> ops;

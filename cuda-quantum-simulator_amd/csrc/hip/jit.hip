@@ -280,7 +280,15 @@ void gen_pass(std::ostringstream& out, const Plan& plan, const FusedPass& p, int
             return e;
         };
         if (s == sb || s == se - 1) o << "  const unsigned long long gb = " << gaddr() << ";\n";
-        if (s != sb || s != se - 1) o << "  const unsigned lb = 16u * (jb ^ ((jb >> 4) & 15u));\n";
+        auto sigma_expr = [](const uint32_t* trow) {
+            std::string e = "jb";
+            for (int i = 0; i < 4; ++i)
+                e += " ^ ((__builtin_popcount(jb & " + std::to_string(trow[i]) + "u) & 1u) << " +
+                     std::to_string(i) + ")";
+            return e;
+        };
+        if (s != sb) o << "  const unsigned lb = 16u * (" << sigma_expr(st.trow_in) << ");\n";
+        if (s != se - 1) o << "  const unsigned lbw = 16u * (" << sigma_expr(st.trow_out) << ");\n";
         if (s == sb) {
             for (int r = 0; r < R; ++r) o << "  " << g.v(r) << " = qld(st + (gb | " << hexu(st.goff[r]) << "));\n";
         } else {
@@ -297,7 +305,7 @@ void gen_pass(std::ostringstream& out, const Plan& plan, const FusedPass& p, int
             }
         } else {
             for (int r = 0; r < R; ++r)
-                o << "  *reinterpret_cast<double2*>(lds + (lb ^ " << st.lds[r] << "u)) = " << g.v(r) << ";\n";
+                o << "  *reinterpret_cast<double2*>(lds + (lbw ^ " << st.lds_w[r] << "u)) = " << g.v(r) << ";\n";
             o << "  __syncthreads();\n";
         }
         o << "  }\n";
