@@ -40,7 +40,82 @@ struct DStep {
     int k = 0;
     int gpos[8] = {0}, lpos[8] = {0};
     std::vector<Op> ops;
+    // Overlap of a remap with local work (split_for_overlap): an exchange with pivot >= 0 runs
+    // as two half-exchanges, one per value of local physical qubit `pivot`; an ops step with
+    // role 1 (just before it) / role 2 (just after it) runs per half, so half 0's transfer
+    // overlaps half 1's local work on the other stream.  Ops steps never touch the pivot.
+    int pivot = -1, role = 0;
+    // planning only: the circuit gates emitted into this step (rank-independent), their physical
+    // qubit masks, and for each op the index of the gate (in this list) it came from
+    std::vector<uint64_t> gmask;
+    std::vector<int> op_gate;
 };
+
+// Choose, for every exchange between two ops steps, a pivot qubit and split the neighbouring
+// steps so that the longest possible tail of the step before and head of the step after avoid
+// it (QSIM_DIST_OVERLAP=0 disables).  Decided from the rank-independent gate lists only, so every
+// rank picks the same pivot and runs the same exchange skeleton.  The pivot is a local physical
+// position >= 6 (never a tile's contiguous run) outside the exchanged positions.
+static void split_for_overlap(std::vector<DStep>& steps, int L) {
+    static const int enabled = [] {
+        const char* e = std::getenv("QSIM_DIST_OVERLAP");
+        return e ? std::atoi(e) : 1;
+    }();
+    if (!enabled || L < 8) return;
+    const int min_gates = 4;
+    std::vector<DStep> out;
+    for (size_t i = 0; i < steps.size(); ++i) {
+        out.push_back(std::move(steps[i]));
+        DStep& ex = out.back();
+        if (ex.kind != 1 || out.size() < 2 || i + 1 >= steps.size()) continue;
+        DStep& A = out[out.size() - 2];
+        DStep& B = steps[i + 1];
+        if (A.kind != 0 || A.role != 0 || B.kind != 0) continue;
+        uint64_t lmask = 0;
+        for (int j = 0; j < ex.k; ++j) lmask |= 1ull << ex.lpos[j];
+        int best_p = -1, best_a = 0, best_b = 0;
+        for (int p = 6; p < L; ++p) {
+            if ((lmask >> p) & 1ull) continue;
+            const uint64_t bit = 1ull << p;
+            int a = 0, b = 0;
+            while (a < (int)A.gmask.size() && !(A.gmask[A.gmask.size() - 1 - a] & bit)) ++a;
+            while (b < (int)B.gmask.size() && !(B.gmask[b] & bit)) ++b;
+            if (a + b > best_a + best_b) {
+                best_p = p;
+                best_a = a;
+                best_b = b;
+            }
+        }
+        if (best_p < 0 || best_a + best_b < min_gates) continue;
+        ex.pivot = best_p;
+        // split A: gates [0, na - best_a) stay, the rest become the role-1 tail
+        auto split = [](DStep& src, int gcut, DStep& head, DStep& tail) {
+            for (size_t o = 0; o < src.ops.size(); ++o) {
+                DStep& dst = src.op_gate[o] < gcut ? head : tail;
+                dst.ops.push_back(src.ops[o]);
+                dst.op_gate.push_back(src.op_gate[o] - (src.op_gate[o] < gcut ? 0 : gcut));
+            }
+            head.gmask.assign(src.gmask.begin(), src.gmask.begin() + gcut);
+            tail.gmask.assign(src.gmask.begin() + gcut, src.gmask.end());
+        };
+        DStep a_head, a_tail, b_head, b_rest;
+        split(A, (int)A.gmask.size() - best_a, a_head, a_tail);
+        split(B, best_b, b_head, b_rest);
+        a_tail.role = 1;
+        a_tail.pivot = best_p;
+        b_head.role = 2;
+        b_head.pivot = best_p;
+        DStep exc = std::move(ex);
+        out.pop_back();
+        out.pop_back();
+        out.push_back(std::move(a_head));  // may be empty: executes nothing
+        out.push_back(std::move(a_tail));
+        out.push_back(std::move(exc));
+        out.push_back(std::move(b_head));
+        steps[i + 1] = std::move(b_rest);  // becomes the next A candidate
+    }
+    steps.swap(out);
+}
 
 // Logical target that must be local for gate g (2x2 ops), or -1 (diagonal, SWAP).
 static int needs_local(const qsim_gate& g) {
@@ -186,7 +261,7 @@ static std::vector<DStep> plan_dist(const qsim_gate* gates, size_t count, int n,
     std::vector<DStep> steps;
     DStep cur;
     auto flush = [&]() {
-        if (!cur.ops.empty()) steps.push_back(cur);
+        if (!cur.ops.empty() || !cur.gmask.empty()) steps.push_back(cur);
         cur = DStep();
     };
     for (size_t i = 0; i < count; ++i) validate_gate(gates[i], n);
@@ -198,6 +273,9 @@ static std::vector<DStep> plan_dist(const qsim_gate* gates, size_t count, int n,
             std::swap(perm[gt.qubits[0]], perm[gt.qubits[1]]);
             return;
         }
+        uint64_t pm = 0;  // physical positions the gate touches (rank-independent)
+        for (int j = 0; j < gt.nqubits; ++j) pm |= 1ull << perm[gt.qubits[j]];
+        cur.gmask.push_back(pm);
         qsim_gate pg = gt;
         for (int j = 0; j < gt.nqubits; ++j) pg.qubits[j] = perm[gt.qubits[j]];
         Op op = lower_gate(pg, n);
@@ -224,6 +302,7 @@ static std::vector<DStep> plan_dist(const qsim_gate* gates, size_t count, int n,
         if (op.t0 >= L || (op.kind == K_SWAP && op.t1 >= L))
             fail(QSIM_ERR_RUNTIME, "distributed planner left a global target");
         cur.ops.push_back(op);
+        cur.op_gate.push_back((int)cur.gmask.size() - 1);
     };
     std::vector<char> done(count, 0);
     size_t left = count;
@@ -268,6 +347,7 @@ static std::vector<DStep> plan_dist(const qsim_gate* gates, size_t count, int n,
         steps.push_back(ex);
     }
     flush();
+    split_for_overlap(steps, L);
     return steps;
 }
 
@@ -279,23 +359,25 @@ struct XArgs {
     int chunk_log;
     int k;
     int my_c;
-    int sorted[8];      // ascending lpos
+    int nsorted;        // zero-insertion positions: lpos, plus the pivot of a half exchange
+    int sorted[9];      // ascending
     int lpos[8];        // chunk bit j <-> lpos[j]
+    uint64_t orval;     // half exchange: the pivot bit's value
 };
 
 __device__ __forceinline__ uint64_t xlocal(const XArgs& a, uint64_t e) {
     const uint64_t c = e >> a.chunk_log;
     uint64_t off = e & (a.chunk - 1);
 #pragma unroll
-    for (int j = 0; j < 8; ++j)
-        if (j < a.k) {
+    for (int j = 0; j < 9; ++j)
+        if (j < a.nsorted) {
             const uint64_t lo = off & ((1ull << a.sorted[j]) - 1ull);
             off = ((off ^ lo) << 1) | lo;
         }
 #pragma unroll
     for (int j = 0; j < 8; ++j)
         if (j < a.k) off |= ((c >> j) & 1ull) << a.lpos[j];
-    return off;
+    return off | a.orval;
 }
 
 // Pack (state -> send slabs) or unpack (receive slabs -> state) the offsets [lo, lo + 2^sub_log)
@@ -345,7 +427,10 @@ struct qsim_dist {
     double* d_result = nullptr;
     hipStream_t stream = nullptr;       // compute: passes, pack / unpack
     hipStream_t comm_stream = nullptr;  // remap transfers (RCCL or, virtual, device copies)
+    hipStream_t copy_stream = nullptr;  // pack / unpack of overlapped (half) remaps
     std::vector<hipEvent_t> events;     // remap pipeline: packed part p, transferred part p
+    hipEvent_t hev[8] = {};             // overlapped remap: tail done, packed, sent, unpacked x 2 halves
+    int overlapped = 0;                 // remaps of the last run that overlapped local work
     ncclComm_t comm = nullptr;
     bool aborted = false;  // the communicator was aborted after an RCCL / HIP error or a timeout
     std::vector<int> perm;
@@ -356,7 +441,7 @@ struct qsim_dist {
         std::vector<qsim_gate> gates;
         std::vector<int> perm_in, perm_out;
         std::vector<std::vector<DStep>> steps;              // per shard
-        std::vector<std::unique_ptr<PlanCache>> fplans;     // per (shard, local segment)
+        std::vector<std::vector<std::unique_ptr<PlanCache>>> fplans;  // per shard, per step
         uint64_t used = 0;
     };
     std::vector<std::unique_ptr<RunPlan>> run_plans;
@@ -386,6 +471,10 @@ struct qsim_dist {
         if (comm_stream) (void)hipStreamSynchronize(comm_stream);
         for (hipEvent_t e : events)
             if (e) (void)hipEventDestroy(e);
+        if (copy_stream) (void)hipStreamSynchronize(copy_stream);
+        for (hipEvent_t e : hev)
+            if (e) (void)hipEventDestroy(e);
+        if (copy_stream) (void)hipStreamDestroy(copy_stream);
         if (comm_stream) (void)hipStreamDestroy(comm_stream);
         if (stream) (void)hipStreamDestroy(stream);
     }
@@ -507,19 +596,26 @@ struct XPlan {
     XArgs a;
     int peer_of[256];
 };
-XPlan xplan(const qsim_dist* d, const Shard& sh, const DStep& ex) {
+// half < 0: the whole shard; half 0 / 1: the amplitudes whose pivot bit is 0 / 1.
+XPlan xplan(const qsim_dist* d, const Shard& sh, const DStep& ex, int half = -1) {
     XPlan x{};
     XArgs& a = x.a;
     a.st = sh.d;
     a.k = ex.k;
-    a.chunk_log = d->L - ex.k;
+    const bool h = half >= 0;
+    a.chunk_log = d->L - ex.k - (h ? 1 : 0);
     a.chunk = 1ull << a.chunk_log;
     for (int j = 0; j < ex.k; ++j) {
         a.lpos[j] = ex.lpos[j];
         a.sorted[j] = ex.lpos[j];
         a.my_c |= ((sh.rank >> (ex.gpos[j] - d->L)) & 1) << j;
     }
-    std::sort(a.sorted, a.sorted + ex.k);
+    a.nsorted = ex.k;
+    if (h) {
+        a.sorted[a.nsorted++] = ex.pivot;
+        a.orval = (uint64_t)half << ex.pivot;
+    }
+    std::sort(a.sorted, a.sorted + a.nsorted);
     for (int c = 0; c < (1 << ex.k); ++c) {
         int peer = sh.rank;
         for (int j = 0; j < ex.k; ++j) {
@@ -620,6 +716,66 @@ void exchange(qsim_dist* d, const DStep& ex) {
         }
     }
 }
+// One overlapped remap: the two halves of every shard (pivot bit 0, then 1) are exchanged one
+// after the other — pack and unpack on copy_stream, transfers on comm_stream — each half waiting
+// for its local work (event hev[h], recorded on the compute stream after the role-1 step's half)
+// and signalling hev[6 + h] when unpacked (the role-2 step's half waits for it).  Half h uses
+// half h of the send / receive buffers, so both halves can be in flight.
+void exchange_halves(qsim_dist* d, const DStep& ex) {
+    const uint64_t half_amps = 1ull << (d->L - 1);
+    const uint64_t chunk = half_amps >> ex.k;
+    const double bytes = 2.0 * 16.0 * (double)(half_amps - chunk) * (double)d->shards.size();
+    for (int h = 0; h < 2; ++h) {
+        TimedLaunch tl(&d->timer, "alltoall_remap", bytes, d->copy_stream);
+        std::vector<XPlan> xs;
+        for (Shard& sh : d->shards) xs.push_back(xplan(d, sh, ex, h));
+        QSIM_HIPCHK(hipStreamWaitEvent(d->copy_stream, d->hev[h], 0));
+        for (size_t i = 0; i < d->shards.size(); ++i) {
+            XArgs a = xs[i].a;
+            a.buf = d->shards[i].sendbuf + (uint64_t)h * half_amps;
+            copy_kernel(true, a, 0, xs[i].a.chunk_log, d->copy_stream);
+        }
+        QSIM_HIPCHK(hipEventRecord(d->hev[2 + h], d->copy_stream));
+        QSIM_HIPCHK(hipStreamWaitEvent(d->comm_stream, d->hev[2 + h], 0));
+        if (!d->virt) {
+            const Shard& sh = d->shards[0];
+            const XPlan& x = xs[0];
+            double2* sb = sh.sendbuf + (uint64_t)h * half_amps;
+            double2* rb = sh.recvbuf + (uint64_t)h * half_amps;
+            QSIM_NCCLCHK(ncclGroupStart());
+            for (int c = 0; c < (1 << ex.k); ++c) {
+                if (c == x.a.my_c) continue;
+                QSIM_NCCLCHK(ncclSend(sb + (uint64_t)c * chunk, (size_t)chunk * 2, ncclDouble, x.peer_of[c],
+                                      d->comm, d->comm_stream));
+                QSIM_NCCLCHK(ncclRecv(rb + (uint64_t)c * chunk, (size_t)chunk * 2, ncclDouble, x.peer_of[c],
+                                      d->comm, d->comm_stream));
+            }
+            QSIM_NCCLCHK(ncclGroupEnd());
+            comm_settle(d, "overlapped remap send/recv");
+        } else {
+            for (size_t i = 0; i < d->shards.size(); ++i) {
+                const XPlan& x = xs[i];
+                for (int c = 0; c < (1 << ex.k); ++c) {
+                    if (c == x.a.my_c) continue;
+                    Shard& dst = d->shards[x.peer_of[c]];
+                    QSIM_HIPCHK(hipMemcpyAsync(dst.recvbuf + (uint64_t)h * half_amps + (uint64_t)x.a.my_c * chunk,
+                                               d->shards[i].sendbuf + (uint64_t)h * half_amps + (uint64_t)c * chunk,
+                                               chunk * sizeof(double2), hipMemcpyDeviceToDevice,
+                                               d->comm_stream));
+                }
+            }
+        }
+        QSIM_HIPCHK(hipEventRecord(d->hev[4 + h], d->comm_stream));
+        QSIM_HIPCHK(hipStreamWaitEvent(d->copy_stream, d->hev[4 + h], 0));
+        for (size_t i = 0; i < d->shards.size(); ++i) {
+            XArgs a = xs[i].a;
+            a.buf = d->shards[i].recvbuf + (uint64_t)h * half_amps;
+            copy_kernel(false, a, 0, xs[i].a.chunk_log, d->copy_stream);
+        }
+        QSIM_HIPCHK(hipEventRecord(d->hev[6 + h], d->copy_stream));
+    }
+}
+
 double allreduce_sum(qsim_dist* d, double local) {
     if (d->virt) return local;
     QSIM_HIPCHK(hipMemcpyAsync(d->d_result, &local, sizeof(double), hipMemcpyHostToDevice, d->stream));
@@ -630,18 +786,40 @@ double allreduce_sum(qsim_dist* d, double local) {
     stream_wait(d, d->stream);
     return out;
 }
-void run_local(qsim_dist* d, Shard& sh, const std::vector<Op>& ops, int flags, PlanCache& pc) {
+// Local ops of one step.  avoid: a pivot the fused plan's tiles must not contain (role 1 / 2
+// steps); half >= 0 runs only the half of the shard whose pivot bit equals `half` — possible when
+// the plan is all staged tile passes, which run_local_halves checks first.
+void run_local(qsim_dist* d, Shard& sh, const std::vector<Op>& ops, int flags, PlanCache& pc,
+               int pivot = -1, int half = -1) {
+    if (ops.empty()) return;
     if (flags & QSIM_RUN_FUSED) {
-        PlanCache::Entry& pe = pc.get(ops, d->L, d->stream);
+        PlanCache::Entry& pe = pc.get(ops, d->L, d->stream, pivot >= 0 ? 1ull << pivot : 0ull);
         const Plan& plan = pe.plan;
         const JitModule* jm = jit_for(pe.jit, plan, d->L);
         d->ops.upload(plan.ops.data(), plan.ops.size() * sizeof(TileOp), d->stream);
         d->stages.upload(plan.stages.data(), plan.stages.size() * sizeof(Stage), d->stream);
+        FusedRange rg;
+        if (half >= 0) {
+            rg.fix_mask = 1ull << pivot;
+            rg.fix_val = (uint64_t)half << pivot;
+        }
         launch_fused(sh.d, d->L, 1, plan, (const TileOp*)d->ops.ptr, (const Stage*)d->stages.ptr,
-                     d->stream, &d->timer, jm);
+                     d->stream, &d->timer, jm, nullptr, rg);
     } else {
         for (const Op& op : ops) launch_op(sh.d, d->L, 1, op, d->stream, &d->timer);
     }
+}
+// Can this step run half by half (fused mode, every pass a staged tile pass avoiding the pivot)?
+bool halves_ok(qsim_dist* d, const std::vector<Op>& ops, int flags, PlanCache& pc, int pivot) {
+    if (ops.empty()) return true;
+    if (!(flags & QSIM_RUN_FUSED)) return false;
+    const Plan& plan = pc.get(ops, d->L, d->stream, 1ull << pivot).plan;
+    for (const FusedPass& p : plan.passes) {
+        if (p.single >= 0 || p.h < 4) return false;
+        for (int i = 0; i < 6 + p.h - p.r0; ++i)
+            if (p.hpos[i] == pivot) return false;
+    }
+    return true;
 }
 // The cached plan of this run (same gates, same start map), or a new one (LRU of 8).
 qsim_dist::RunPlan& run_plan(qsim_dist* d, const qsim_gate* gates, size_t count) {
@@ -659,8 +837,9 @@ qsim_dist::RunPlan& run_plan(qsim_dist* d, const qsim_gate* gates, size_t count)
         std::vector<int> perm = d->perm;
         rp->steps.push_back(plan_dist(gates, count, d->n, d->g, sh.rank, perm));
         rp->perm_out = perm;
+        rp->fplans.emplace_back();
         for (const DStep& s : rp->steps.back())
-            if (s.kind == 0) rp->fplans.push_back(std::make_unique<PlanCache>());
+            rp->fplans.back().push_back(s.kind == 0 ? std::make_unique<PlanCache>() : nullptr);
     }
     rp->used = ++d->run_clock;
     if (d->run_plans.size() >= 8) {
@@ -705,6 +884,8 @@ int qsim_dist_create(int n_qubits, int rank, int world, const void* unique_id, i
         QSIM_HIPCHK(hipSetDevice(device));
         QSIM_HIPCHK(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
         QSIM_HIPCHK(hipStreamCreateWithFlags(&d->comm_stream, hipStreamNonBlocking));
+        QSIM_HIPCHK(hipStreamCreateWithFlags(&d->copy_stream, hipStreamNonBlocking));
+        for (hipEvent_t& e : d->hev) QSIM_HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         d->timer.stream = d->stream;
         alloc_shards(d.get(), {rank});
         ncclUniqueId id;
@@ -751,6 +932,8 @@ int qsim_dist_create_virtual(int n_qubits, int world, int device, qsim_dist** ou
         QSIM_HIPCHK(hipSetDevice(device));
         QSIM_HIPCHK(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
         QSIM_HIPCHK(hipStreamCreateWithFlags(&d->comm_stream, hipStreamNonBlocking));
+        QSIM_HIPCHK(hipStreamCreateWithFlags(&d->copy_stream, hipStreamNonBlocking));
+        for (hipEvent_t& e : d->hev) QSIM_HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         d->timer.stream = d->stream;
         std::vector<int> ranks(world);
         for (int r = 0; r < world; ++r) ranks[r] = r;
@@ -779,23 +962,81 @@ int qsim_dist_run(qsim_dist* d, const qsim_gate* gates, size_t count, int flags)
         QSIM_HIPCHK(hipSetDevice(d->device));
         qsim_dist::RunPlan& rp = run_plan(d, gates, count);
         const auto& plans = rp.steps;
-        size_t fp = 0;
-        // Every rank's plan has the same exchange skeleton: walk the steps in lockstep.
-        std::vector<size_t> pos(d->shards.size(), 0);
-        for (;;) {
-            for (size_t i = 0; i < d->shards.size(); ++i)  // local ops up to the next exchange
-                while (pos[i] < plans[i].size() && plans[i][pos[i]].kind == 0) {
-                    run_local(d, d->shards[i], plans[i][pos[i]].ops, flags, *rp.fplans[fp++]);
-                    ++pos[i];
+        const size_t S = d->shards.size();
+        for (size_t i = 1; i < S; ++i)
+            if (plans[i].size() != plans[0].size()) fail(QSIM_ERR_RUNTIME, "exchange skeleton mismatch");
+        d->overlapped = 0;
+        bool pending = false;  // an overlapped remap's halves still to be waited for
+        auto wait_pending = [&]() {
+            if (!pending) return;
+            QSIM_HIPCHK(hipStreamWaitEvent(d->stream, d->hev[6], 0));
+            QSIM_HIPCHK(hipStreamWaitEvent(d->stream, d->hev[7], 0));
+            pending = false;
+        };
+        // Every rank's plan has the same step skeleton (split_for_overlap decides from
+        // rank-independent data): walk the steps in lockstep.
+        for (size_t k = 0; k < plans[0].size(); ++k) {
+            const DStep& s0 = plans[0][k];
+            for (size_t i = 1; i < S; ++i)
+                if (plans[i][k].kind != s0.kind || plans[i][k].role != s0.role)
+                    fail(QSIM_ERR_RUNTIME, "exchange skeleton mismatch");
+            if (s0.kind == 1) {
+                if (s0.pivot >= 0) {
+                    // the role-1 step before recorded hev[0] / hev[1]; if it had nothing to
+                    // split, both halves are ready now
+                    if (k == 0 || plans[0][k - 1].role != 1) {
+                        QSIM_HIPCHK(hipEventRecord(d->hev[0], d->stream));
+                        QSIM_HIPCHK(hipEventRecord(d->hev[1], d->stream));
+                    }
+                    exchange_halves(d, s0);
+                    pending = true;
+                    ++d->overlapped;
+                } else {
+                    wait_pending();
+                    exchange(d, s0);
                 }
-            const bool ex = pos[0] < plans[0].size();
-            for (size_t i = 1; i < d->shards.size(); ++i)
-                if ((pos[i] < plans[i].size()) != ex) fail(QSIM_ERR_RUNTIME, "exchange skeleton mismatch");
-            if (!ex) break;
-            exchange(d, plans[0][pos[0]]);
-            for (size_t i = 0; i < d->shards.size(); ++i) ++pos[i];
+                continue;
+            }
+            if (s0.role == 0) {
+                wait_pending();
+                for (size_t i = 0; i < S; ++i) run_local(d, d->shards[i], plans[i][k].ops, flags, *rp.fplans[i][k]);
+                continue;
+            }
+            bool split = true;  // the same decision on every shard of this process
+            for (size_t i = 0; i < S; ++i)
+                split = split && halves_ok(d, plans[i][k].ops, flags, *rp.fplans[i][k], s0.pivot);
+            if (s0.role == 1) {  // before the remap: half 0, signal, half 1, signal
+                for (int h = 0; h < 2; ++h) {
+                    if (split || h == 0)
+                        for (size_t i = 0; i < S; ++i)
+                            run_local(d, d->shards[i], plans[i][k].ops, flags, *rp.fplans[i][k], s0.pivot,
+                                      split ? h : -1);
+                    QSIM_HIPCHK(hipEventRecord(d->hev[h], d->stream));
+                }
+            } else {  // after the remap: each half once its half-exchange has landed
+                for (int h = 0; h < 2; ++h) {
+                    if (!split && h == 0) continue;
+                    if (split) {
+                        QSIM_HIPCHK(hipStreamWaitEvent(d->stream, d->hev[6 + h], 0));
+                    } else {
+                        wait_pending();
+                    }
+                    for (size_t i = 0; i < S; ++i)
+                        run_local(d, d->shards[i], plans[i][k].ops, flags, *rp.fplans[i][k], s0.pivot,
+                                  split ? h : -1);
+                }
+                pending = false;
+            }
         }
+        wait_pending();
         d->perm = rp.perm_out;
+    });
+}
+
+int qsim_dist_overlapped(qsim_dist* d, int* remaps) {
+    return dguard([&] {
+        need(d);
+        if (remaps) *remaps = d->overlapped;
     });
 }
 
@@ -804,6 +1045,7 @@ int qsim_dist_sync(qsim_dist* d) {
         need(d);
         QSIM_HIPCHK(hipSetDevice(d->device));
         stream_wait(d, d->comm_stream);
+        stream_wait(d, d->copy_stream);
         stream_wait(d, d->stream);
     });
 }
@@ -953,6 +1195,8 @@ int qsim_dist_plan(int n, int world, int rank, const qsim_gate* gates, size_t co
                     o.gpos[j] = s.gpos[j];
                     o.lpos[j] = s.lpos[j];
                 }
+                o.pivot = s.pivot;
+                o.role = s.role;
             }
             for (const Op& op : s.ops) {
                 if (oi < op_cap) {

@@ -160,7 +160,8 @@ struct Plan {
 constexpr int kTileHMax = 6;  // 64 << 6 = 4096 amplitudes = 64 KiB of LDS per workgroup
 constexpr int kTileR0 = 6;    // contiguous run bits of a staged tile (QSIM_TILE_R0 in 4..6)
 // hmax < 0: the process default (kTileHMax, or QSIM_TILE_HMAX for tuning runs).
-Plan plan_fused(const std::vector<Op>& ops, int n, int hmax = -1);
+// avoid: qubits no tile may contain (ops never act on them; only tile padding is affected).
+Plan plan_fused(const std::vector<Op>& ops, int n, int hmax = -1, uint64_t avoid = 0);
 // Circuit-specialised pass kernels (jit.hip): hipRTC code object of one plan on one device.
 struct JitJob;
 struct JitModule {
@@ -187,6 +188,7 @@ const JitModule* jit_for(JitState& js, const Plan& plan, int n);
 struct PlanCache {
     struct Entry {
         int n = -1;
+        uint64_t avoid = 0;
         std::vector<Op> key;
         Plan plan;
         JitState jit;
@@ -196,12 +198,18 @@ struct PlanCache {
     std::vector<std::unique_ptr<Entry>> entries;
     uint64_t clock = 0;
     // stream: where the owner runs this cache's plans (drained before a plan is evicted)
-    Entry& get(const std::vector<Op>& ops, int n_qubits, hipStream_t stream);
+    Entry& get(const std::vector<Op>& ops, int n_qubits, hipStream_t stream, uint64_t avoid = 0);
+};
+// Which part of a plan to launch: passes [first, last) over the sub-space whose qubits in
+// fix_mask read fix_val (fix_mask = 0: the whole state).  Sub-space launches need staged passes.
+struct FusedRange {
+    size_t first = 0, last = SIZE_MAX;
+    uint64_t fix_mask = 0, fix_val = 0;
 };
 // frames != null: batched noisy run under per-trajectory Pauli frames (FArgs::frames).
 void launch_fused(double2* st, int n, uint64_t batch, const Plan& plan, const TileOp* d_ops,
                   const Stage* d_stages, hipStream_t s, Timer* tm, const JitModule* jm = nullptr,
-                  const uint64_t* frames = nullptr);
+                  const uint64_t* frames = nullptr, const FusedRange& range = FusedRange());
 
 // Single-trajectory Monte-Carlo noise (noise.hip): one per-pair pass of channel `type`
 // (reference NoiseType numbering) on `qubit`, uniforms from the hash of (seed, counter, pair).

@@ -550,9 +550,10 @@ static bool same_op(const Op& a, const Op& b) {
     return true;
 }
 
-PlanCache::Entry& PlanCache::get(const std::vector<Op>& ops, int n_qubits, hipStream_t stream) {
+PlanCache::Entry& PlanCache::get(const std::vector<Op>& ops, int n_qubits, hipStream_t stream,
+                                 uint64_t avoid) {
     for (auto& e : entries) {
-        bool hit = e->n == n_qubits && e->key.size() == ops.size();
+        bool hit = e->n == n_qubits && e->avoid == avoid && e->key.size() == ops.size();
         for (size_t i = 0; hit && i < ops.size(); ++i) hit = same_op(e->key[i], ops[i]);
         if (hit) {
             e->used = ++clock;
@@ -567,9 +568,10 @@ PlanCache::Entry& PlanCache::get(const std::vector<Op>& ops, int n_qubits, hipSt
         entries.erase(lru);
     }
     auto e = std::make_unique<Entry>();
-    e->plan = plan_fused(ops, n_qubits);
+    e->plan = plan_fused(ops, n_qubits, -1, avoid);
     e->key = ops;
     e->n = n_qubits;
+    e->avoid = avoid;
     e->used = ++clock;
     entries.push_back(std::move(e));
     return *entries.back();
@@ -580,7 +582,7 @@ static int env_int(const char* k, int d) {
     return e ? std::atoi(e) : d;
 }
 
-Plan plan_fused(const std::vector<Op>& ops, int n, int hmax) {
+Plan plan_fused(const std::vector<Op>& ops, int n, int hmax, uint64_t avoid) {
     if (hmax < 0) {
         static const int def = std::min(kTileHMax, std::max(0, env_int("QSIM_TILE_HMAX", kTileHMax)));
         hmax = def;
@@ -631,6 +633,11 @@ Plan plan_fused(const std::vector<Op>& ops, int n, int hmax) {
         const int nfree = 6 + heff - r0;
         uint64_t hi = ch.hi;
         // Pad the tile to nfree chosen qubits (uniform tile size / occupancy).
+        for (int q = r0; q < n && __builtin_popcountll(hi) < nfree; ++q)
+            if (!((avoid >> q) & 1ull)) hi |= 1ull << q;
+        // too few qubits outside `avoid` (small states): fill up anyway — such a tile contains
+        // the avoided qubit, which the caller detects (the sharded engine then runs the step on
+        // the whole shard)
         for (int q = r0; q < n && __builtin_popcountll(hi) < nfree; ++q) hi |= 1ull << q;
         FusedPass p;
         p.h = heff;
@@ -695,6 +702,9 @@ struct FArgs {
     // frame X^F Z^G (phase dropped) in force before circuit step `step` (batched.hip).
     const uint64_t* frames;
     int nbatch;
+    // Sub-space launch (sharded engine's overlapped remaps): tiles skip the fix_mask positions,
+    // which read fix_val; zmask = fix_mask | the tile's own positions above the run.
+    uint64_t fix_mask, fix_val, zmask;
 };
 
 // Runtime-count forms for the staged kernel (count = tile bits above the run, <= 8).
@@ -1079,8 +1089,17 @@ __global__ __launch_bounds__(256, 2) void k_fused_staged(FArgs a) {  // 2 WGs/CU
     __shared__ double2 tile[T];
     const uint64_t tile_id = blockIdx.x;
     const int r0 = a.r0, nh = 6 + H - r0;  // run bits, tile bits above the run
-    const uint64_t base =
-        (tile_id >> a.log_tpt) * a.stride + deposit_n((tile_id & a.tpt_mask) << r0, a.hpos, nh);
+    uint64_t kt = (tile_id & a.tpt_mask) << r0;
+    if (a.fix_mask) {  // uniform: zero insertion at every skipped position, ascending
+        for (uint64_t m = a.zmask; m; m &= m - 1ull) {
+            const uint64_t lo = kt & ((1ull << __builtin_ctzll(m)) - 1ull);
+            kt = ((kt ^ lo) << 1) | lo;
+        }
+        kt |= a.fix_val;
+    } else {
+        kt = deposit_n(kt, a.hpos, nh);
+    }
+    const uint64_t base = (tile_id >> a.log_tpt) * a.stride + kt;
     const uint32_t run_mask = (1u << r0) - 1u;
     const int sb = a.stage_begin, se = a.stage_end;
     double2 v[R];
@@ -1135,10 +1154,15 @@ static bool fused_nt() {
 
 void launch_fused(double2* st, int n, uint64_t batch, const Plan& plan, const TileOp* d_ops,
                   const Stage* d_stages, hipStream_t s, Timer* tm, const JitModule* jm,
-                  const uint64_t* frames) {
-    const double pass_bytes = 32.0 * (double)(1ull << n) * (double)batch;
+                  const uint64_t* frames, const FusedRange& range) {
+    const int nfix = __builtin_popcountll(range.fix_mask);
+    const double pass_bytes = 32.0 * std::ldexp((double)(1ull << n), -nfix) * (double)batch;
     const bool nt = fused_nt();
-    for (const FusedPass& p : plan.passes) {
+    const size_t last = std::min(range.last, plan.passes.size());
+    for (size_t pidx = range.first; pidx < last; ++pidx) {
+        const FusedPass& p = plan.passes[pidx];
+        if (range.fix_mask && (p.single >= 0 || p.h < 4 || frames))
+            fail(QSIM_ERR_RUNTIME, "sub-space launch needs staged tile passes");
         if (frames && (p.single >= 0 || p.h < 4))
             fail(QSIM_ERR_RUNTIME, "Pauli-frame passes need staged tiles (n >= 10)");
         if (p.single >= 0) {
@@ -1158,7 +1182,13 @@ void launch_fused(double2* st, int n, uint64_t batch, const Plan& plan, const Ti
         a.scale = std::ldexp(1.0, -(p.hu_count / 2)) * ((p.hu_count & 1) ? kInvSqrt2 : 1.0);
         for (int i = 0; i < 8; ++i) a.hpos[i] = p.hpos[i];
         a.r0 = p.r0;
-        const int lt = n - 6 - p.h;
+        uint64_t hmask = 0;
+        for (int i = 0; i < 6 + p.h - p.r0; ++i) hmask |= 1ull << p.hpos[i];
+        if (hmask & range.fix_mask) fail(QSIM_ERR_RUNTIME, "sub-space launch: pass uses a fixed qubit");
+        a.fix_mask = range.fix_mask;
+        a.fix_val = range.fix_val;
+        a.zmask = hmask | range.fix_mask;
+        const int lt = n - 6 - p.h - nfix;
         a.log_tpt = lt;
         a.tpt_mask = (1ull << lt) - 1ull;
         const uint64_t blocks = batch << lt;
@@ -1179,11 +1209,11 @@ void launch_fused(double2* st, int n, uint64_t batch, const Plan& plan, const Ti
             QSIM_HIPCHK(hipGetLastError());
             continue;
         }
-        const size_t pi = (size_t)(&p - plan.passes.data());
+        const size_t pi = pidx;
         if (jm && pi < jm->fn.size() && jm->fn[pi]) {  // circuit-specialised kernel (jit.hip)
-            unsigned long long stride = a.stride, tpt = a.tpt_mask;
+            unsigned long long stride = a.stride, tpt = a.tpt_mask, zm = a.zmask, fv = a.fix_val;
             int lt_arg = lt;
-            void* args[] = {&a.st, &stride, &tpt, &lt_arg};
+            void* args[] = {&a.st, &stride, &tpt, &lt_arg, &zm, &fv};
             QSIM_HIPCHK(hipModuleLaunchKernel(jm->fn[pi], (unsigned)blocks, 1, 1, 256, 1, 1, 0, s,
                                               args, nullptr));
             continue;

@@ -254,17 +254,21 @@ void gen_pass(std::ostringstream& out, const Plan& plan, const FusedPass& p, int
     g.RB = RB;
     for (int r = 0; r < R; ++r) g.nm[r] = r;
     std::ostringstream& o = g.o;
+    // zmask: positions the tile-id bits skip — the tile's own qubits above the run, plus (for a
+    // sub-space launch of the sharded engine) fixed qubits whose values fix_val supplies.  Zero
+    // insertion in ascending position order, uniform per workgroup (scalar ALU).
     o << "extern \"C\" __global__ void __launch_bounds__(256, 2)\nqk" << idx
-      << "(double2* __restrict__ st, unsigned long long stride, unsigned long long tpt_mask, int log_tpt) {\n"
+      << "(double2* __restrict__ st, unsigned long long stride, unsigned long long tpt_mask, int log_tpt,"
+         " unsigned long long zmask, unsigned long long fix_val) {\n"
       << "  __shared__ double2 tile[" << T << "];\n"
       << "  char* const lds = reinterpret_cast<char*>(tile);\n"
       << "  const unsigned tid = threadIdx.x;\n"
       << tile_id_expr()
-      << "  unsigned long long k = (tile_id & tpt_mask) << " << r0 << ";\n";
-    for (int i = 0; i < nh; ++i)
-        o << "  { const unsigned long long lo = k & " << hexu((1ull << p.hpos[i]) - 1ull)
-          << "; k = ((k ^ lo) << 1) | lo; }\n";
-    o << "  const unsigned long long base = (tile_id >> log_tpt) * stride + k;\n";
+      << "  unsigned long long k = (tile_id & tpt_mask) << " << r0 << ";\n"
+      << "  for (unsigned long long m = zmask; m; m &= m - 1ull) {\n"
+      << "    const unsigned long long lo = k & ((1ull << __builtin_ctzll(m)) - 1ull);\n"
+      << "    k = ((k ^ lo) << 1) | lo;\n  }\n";
+    o << "  const unsigned long long base = (tile_id >> log_tpt) * stride + (k | fix_val);\n";
     o << "  double2";
     for (int r = 0; r < R; ++r) o << (r ? ", v" : " v") << r;
     o << ";\n";

@@ -147,7 +147,7 @@ class qsim_op(Structure):
 
 class qsim_dist_step(Structure):
     _fields_ = [("kind", c_int32), ("k", c_int32), ("op_begin", c_int32), ("op_end", c_int32),
-                ("gpos", c_int32 * 8), ("lpos", c_int32 * 8)]
+                ("gpos", c_int32 * 8), ("lpos", c_int32 * 8), ("pivot", c_int32), ("role", c_int32)]
 
 
 _sig(hip, "qsim_dist_unique_id", [_P])
@@ -156,6 +156,7 @@ _sig(hip, "qsim_dist_create_virtual", [c_int, c_int, c_int, POINTER(_P)])
 _sig(hip, "qsim_dist_destroy", [_P])
 _sig(hip, "qsim_dist_run", [_P, POINTER(qsim_gate), c_size_t, c_int])
 _sig(hip, "qsim_dist_sync", [_P])
+_sig(hip, "qsim_dist_overlapped", [_P, POINTER(c_int)])
 _sig(hip, "qsim_dist_reset", [_P])
 _sig(hip, "qsim_dist_perm", [_P, POINTER(c_int32)])
 _sig(hip, "qsim_dist_local_state", [_P, _P])

@@ -68,6 +68,12 @@ class DistributedSimulator:
                                           _lib.QSIM_RUN_FUSED if fused else _lib.QSIM_RUN_PER_GATE))
 
     def synchronize(self) -> None: _lib.check(_lib.hip.qsim_dist_sync(self._h))
+
+    def overlappedRemaps(self) -> int:
+        """Remaps of the last run that were split in halves overlapping local work."""
+        v = _c.c_int(0)
+        _lib.check(_lib.hip.qsim_dist_overlapped(self._h, _c.byref(v)))
+        return v.value
     def reset(self) -> None: _lib.check(_lib.hip.qsim_dist_reset(self._h))
 
     def perm(self) -> List[int]:
@@ -137,7 +143,8 @@ def plan(circuit: Circuit, world: int, rank: int, perm: Optional[List[int]] = No
     for s in steps[:ns.value]:
         if s.kind == 1:
             out_steps.append({"kind": "exchange", "k": s.k, "gpos": list(s.gpos[:s.k]),
-                              "lpos": list(s.lpos[:s.k])})
+                              "lpos": list(s.lpos[:s.k]), "pivot": s.pivot})
         else:
-            out_steps.append({"kind": "ops", "ops": out_ops[s.op_begin:s.op_end]})
+            out_steps.append({"kind": "ops", "ops": out_ops[s.op_begin:s.op_end],
+                              "role": s.role, "pivot": s.pivot})
     return out_steps, list(p)

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define QSIM_ABI_VERSION 1
+#define QSIM_ABI_VERSION 2
 
 /* ---- status codes (mapped to the reference's exception types by the C++ layer) ---- */
 enum {
@@ -271,11 +271,15 @@ typedef struct qsim_op {
     double m[8];
 } qsim_op;
 /* One plan step: kind 0 = ops[op_begin, op_end) on the local shard; kind 1 = exchange that
- * swaps global physical positions gpos[i] with local positions lpos[i], i < k. */
+ * swaps global physical positions gpos[i] with local positions lpos[i], i < k.  Overlapped
+ * remaps: an exchange with pivot >= 0 runs as two half-exchanges (pivot bit 0, then 1); the ops
+ * step just before it has role 1 and the one just after role 2 (run per half so each half's
+ * transfer overlaps the other half's local work; they never touch the pivot); role 0 = plain. */
 typedef struct qsim_dist_step {
     int32_t kind, k;
     int32_t op_begin, op_end;
     int32_t gpos[8], lpos[8];
+    int32_t pivot, role;
 } qsim_dist_step;
 
 int qsim_dist_unique_id(void* id_out);  /* ncclGetUniqueId, on rank 0 */
@@ -287,6 +291,7 @@ int qsim_dist_create_virtual(int n_qubits, int world, int device, qsim_dist** ou
 int qsim_dist_destroy(qsim_dist* d);
 int qsim_dist_run(qsim_dist* d, const qsim_gate* gates, size_t count, int flags);
 int qsim_dist_sync(qsim_dist* d);
+int qsim_dist_overlapped(qsim_dist* d, int* remaps); /* remaps of the last run that overlapped local work */
 int qsim_dist_reset(qsim_dist* d);                         /* |0..0>, identity qubit map */
 int qsim_dist_perm(qsim_dist* d, int32_t* perm);            /* logical -> physical, n entries */
 /* This rank's 2*2^(n-g) doubles (virtual mode: all shards in rank order, 2*2^n doubles). */

@@ -42,7 +42,7 @@ def test_every_declared_symbol_is_exported(qsim):
 
 def test_abi_version(qsim):
     from qsim_amd import _lib
-    assert _lib.hip.qsim_abi_version() == 1
+    assert _lib.hip.qsim_abi_version() == 2
 
 
 def test_state_create_validation_without_gpu(qsim):
