@@ -22,11 +22,13 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import resource
 import sys
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "cuda-quantum-simulator_amd"))
+resource.setrlimit(resource.RLIMIT_CORE, (0, 0))  # an abort fails fast, no core dump
 
 METRIC = "gates/s + achieved HBM GB/s (% peak), 100-gate H+CNOT circuit @ n qubits"
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)

@@ -552,6 +552,10 @@ int qsim_set_jit(int mode, int min_qubits) {
     });
 }
 
+int qsim_jit_shutdown(void) {
+    return guarded([&] { jit_shutdown(); });
+}
+
 int qsim_jit_source(int n_qubits, const qsim_gate* gates, size_t count, char* buf, size_t cap,
                     size_t* len) {
     return guarded([&] {

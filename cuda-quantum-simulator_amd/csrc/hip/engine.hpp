@@ -177,6 +177,7 @@ struct JitState {
 int jit_mode();        // 0 off, 1 background compile (default), 2 compile on first use
 int jit_min_qubits();  // smaller states never JIT (QSIM_JIT_MIN_QUBITS, default 20)
 void jit_configure(int mode, int min_qubits);  // < 0 leaves a setting unchanged
+void jit_shutdown();  // stop the background compiler (queued jobs dropped, running one joined)
 std::string jit_source(const Plan& plan);      // empty when the plan has no staged pass
 bool jit_compile(const std::string& src, std::vector<char>& code, std::string& log);
 // The loaded module for `plan`, or null while it compiles / when JIT does not apply.

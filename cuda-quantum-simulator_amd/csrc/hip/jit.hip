@@ -373,6 +373,14 @@ struct JitJob {
 };
 
 bool jit_compile(const std::string& src, std::vector<char>& code, std::string& log) {
+    if (const char* dir = std::getenv("QSIM_JIT_DUMP")) {  // keep every generated source (debugging)
+        static std::atomic<int> seq{0};
+        const std::string path = std::string(dir) + "/qsim_jit_" + std::to_string(seq++) + ".hip";
+        if (FILE* f = std::fopen(path.c_str(), "w")) {
+            std::fwrite(src.data(), 1, src.size(), f);
+            std::fclose(f);
+        }
+    }
     hiprtcProgram prog;
     if (hiprtcCreateProgram(&prog, src.c_str(), "qsim_pass.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS) {
         log = "hiprtcCreateProgram failed";
@@ -407,20 +415,34 @@ public:
     void submit(std::shared_ptr<JitJob> j) {
         {
             std::lock_guard<std::mutex> l(mu_);
+            if (stop_) {  // shut down (process exit): the plan stays on the interpreter
+                j->log = "JIT worker stopped";
+                j->state.store(2);
+                return;
+            }
             q_.push_back(std::move(j));
             if (!th_.joinable()) th_ = std::thread([this] { loop(); });
         }
         cv_.notify_one();
     }
-    ~Worker() {
+    // Drop queued jobs and wait for the compile in progress.  Must run before the compiler's own
+    // static state is torn down at exit: a compile still running while LLVM's statics are
+    // destroyed dies with "LLVM ERROR" (seen in a pytest process that exited mid-compile).
+    void shutdown() {
         {
             std::lock_guard<std::mutex> l(mu_);
             stop_ = true;
+            for (auto& j : q_) {
+                j->log = "JIT worker stopped";
+                j->state.store(2);
+            }
             q_.clear();
         }
         cv_.notify_all();
-        if (th_.joinable()) th_.join();
+        std::lock_guard<std::mutex> l(join_mu_);
+        if (th_.joinable() && th_.get_id() != std::this_thread::get_id()) th_.join();
     }
+    ~Worker() { shutdown(); }
 
 private:
     void loop() {
@@ -435,15 +457,24 @@ private:
             }
             const bool ok = jit_compile(j->src, j->code, j->log);
             j->state.store(ok ? 1 : 2);
+            // The first compile constructed the compiler's static objects; an exit handler
+            // registered after them runs before their destructors (reverse registration order).
+            if (!atexit_registered_) {
+                atexit_registered_ = true;
+                std::atexit([] { Worker::get().shutdown(); });
+            }
         }
     }
-    std::mutex mu_;
+    std::mutex mu_, join_mu_;
+    bool atexit_registered_ = false;
     std::condition_variable cv_;
     std::deque<std::shared_ptr<JitJob>> q_;
     std::thread th_;
     bool stop_ = false;
 };
 }  // namespace
+
+void jit_shutdown() { Worker::get().shutdown(); }
 
 JitModule::~JitModule() {
     // the owner has drained the stream that ran this module's kernels (engine destructors

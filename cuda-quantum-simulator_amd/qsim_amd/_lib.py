@@ -5,6 +5,7 @@ package.  If the shared object is missing or cannot be loaded, import fails loud
 """
 from __future__ import annotations
 
+import atexit
 import ctypes
 import os
 from ctypes import (POINTER, Structure, c_char_p, c_double, c_int, c_int32, c_int64,
@@ -92,6 +93,10 @@ _sig(hip, "qsim_apply_gate_raw", [_P, c_int, POINTER(qsim_gate), _P])
 _sig(hip, "qsim_plan_fused", [c_int, POINTER(qsim_gate), c_size_t, c_int, _P, _P,
                               POINTER(c_int32)])
 _sig(hip, "qsim_set_jit", [c_int, c_int])
+_sig(hip, "qsim_jit_shutdown", [])
+# Stop the background pass compiler before interpreter / library teardown (a hipRTC compile that
+# is still running while the compiler's statics are destroyed aborts the process).
+atexit.register(hip.qsim_jit_shutdown)
 _sig(hip, "qsim_jit_source", [c_int, POINTER(qsim_gate), c_size_t, c_char_p, c_size_t,
                               POINTER(c_size_t)])
 _sig(hip, "qsim_jit_build", [c_int, POINTER(qsim_gate), c_size_t, POINTER(c_size_t)])

@@ -139,6 +139,11 @@ int qsim_plan_fused(int n_qubits, const qsim_gate* gates, size_t count, int hmax
  * the first run before launching; states below min_qubits always use the pass interpreter.
  * A negative argument leaves that setting unchanged (env defaults: QSIM_JIT, QSIM_JIT_MIN_QUBITS). */
 int qsim_set_jit(int mode, int min_qubits);
+/* Stop the background compiler: queued compiles are dropped (their plans stay on the
+ * interpreter) and the one in progress is waited for.  Called at exit (the Python package
+ * registers it with atexit; the library registers it after its first compile) so no compile runs
+ * while the compiler's static state is destroyed; later background requests are refused. */
+int qsim_jit_shutdown(void);
 /* Host-only: the generated source of a circuit's plan (len = its size; buf gets up to cap-1
  * bytes + NUL), and a hipRTC compile of it for gfx950 (code_bytes = code-object size). */
 int qsim_jit_source(int n_qubits, const qsim_gate* gates, size_t count, char* buf, size_t cap,

@@ -8,6 +8,7 @@ GPU tests that launch child processes (the C++ API harness, multi-rank runs) are
 a process that has initialised the GPU must not fork+exec afterwards (pool rule).
 """
 import os
+import resource
 import sys
 
 import pytest
@@ -15,6 +16,8 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "cuda-quantum-simulator_amd")
 ORACLE = os.path.join(ROOT, "oracle")
+# No core files: a process that aborts should fail fast, not spend minutes dumping GPU mappings.
+resource.setrlimit(resource.RLIMIT_CORE, (0, 0))
 for p in (ROOT, PKG, ORACLE):
     if p not in sys.path:
         sys.path.insert(0, p)
