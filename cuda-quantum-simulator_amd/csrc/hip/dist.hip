@@ -40,10 +40,12 @@ struct DStep {
     int k = 0;
     int gpos[8] = {0}, lpos[8] = {0};
     std::vector<Op> ops;
-    // Overlap of a remap with local work (split_for_overlap): an exchange with pivot >= 0 runs
-    // as two half-exchanges, one per value of local physical qubit `pivot`; an ops step with
-    // role 1 (just before it) / role 2 (just after it) runs per half, so half 0's transfer
-    // overlaps half 1's local work on the other stream.  Ops steps never touch the pivot.
+    // Overlap of a remap with local work (mark_overlap): an exchange with pivot >= 0 runs as two
+    // half-exchanges, one per value of local physical qubit `pivot`.  An ops step with role bit 1
+    // runs the trailing passes of its fused plan that avoid the pivot of the exchange after it
+    // per half (so half 0's transfer overlaps half 1's passes); role bit 2: the leading passes
+    // that avoid the pivot of the exchange before it run per half, each as soon as its half has
+    // landed.  The step's plan is the same one-piece fused plan either way (no extra passes).
     int pivot = -1, role = 0;
     // planning only: the circuit gates emitted into this step (rank-independent), their physical
     // qubit masks, and for each op the index of the gate (in this list) it came from
@@ -51,70 +53,44 @@ struct DStep {
     std::vector<int> op_gate;
 };
 
-// Choose, for every exchange between two ops steps, a pivot qubit and split the neighbouring
-// steps so that the longest possible tail of the step before and head of the step after avoid
-// it (QSIM_DIST_OVERLAP=0 disables).  Decided from the rank-independent gate lists only, so every
+// Choose, for every exchange between two ops steps, a pivot qubit: the local position most of the
+// trailing gates of the step before and the leading gates of the step after leave alone
+// (QSIM_DIST_OVERLAP=0 disables).  Decided from the rank-independent gate lists only, so every
 // rank picks the same pivot and runs the same exchange skeleton.  The pivot is a local physical
-// position >= 6 (never a tile's contiguous run) outside the exchanged positions.
-static void split_for_overlap(std::vector<DStep>& steps, int L) {
+// position >= 6 (never a tile's contiguous run) outside the exchanged positions.  The ops steps
+// are not split: each rank plans a step as one fused plan (tiles padded away from the pivots) and
+// runs per half only the passes at its ends that avoid them (run_step).
+static void mark_overlap(std::vector<DStep>& steps, int L) {
     static const int enabled = [] {
         const char* e = std::getenv("QSIM_DIST_OVERLAP");
         return e ? std::atoi(e) : 1;
     }();
     if (!enabled || L < 8) return;
     const int min_gates = 4;
-    std::vector<DStep> out;
-    for (size_t i = 0; i < steps.size(); ++i) {
-        out.push_back(std::move(steps[i]));
-        DStep& ex = out.back();
-        if (ex.kind != 1 || out.size() < 2 || i + 1 >= steps.size()) continue;
-        DStep& A = out[out.size() - 2];
+    for (size_t i = 1; i + 1 < steps.size(); ++i) {
+        DStep& ex = steps[i];
+        DStep& A = steps[i - 1];
         DStep& B = steps[i + 1];
-        if (A.kind != 0 || A.role != 0 || B.kind != 0) continue;
+        if (ex.kind != 1 || A.kind != 0 || B.kind != 0) continue;
         uint64_t lmask = 0;
         for (int j = 0; j < ex.k; ++j) lmask |= 1ull << ex.lpos[j];
-        int best_p = -1, best_a = 0, best_b = 0;
+        int best_p = -1, best = 0;
         for (int p = 6; p < L; ++p) {
             if ((lmask >> p) & 1ull) continue;
             const uint64_t bit = 1ull << p;
             int a = 0, b = 0;
             while (a < (int)A.gmask.size() && !(A.gmask[A.gmask.size() - 1 - a] & bit)) ++a;
             while (b < (int)B.gmask.size() && !(B.gmask[b] & bit)) ++b;
-            if (a + b > best_a + best_b) {
+            if (a + b > best) {
                 best_p = p;
-                best_a = a;
-                best_b = b;
+                best = a + b;
             }
         }
-        if (best_p < 0 || best_a + best_b < min_gates) continue;
+        if (best_p < 0 || best < min_gates) continue;
         ex.pivot = best_p;
-        // split A: gates [0, na - best_a) stay, the rest become the role-1 tail
-        auto split = [](DStep& src, int gcut, DStep& head, DStep& tail) {
-            for (size_t o = 0; o < src.ops.size(); ++o) {
-                DStep& dst = src.op_gate[o] < gcut ? head : tail;
-                dst.ops.push_back(src.ops[o]);
-                dst.op_gate.push_back(src.op_gate[o] - (src.op_gate[o] < gcut ? 0 : gcut));
-            }
-            head.gmask.assign(src.gmask.begin(), src.gmask.begin() + gcut);
-            tail.gmask.assign(src.gmask.begin() + gcut, src.gmask.end());
-        };
-        DStep a_head, a_tail, b_head, b_rest;
-        split(A, (int)A.gmask.size() - best_a, a_head, a_tail);
-        split(B, best_b, b_head, b_rest);
-        a_tail.role = 1;
-        a_tail.pivot = best_p;
-        b_head.role = 2;
-        b_head.pivot = best_p;
-        DStep exc = std::move(ex);
-        out.pop_back();
-        out.pop_back();
-        out.push_back(std::move(a_head));  // may be empty: executes nothing
-        out.push_back(std::move(a_tail));
-        out.push_back(std::move(exc));
-        out.push_back(std::move(b_head));
-        steps[i + 1] = std::move(b_rest);  // becomes the next A candidate
+        A.role |= 1;
+        B.role |= 2;
     }
-    steps.swap(out);
 }
 
 // Logical target that must be local for gate g (2x2 ops), or -1 (diagonal, SWAP).
@@ -347,7 +323,15 @@ static std::vector<DStep> plan_dist(const qsim_gate* gates, size_t count, int n,
         steps.push_back(ex);
     }
     flush();
-    split_for_overlap(steps, L);
+    // an exchange needs an ops step on both sides to overlap with (possibly empty)
+    std::vector<DStep> framed;
+    for (size_t i = 0; i < steps.size(); ++i) {
+        if (steps[i].kind == 1 && (framed.empty() || framed.back().kind == 1)) framed.push_back(DStep());
+        framed.push_back(std::move(steps[i]));
+    }
+    if (!framed.empty() && framed.back().kind == 1) framed.push_back(DStep());
+    steps.swap(framed);
+    mark_overlap(steps, L);
     return steps;
 }
 
@@ -786,40 +770,60 @@ double allreduce_sum(qsim_dist* d, double local) {
     stream_wait(d, d->stream);
     return out;
 }
-// Local ops of one step.  avoid: a pivot the fused plan's tiles must not contain (role 1 / 2
-// steps); half >= 0 runs only the half of the shard whose pivot bit equals `half` — possible when
-// the plan is all staged tile passes, which run_local_halves checks first.
-void run_local(qsim_dist* d, Shard& sh, const std::vector<Op>& ops, int flags, PlanCache& pc,
-               int pivot = -1, int half = -1) {
-    if (ops.empty()) return;
-    if (flags & QSIM_RUN_FUSED) {
-        PlanCache::Entry& pe = pc.get(ops, d->L, d->stream, pivot >= 0 ? 1ull << pivot : 0ull);
-        const Plan& plan = pe.plan;
-        const JitModule* jm = jit_for(pe.jit, plan, d->L);
-        d->ops.upload(plan.ops.data(), plan.ops.size() * sizeof(TileOp), d->stream);
-        d->stages.upload(plan.stages.data(), plan.stages.size() * sizeof(Stage), d->stream);
-        FusedRange rg;
-        if (half >= 0) {
-            rg.fix_mask = 1ull << pivot;
-            rg.fix_val = (uint64_t)half << pivot;
-        }
-        launch_fused(sh.d, d->L, 1, plan, (const TileOp*)d->ops.ptr, (const Stage*)d->stages.ptr,
-                     d->stream, &d->timer, jm, nullptr, rg);
-    } else {
-        for (const Op& op : ops) launch_op(sh.d, d->L, 1, op, d->stream, &d->timer);
-    }
-}
-// Can this step run half by half (fused mode, every pass a staged tile pass avoiding the pivot)?
-bool halves_ok(qsim_dist* d, const std::vector<Op>& ops, int flags, PlanCache& pc, int pivot) {
-    if (ops.empty()) return true;
-    if (!(flags & QSIM_RUN_FUSED)) return false;
-    const Plan& plan = pc.get(ops, d->L, d->stream, 1ull << pivot).plan;
-    for (const FusedPass& p : plan.passes) {
-        if (p.single >= 0 || p.h < 4) return false;
-        for (int i = 0; i < 6 + p.h - p.r0; ++i)
-            if (p.hpos[i] == pivot) return false;
-    }
+// One ops step on one shard, split by passes around the neighbouring half-exchanges:
+//   head   passes [0, j1) that avoid pivot pb (the exchange before): per half, each after its half
+//          of the exchange has landed;
+//   middle passes [j1, j2): whole shard, after both halves landed;
+//   tail   passes [j2, P) that avoid pivot pa (the exchange after): per half, each followed by the
+//          event its half-exchange waits for.
+// The plan is the step's ordinary fused plan with tiles padded away from both pivots, so the
+// split costs no extra HBM pass.  Per-gate mode (or a plan without such passes) runs whole.
+struct StepRun {
+    const Plan* plan = nullptr;
+    const JitModule* jm = nullptr;
+    size_t j1 = 0, j2 = 0, np = 0;
+};
+static bool pass_avoids(const FusedPass& p, int pivot) {
+    if (p.single >= 0 || p.h < 4) return false;
+    for (int i = 0; i < 6 + p.h - p.r0; ++i)
+        if (p.hpos[i] == pivot) return false;
     return true;
+}
+StepRun prepare_step(qsim_dist* d, const std::vector<Op>& ops, int flags, PlanCache& pc, int pb, int pa) {
+    StepRun r;
+    if (ops.empty() || !(flags & QSIM_RUN_FUSED)) return r;
+    const uint64_t avoid = (pb >= 0 ? 1ull << pb : 0ull) | (pa >= 0 ? 1ull << pa : 0ull);
+    PlanCache::Entry& pe = pc.get(ops, d->L, d->stream, avoid);
+    r.plan = &pe.plan;
+    r.jm = jit_for(pe.jit, pe.plan, d->L);
+    r.np = pe.plan.passes.size();
+    if (pb >= 0)
+        while (r.j1 < r.np && pass_avoids(pe.plan.passes[r.j1], pb)) ++r.j1;
+    r.j2 = r.np;
+    if (pa >= 0)
+        while (r.j2 > r.j1 && pass_avoids(pe.plan.passes[r.j2 - 1], pa)) --r.j2;
+    return r;
+}
+// Launch passes [first, last) of a prepared step (half >= 0: the half whose `pivot` bit is half);
+// per-gate mode: the whole op list when called for the middle part.
+void run_part(qsim_dist* d, Shard& sh, const std::vector<Op>& ops, const StepRun& r, size_t first,
+              size_t last, int pivot = -1, int half = -1) {
+    if (ops.empty() || first >= last) return;
+    if (!r.plan) {
+        for (const Op& op : ops) launch_op(sh.d, d->L, 1, op, d->stream, &d->timer);
+        return;
+    }
+    d->ops.upload(r.plan->ops.data(), r.plan->ops.size() * sizeof(TileOp), d->stream);
+    d->stages.upload(r.plan->stages.data(), r.plan->stages.size() * sizeof(Stage), d->stream);
+    FusedRange rg;
+    rg.first = first;
+    rg.last = last;
+    if (half >= 0) {
+        rg.fix_mask = 1ull << pivot;
+        rg.fix_val = (uint64_t)half << pivot;
+    }
+    launch_fused(sh.d, d->L, 1, *r.plan, (const TileOp*)d->ops.ptr, (const Stage*)d->stages.ptr, d->stream,
+                 &d->timer, r.jm, nullptr, rg);
 }
 // The cached plan of this run (same gates, same start map), or a new one (LRU of 8).
 qsim_dist::RunPlan& run_plan(qsim_dist* d, const qsim_gate* gates, size_t count) {
@@ -973,7 +977,7 @@ int qsim_dist_run(qsim_dist* d, const qsim_gate* gates, size_t count, int flags)
             QSIM_HIPCHK(hipStreamWaitEvent(d->stream, d->hev[7], 0));
             pending = false;
         };
-        // Every rank's plan has the same step skeleton (split_for_overlap decides from
+        // Every rank's plan has the same step skeleton (mark_overlap decides from
         // rank-independent data): walk the steps in lockstep.
         for (size_t k = 0; k < plans[0].size(); ++k) {
             const DStep& s0 = plans[0][k];
@@ -982,9 +986,9 @@ int qsim_dist_run(qsim_dist* d, const qsim_gate* gates, size_t count, int flags)
                     fail(QSIM_ERR_RUNTIME, "exchange skeleton mismatch");
             if (s0.kind == 1) {
                 if (s0.pivot >= 0) {
-                    // the role-1 step before recorded hev[0] / hev[1]; if it had nothing to
-                    // split, both halves are ready now
-                    if (k == 0 || plans[0][k - 1].role != 1) {
+                    // the ops step before (role bit 1) recorded hev[0] / hev[1] after its tail
+                    // halves; otherwise both halves are ready now
+                    if (k == 0 || !(plans[0][k - 1].role & 1)) {
                         QSIM_HIPCHK(hipEventRecord(d->hev[0], d->stream));
                         QSIM_HIPCHK(hipEventRecord(d->hev[1], d->stream));
                     }
@@ -997,35 +1001,30 @@ int qsim_dist_run(qsim_dist* d, const qsim_gate* gates, size_t count, int flags)
                 }
                 continue;
             }
-            if (s0.role == 0) {
-                wait_pending();
-                for (size_t i = 0; i < S; ++i) run_local(d, d->shards[i], plans[i][k].ops, flags, *rp.fplans[i][k]);
-                continue;
-            }
-            bool split = true;  // the same decision on every shard of this process
-            for (size_t i = 0; i < S; ++i)
-                split = split && halves_ok(d, plans[i][k].ops, flags, *rp.fplans[i][k], s0.pivot);
-            if (s0.role == 1) {  // before the remap: half 0, signal, half 1, signal
+            // ops step: head per half (after the exchange before), middle, tail per half
+            const int pb = (s0.role & 2) ? plans[0][k - 1].pivot : -1;
+            const int pa = (s0.role & 1) ? plans[0][k + 1].pivot : -1;
+            std::vector<StepRun> runs(S);
+            for (size_t i = 0; i < S; ++i) runs[i] = prepare_step(d, plans[i][k].ops, flags, *rp.fplans[i][k], pb, pa);
+            const bool head = pb >= 0 && pending;
+            if (head) {
                 for (int h = 0; h < 2; ++h) {
-                    if (split || h == 0)
-                        for (size_t i = 0; i < S; ++i)
-                            run_local(d, d->shards[i], plans[i][k].ops, flags, *rp.fplans[i][k], s0.pivot,
-                                      split ? h : -1);
+                    QSIM_HIPCHK(hipStreamWaitEvent(d->stream, d->hev[6 + h], 0));
+                    for (size_t i = 0; i < S; ++i)
+                        if (runs[i].plan) run_part(d, d->shards[i], plans[i][k].ops, runs[i], 0, runs[i].j1, pb, h);
+                }
+            }
+            wait_pending();
+            for (size_t i = 0; i < S; ++i) {
+                if (runs[i].plan) run_part(d, d->shards[i], plans[i][k].ops, runs[i], head ? runs[i].j1 : 0, runs[i].j2);
+                else run_part(d, d->shards[i], plans[i][k].ops, runs[i], 0, 1);  // per-gate: the whole list
+            }
+            if (pa >= 0) {  // the exchange after waits for hev[h]
+                for (int h = 0; h < 2; ++h) {
+                    for (size_t i = 0; i < S; ++i)
+                        if (runs[i].plan) run_part(d, d->shards[i], plans[i][k].ops, runs[i], runs[i].j2, runs[i].np, pa, h);
                     QSIM_HIPCHK(hipEventRecord(d->hev[h], d->stream));
                 }
-            } else {  // after the remap: each half once its half-exchange has landed
-                for (int h = 0; h < 2; ++h) {
-                    if (!split && h == 0) continue;
-                    if (split) {
-                        QSIM_HIPCHK(hipStreamWaitEvent(d->stream, d->hev[6 + h], 0));
-                    } else {
-                        wait_pending();
-                    }
-                    for (size_t i = 0; i < S; ++i)
-                        run_local(d, d->shards[i], plans[i][k].ops, flags, *rp.fplans[i][k], s0.pivot,
-                                  split ? h : -1);
-                }
-                pending = false;
             }
         }
         wait_pending();

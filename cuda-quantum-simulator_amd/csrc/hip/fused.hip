@@ -316,8 +316,9 @@ struct PassChoice {
 //   greedy: first fit in program order — a gate joins when its qubits still fit the tile.
 //   lookahead: grow the tile's qubit set one qubit (or, when no single qubit helps, one pair) at
 //     a time, each time taking the choice that lets the most upcoming gates into the pass.
+// avoid: qubits a tile should contain only when that lets more gates in (ties go to others).
 static std::vector<PassChoice> choose_passes(const std::vector<Op>& ops, int n, int r0, int nfree,
-                                             bool lookahead) {
+                                             bool lookahead, uint64_t avoid) {
     const uint64_t low = (1ull << r0) - 1ull;
     std::vector<PassChoice> out;
     std::vector<Op> rem = ops;
@@ -350,10 +351,10 @@ static std::vector<PassChoice> choose_passes(const std::vector<Op>& ops, int n, 
             for (size_t i = 0; i < rem.size(); ++i) qm[i] = op_qubits(rem[i]);
             while (__builtin_popcountll(hi) < nfree) {
                 const int base = score(low | hi);
-                int best = base, bq = -1;
+                int best = 2 * base + 1, bq = -1;  // key 2 * score + (not avoided)
                 for (int q = r0; q < n; ++q) {
                     if ((hi >> q) & 1ull) continue;
-                    const int c = score(low | hi | (1ull << q));
+                    const int c = 2 * score(low | hi | (1ull << q)) + (((avoid >> q) & 1ull) ? 0 : 1);
                     if (c > best) best = c, bq = q;
                 }
                 if (bq >= 0) {
@@ -362,6 +363,7 @@ static std::vector<PassChoice> choose_passes(const std::vector<Op>& ops, int n, 
                 }
                 if (__builtin_popcountll(hi) + 2 > nfree) break;
                 int pa = -1, pb = -1;
+                best = base;
                 for (int qa = r0; qa < n; ++qa) {
                     if ((hi >> qa) & 1ull) continue;
                     for (int qb = qa + 1; qb < n; ++qb) {
@@ -404,7 +406,8 @@ static std::vector<PassChoice> choose_passes(const std::vector<Op>& ops, int n, 
 // partly covers, so a 2-qubit gate's first qubit already counts) — and the `width` states with
 // the fewest remaining gates survive each step.  The first state to run out of gates gives the
 // plan.  W-HC 30q: 7 passes (one-tile-at-a-time lookahead) -> 5.
-static std::vector<PassChoice> beam_passes(const std::vector<Op>& ops, int n, int heff, int width) {
+static std::vector<PassChoice> beam_passes(const std::vector<Op>& ops, int n, int heff, int width,
+                                           uint64_t avoid) {
     const size_t window = 512;
     std::vector<uint64_t> qm(ops.size());
     for (size_t i = 0; i < ops.size(); ++i) qm[i] = op_qubits(ops[i]);
@@ -508,7 +511,8 @@ static std::vector<PassChoice> beam_passes(const std::vector<Op>& ops, int n, in
                             const uint64_t h = pp.second | (1ull << q);
                             bool dup = false;
                             for (const auto& g2 : grown) dup = dup || g2.second == h;
-                            if (!dup) grown.push_back({score(s.rem, low | h, low), h});
+                            // key 2 * score + (not avoided): an avoided qubit only on merit
+                            if (!dup) grown.push_back({2 * score(s.rem, low | h, low) + (((avoid >> q) & 1ull) ? 0 : 1), h});
                         }
                     if (grown.empty()) break;
                     std::stable_sort(grown.begin(), grown.end(),
@@ -611,7 +615,7 @@ Plan plan_fused(const std::vector<Op>& ops, int n, int hmax, uint64_t avoid) {
         if (r0_pin && heff >= 4 && r0 != std::min(6, std::max(4, r0_pin))) continue;
         for (int la = 0; la <= (heff >= 4 ? 1 : 0); ++la) {
             if (strat_pin >= 0 && heff >= 4 && la != (strat_pin ? 1 : 0)) continue;
-            std::vector<PassChoice> c = choose_passes(ops, n, r0, 6 + heff - r0, la != 0);
+            std::vector<PassChoice> c = choose_passes(ops, n, r0, 6 + heff - r0, la != 0, avoid);
             for (PassChoice& ch : c) ch.r0 = r0;
             if (best.empty() || c.size() < best.size()) best.swap(c);
         }
@@ -621,7 +625,7 @@ Plan plan_fused(const std::vector<Op>& ops, int n, int hmax, uint64_t avoid) {
     if (beam > 0 && heff >= 4 && n >= beam_min_q && !r0_pin && strat_pin < 0 && best.size() > 1) {
         // width shrinks with the circuit so the search stays ~O(10^8) simple steps
         const int w = std::max(2, std::min(beam, (int)(32.0 * 256.0 / std::max<size_t>(256, ops.size()))));
-        std::vector<PassChoice> c = beam_passes(ops, n, heff, w);
+        std::vector<PassChoice> c = beam_passes(ops, n, heff, w, avoid);
         if (!c.empty() && c.size() < best.size()) best.swap(c);
     }
     for (PassChoice& ch : best) {

@@ -277,9 +277,11 @@ typedef struct qsim_op {
 } qsim_op;
 /* One plan step: kind 0 = ops[op_begin, op_end) on the local shard; kind 1 = exchange that
  * swaps global physical positions gpos[i] with local positions lpos[i], i < k.  Overlapped
- * remaps: an exchange with pivot >= 0 runs as two half-exchanges (pivot bit 0, then 1); the ops
- * step just before it has role 1 and the one just after role 2 (run per half so each half's
- * transfer overlaps the other half's local work; they never touch the pivot); role 0 = plain. */
+ * remaps: an exchange with pivot >= 0 runs as two half-exchanges (pivot bit 0, then 1).  An ops
+ * step with role bit 1 runs the trailing passes of its fused plan that avoid the pivot of the
+ * exchange after it per half (each half's transfer then overlaps the other half's passes); role
+ * bit 2: its leading passes that avoid the pivot of the exchange before it run per half as each
+ * half lands.  The step is planned as one fused plan either way (ops steps report pivot -1). */
 typedef struct qsim_dist_step {
     int32_t kind, k;
     int32_t op_begin, op_end;
