@@ -299,7 +299,12 @@ def main():
                               timeout_s=args.launch_timeout))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if args.workload == "batch":
-        run_batch(args)
+        if world > 1 or args.dry_run:
+            from qsim_amd import dist_bench  # trajectory-sharded replicas
+            dist_bench.run_batch(args, "trajectory-gates/s, W-HC circuit on noisy trajectories "
+                                       "(BatchedSimulator)", HBM_PEAK_GBPS)
+        else:
+            run_batch(args)
         return
     if world > 1 or args.gpus > 1 or args.dry_run:
         from qsim_amd import dist_bench  # sharded strong-scaling path (RCCL over xGMI)

@@ -46,14 +46,16 @@ struct DevChannel {
 };
 
 // This step's Pauli picks of trajectory b, composed into i^e X^x Z^z (channels in order).
+// b is the GLOBAL trajectory index (qsim_batch_set_trajectory_offset): a sharded ensemble draws
+// exactly what one object holding every trajectory draws.
 __device__ __forceinline__ void draw_step(const DevChannel* ch, int nch, uint64_t seed, uint64_t step,
-                                          int b, uint64_t& x, uint64_t& z, int& e) {
+                                          uint64_t b, uint64_t& x, uint64_t& z, int& e) {
     x = 0;
     z = 0;
     e = 0;
     for (int c = 0; c < nch; ++c) {
         const uint64_t key = mix64(seed ^ mix64(step * 0x100000001b3ull + (uint64_t)c) ^
-                                   ((uint64_t)b << 20));
+                                   (b << 20));
         const double r1 = u01(mix64(key));
         int pauli = 0;  // 1 X, 2 Y, 3 Z
         const int t = ch[c].type;
@@ -83,12 +85,12 @@ __device__ __forceinline__ void draw_step(const DevChannel* ch, int nch, uint64_
 
 // One thread per trajectory: compose this step's Pauli picks into (e, x, z).
 __global__ void k_pauli_draw(const DevChannel* ch, int nch, uint64_t seed, uint64_t step,
-                             int batch, uint64_t* xz, int* ephase) {
+                             int batch, uint64_t traj0, uint64_t* xz, int* ephase) {
     const int b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= batch) return;
     uint64_t x, z;
     int e;
-    draw_step(ch, nch, seed, step, b, x, z, e);
+    draw_step(ch, nch, seed, step, traj0 + (uint64_t)b, x, z, e);
     xz[2 * b] = x;
     xz[2 * b + 1] = z;
     ephase[b] = e;
@@ -102,13 +104,13 @@ __global__ void k_pauli_draw(const DevChannel* ch, int nch, uint64_t seed, uint6
 // parallel (written into frames[s] as (x, z) plus ephase[s]), then one thread per trajectory
 // scans the steps in order, replacing each draw by the frame before it.
 __global__ void k_draw_steps(const DevChannel* ch, int nch, uint64_t seed, uint64_t step0,
-                             int count, int batch, uint64_t* frames, int* ephase) {
+                             int count, int batch, uint64_t traj0, uint64_t* frames, int* ephase) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= (uint64_t)count * batch) return;
     const int s = (int)(i / batch), b = (int)(i - (uint64_t)s * batch);
     uint64_t x, z;
     int e;
-    draw_step(ch, nch, seed, step0 + (uint64_t)s, b, x, z, e);
+    draw_step(ch, nch, seed, step0 + (uint64_t)s, traj0 + (uint64_t)b, x, z, e);
     frames[2 * i] = x;
     frames[2 * i + 1] = z;
     ephase[i] = e;
@@ -234,6 +236,7 @@ struct qsim_batch {
     double2* d = nullptr;
     hipStream_t stream = nullptr;
     uint64_t seed = 0, step = 0;
+    uint64_t traj0 = 0;     // global index of trajectory 0 (trajectory-sharded ensembles)
     uint64_t ncounter = 0;  // per-pair noise passes so far (QSIM_BATCH_REFERENCE_NOISE)
     uint64_t* d_xz = nullptr;
     int* d_e = nullptr;
@@ -325,6 +328,14 @@ int qsim_batch_set_seed(qsim_batch* b, uint64_t seed) {
     });
 }
 
+int qsim_batch_set_trajectory_offset(qsim_batch* b, uint64_t first) {
+    return bguard([&] {
+        need(b);
+        if (first > (1ull << 40)) fail(QSIM_ERR_INVALID_ARGUMENT, "trajectory offset out of range");
+        b->traj0 = first;
+    });
+}
+
 int qsim_batch_run(qsim_batch* b, const qsim_gate* gates, size_t count,
                    const qsim_noise_channel* channels, size_t n_channels, int flags) {
     return bguard([&] {
@@ -376,7 +387,7 @@ int qsim_batch_run(qsim_batch* b, const qsim_gate* gates, size_t count,
                 if (op.kind >= 0) launch_op(b->d, b->n, (uint64_t)b->batch, op, b->stream, &b->timer);
                 for (const qsim_noise_channel* c : dep)
                     launch_noise(b->d, b->n, 0, c->qubit, c->probability, b->seed, b->ncounter++,
-                                 b->stream, &b->timer, (uint64_t)b->batch);
+                                 b->stream, &b->timer, (uint64_t)b->batch, b->traj0);
             }
             return;
         }
@@ -420,7 +431,7 @@ int qsim_batch_run(qsim_batch* b, const qsim_gate* gates, size_t count,
                 const uint64_t draws = (uint64_t)count * b->batch;
                 hipLaunchKernelGGL(k_draw_steps, dim3((unsigned)((draws + 255) / 256)), dim3(256), 0,
                                    b->stream, b->d_ch, (int)ch.size(), b->seed, b->step, (int)count,
-                                   b->batch, b->d_frames, b->d_fe);
+                                   b->batch, b->traj0, b->d_frames, b->d_fe);
                 b->cliff.upload(cl.data(), cl.size() * sizeof(StepClifford), b->stream);
                 hipLaunchKernelGGL(k_frame_build, dim3((b->batch + 63) / 64), dim3(64), 0, b->stream,
                                    (int)count, b->batch, b->d_frames, b->d_fe,
@@ -462,7 +473,7 @@ int qsim_batch_run(qsim_batch* b, const qsim_gate* gates, size_t count,
                     TimedLaunch tl(&b->timer, "pauli_draw", 0.0, b->stream);
                     hipLaunchKernelGGL(k_pauli_draw, dim3((b->batch + 255) / 256), dim3(256), 0,
                                        b->stream, b->d_ch, (int)ch.size(), b->seed, b->step,
-                                       b->batch, b->d_xz, b->d_e);
+                                       b->batch, b->traj0, b->d_xz, b->d_e);
                     QSIM_HIPCHK(hipGetLastError());
                 }
                 ++b->step;

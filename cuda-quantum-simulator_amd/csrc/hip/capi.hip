@@ -225,6 +225,15 @@ int qsim_state_last_run(qsim_state* s, int* passes, int* jit_passes) {
 }
 int qsim_abi_version(void) { return QSIM_ABI_VERSION; }
 
+int qsim_set_device(int device) {
+    return guarded([&] {
+        int c = 0;
+        QSIM_HIPCHK(hipGetDeviceCount(&c));
+        if (device < 0 || device >= c) fail(QSIM_ERR_INVALID_ARGUMENT, "device index out of range");
+        QSIM_HIPCHK(hipSetDevice(device));
+    });
+}
+
 int qsim_device_count(int* count) {
     return guarded([&] {
         QSIM_REQUIRE(count, QSIM_ERR_INVALID_ARGUMENT, "null count");

@@ -213,9 +213,10 @@ void launch_fused(double2* st, int n, uint64_t batch, const Plan& plan, const Ti
                   const uint64_t* frames = nullptr, const FusedRange& range = FusedRange());
 
 // Single-trajectory Monte-Carlo noise (noise.hip): one per-pair pass of channel `type`
-// (reference NoiseType numbering) on `qubit`, uniforms from the hash of (seed, counter, pair).
+// (reference NoiseType numbering) on `qubit`, uniforms from the hash of (seed, counter, pair);
+// traj0: global trajectory index of trajectory 0 (the pair index hashed is the global one).
 void launch_noise(double2* st, int n, int type, int qubit, double p, uint64_t seed,
-                  uint64_t counter, hipStream_t s, Timer* tm, uint64_t batch = 1);
+                  uint64_t counter, hipStream_t s, Timer* tm, uint64_t batch = 1, uint64_t traj0 = 0);
 
 // Density matrices as 2n-index-bit states (density.hip).
 void dm_lower(int n, const qsim_gate* gates, size_t count, const qsim_noise_channel* ch,

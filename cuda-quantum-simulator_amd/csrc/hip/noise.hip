@@ -48,6 +48,7 @@ struct NArgs {
     uint64_t pairs;  // B x 2^(n-1): pair idx of trajectory t is t * 2^(n-1) + its index in t
     int log_ppt;     // n - 1
     uint64_t key;    // noise_key(seed, counter)
+    uint64_t idx0;   // global pair index of local pair 0 (trajectory-sharded ensembles)
     int target;
     double p;
 };
@@ -57,7 +58,7 @@ __global__ __launch_bounds__(256) void k_noise(NArgs a) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     const uint64_t mask = (1ull << a.target) - 1ull;
     for (uint64_t idx = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < a.pairs; idx += stride) {
-        const uint64_t h = nz_mix(a.key ^ nz_mix(idx));
+        const uint64_t h = nz_mix(a.key ^ nz_mix(a.idx0 + idx));
         const float r1 = nz_uniform(h);
         // reference idx -> (traj, pair_idx) split (src/NoiseModel.cu:843-856); batch 1: traj 0
         const uint64_t traj = idx >> a.log_ppt, pr = idx & ((1ull << a.log_ppt) - 1ull);
@@ -132,7 +133,7 @@ uint64_t noise_key(uint64_t seed, uint64_t counter) {
 }
 
 void launch_noise(double2* st, int n, int type, int qubit, double p, uint64_t seed,
-                  uint64_t counter, hipStream_t s, Timer* tm, uint64_t batch) {
+                  uint64_t counter, hipStream_t s, Timer* tm, uint64_t batch, uint64_t traj0) {
     if (type < 0 || type > 5) fail(QSIM_ERR_INVALID_ARGUMENT, "unknown noise type");
     if (qubit < 0 || qubit >= n)
         fail(QSIM_ERR_OUT_OF_RANGE, "Qubit index " + std::to_string(qubit) + " out of range");
@@ -142,6 +143,7 @@ void launch_noise(double2* st, int n, int type, int qubit, double p, uint64_t se
     a.pairs = batch << (n - 1);
     a.log_ppt = n - 1;
     a.key = noise_key(seed, counter);
+    a.idx0 = traj0 << (n - 1);
     a.target = qubit;
     a.p = p;
     const uint64_t blocks = std::min<uint64_t>((a.pairs + 255) / 256, 256ull * 32);

@@ -145,6 +145,10 @@ void BatchedSimulator::setSeed(unsigned int seed) {
     check(qsim_batch_set_seed(h_, seed));
 }
 
+void BatchedSimulator::setTrajectoryOffset(unsigned long long first) {
+    check(qsim_batch_set_trajectory_offset(h_, first));
+}
+
 void BatchedSimulator::reset() { check(qsim_batch_reset(h_)); }
 
 void BatchedSimulator::run(const Circuit& circuit) {

@@ -8,7 +8,8 @@ from .circuit import (Circuit, GateOp, GateType, MAX_QUBITS, MIN_QUBITS, createB
                       createGHZCircuit, createRandomCircuit, createRandomHCCircuit,
                       createScalingBenchmarkCircuit, is_valid_qubit_count)
 from .simulator import (BatchedGateSet, BatchedNoise, BatchedSimulator, NoiseChannel, NoiseModel, NoiseType,
-                        NoisySimulator, RunMode, Simulator, StateVector, device_count, device_info)
+                        NoisySimulator, RunMode, Simulator, StateVector, device_count, device_info,
+                        set_device)
 from .density import DensityMatrix, DensityMatrixSimulator
 
 __all__ = [
@@ -17,5 +18,5 @@ __all__ = [
     "createGHZCircuit", "createRandomCircuit", "createRandomHCCircuit",
     "createScalingBenchmarkCircuit", "is_valid_qubit_count", "BatchedGateSet", "BatchedNoise",
     "BatchedSimulator", "NoiseChannel", "NoiseModel", "NoiseType", "NoisySimulator", "RunMode", "Simulator",
-    "StateVector", "device_count", "device_info",
+    "StateVector", "device_count", "device_info", "set_device",
 ]

@@ -70,6 +70,7 @@ def _sig(lib, name, argtypes, restype=c_int):
 _sig(hip, "qsim_last_error", [], c_char_p)
 _sig(hip, "qsim_abi_version", [])
 _sig(hip, "qsim_device_count", [POINTER(c_int)])
+_sig(hip, "qsim_set_device", [c_int])
 _sig(hip, "qsim_device_info", [c_int, c_char_p, c_size_t, POINTER(c_int), POINTER(c_size_t)])
 _sig(hip, "qsim_state_create", [c_int, POINTER(_P)])
 _sig(hip, "qsim_state_create_on", [c_int, c_int, POINTER(_P)])
@@ -116,6 +117,7 @@ _sig(hip, "qsim_batch_create", [c_int, c_int, POINTER(_P)])
 _sig(hip, "qsim_batch_destroy", [_P])
 _sig(hip, "qsim_batch_reset", [_P])
 _sig(hip, "qsim_batch_set_seed", [_P, c_uint64])
+_sig(hip, "qsim_batch_set_trajectory_offset", [_P, c_uint64])
 _sig(hip, "qsim_batch_run", [_P, POINTER(qsim_gate), c_size_t, POINTER(qsim_noise_channel),
                              c_size_t, c_int])
 _sig(hip, "qsim_batch_avg_probabilities", [_P, _P])

@@ -139,3 +139,93 @@ def run(args, metric: str, peak_gbps: float) -> None:
         print(json.dumps(out), flush=True)
     sim.close()
     grp.close()
+
+
+def split_trajectories(total: int, world: int, rank: int):
+    """(first, count) of rank's share of `total` trajectories: contiguous, sizes differing by at
+    most one.  The shards' noise draws are keyed by the global index (setTrajectoryOffset)."""
+    base, extra = divmod(total, world)
+    return rank * base + min(rank, extra), base + (1 if rank < extra else 0)
+
+
+def run_batch(args, metric: str, peak_gbps: float) -> None:
+    """W-BATCH over N GPUs (SURVEY §8(e) "BatchedSimulator shards trivially by trajectory"): each
+    rank runs its contiguous share of the --trajectories total (replicas, no data-path exchange;
+    strong scaling: the ensemble is fixed), and the ensemble's average probabilities are the
+    trajectory-weighted sum of the ranks' averages, reduced once after the timed region.  The
+    noise realisations are those of a single-GPU run of the whole ensemble (global trajectory
+    keys), so the reduced average is the single-GPU one up to summation order."""
+    import numpy as np
+    rank, world, local = _rank_world(args)
+    grp = FileGroup(rank, world)
+    first, count = split_trajectories(args.trajectories, world, rank)
+    n = args.qubits
+    dry = getattr(args, "dry_run", False)
+    from . import circuit as qc
+    circuit = qc.createRandomHCCircuit(n, args.depth, args.seed)
+    gates = circuit.getGateCount()
+    if dry:  # skeleton only: split, barriers, max-over-ranks timing, the weighted reduction
+        grp.barrier()
+        t0 = time.perf_counter()
+        t1 = time.perf_counter()
+        avg = np.full(1 << n, 1.0 / (1 << n))
+        stats, roof = [], None
+    else:
+        from . import simulator as qs
+        from .plan import set_jit
+        ndev = qs.device_count()
+        if local >= ndev:  # replicas may share a GPU (e.g. a 2-rank rehearsal on a 1-GPU box)
+            import sys
+            print(f"rank {rank}: LOCAL_RANK {local} >= {ndev} visible GPUs, using GPU {local % ndev}",
+                  file=sys.stderr)
+        qs.set_device(local % ndev)
+        set_jit(getattr(args, "jit", 2), -1)
+        nm = qs.NoiseModel()
+        nm.addDepolarizingAll(n, args.noise)
+        sem = qs.BatchedNoise.Reference if args.batch_noise == "reference" else qs.BatchedNoise.Physical
+        sim = qs.BatchedSimulator(n, count, nm, noise=sem)
+        sim.setSeed(args.seed)
+        sim.setTrajectoryOffset(first)
+        for _ in range(max(1, args.warmup)):
+            sim.run(circuit)
+        sim.synchronize()
+        sim.profile(True)
+        grp.barrier()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            sim.run(circuit)
+        sim.synchronize()
+        t1 = time.perf_counter()
+        stats = sim.profileStats()
+        gate_stats = [s for s in stats if s["alg_bytes"] > 0]
+        dom = max(gate_stats, key=lambda s: s["ms"]) if gate_stats else None
+        roof = None
+        if dom and dom["launches"]:
+            per = dom["alg_bytes"] / dom["launches"]
+            avg_s = dom["ms"] / dom["launches"] / 1e3
+            roof = {"bound": "hbm", "kernel": dom["name"], "achieved": round(per / avg_s / 1e9, 1),
+                    "peak": peak_gbps, "unit": "GB/s", "frac": round(per / avg_s / 1e9 / peak_gbps, 4),
+                    "traffic": None, "alg_bytes_per_launch": per,
+                    "avg_launch_ms": round(avg_s * 1e3, 4), "launches": dom["launches"]}
+        avg = sim.getAverageProbabilities()
+    grp.barrier()
+    wall = max(grp.all_reduce_max(t1 - t0), 1e-9)
+    # ensemble average: sum over ranks of (count_r / total) * average_r (after the timed region)
+    parts = grp.all_gather((avg * (count / args.trajectories)).astype(np.float64).tobytes())
+    ens = np.sum([np.frombuffer(p, dtype=np.float64) for p in parts], axis=0)
+    if rank == 0:
+        total = args.trajectories
+        print(json.dumps({
+            "metric": metric, "value": round(gates * total * args.steps / wall, 1),
+            "unit": "trajectory-gates/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(wall / args.steps * 1e3, 3), "higher_is_better": True,
+            "scaling": "strong", "vs_baseline": None, "dtype": "c128 (complex<double>)",
+            "data": "synthetic", "dry_run": bool(dry),
+            "config": {"workload": f"W-BATCH {n}q x {total} trajectories, depolarizing {args.noise} "
+                                   f"on all qubits after every gate, W-HC depth {args.depth} seed {args.seed}",
+                       "qubits": n, "trajectories": total, "gates": gates,
+                       "trajectories_per_rank": [split_trajectories(total, world, r)[1] for r in range(world)],
+                       "ensemble_probability_sum": float(ens.sum()),
+                       "parallelism": f"trajectories sharded over {world} GPUs (replicas, no exchange)"},
+            "roofline": roof, "kernels_rank0": stats, "cpu_baseline": None}), flush=True)
+    grp.close()

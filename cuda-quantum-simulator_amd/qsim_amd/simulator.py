@@ -36,6 +36,11 @@ def device_count() -> int:
     return c.value
 
 
+def set_device(device: int) -> None:
+    """Device the calling thread's next objects are created on (one process per GPU)."""
+    _lib.check(_lib.hip.qsim_set_device(int(device)))
+
+
 def device_info(device: int = 0):
     name = _c.create_string_buffer(256)
     cus = _c.c_int(0)
@@ -475,6 +480,12 @@ class BatchedSimulator:
     def setSeed(self, seed: int) -> None:
         self._rng = np.random.default_rng(seed)
         _lib.check(_lib.hip.qsim_batch_set_seed(self._h, seed))
+
+    def setTrajectoryOffset(self, first: int) -> None:
+        """This object's trajectories are [first, first + batch_size) of a larger ensemble: noise
+        draws are keyed by the global trajectory index, so shards of an ensemble (one per GPU)
+        reproduce the single-object run exactly (qsim_batch_set_trajectory_offset)."""
+        _lib.check(_lib.hip.qsim_batch_set_trajectory_offset(self._h, int(first)))
 
     def reset(self) -> None: _lib.check(_lib.hip.qsim_batch_reset(self._h))
 

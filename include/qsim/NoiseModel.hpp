@@ -121,6 +121,9 @@ public:
 
     void setNoiseModel(const NoiseModel& noise_model) { noise_model_ = noise_model; }
     void setSeed(unsigned int seed);
+    // Trajectory sharding (one object per GPU): this object's trajectories are
+    // [first, first + batch_size) of a larger ensemble; noise draws use the global index.
+    void setTrajectoryOffset(unsigned long long first);
     void reset();
     void run(const Circuit& circuit);
 

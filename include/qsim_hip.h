@@ -79,6 +79,9 @@ typedef struct qsim_batch qsim_batch; /* B trajectories of 2^n amplitudes (Batch
 const char* qsim_last_error(void);
 int qsim_abi_version(void);
 int qsim_device_count(int* count);
+/* Device of the calling thread's next objects (hipSetDevice; the reference always uses the
+ * default device).  One process per GPU selects its LOCAL_RANK with this. */
+int qsim_set_device(int device);
 /* Name/bandwidth facts of the current device (for bench reports). name_len includes NUL. */
 int qsim_device_info(int device, char* name, size_t name_len, int* cu_count, size_t* total_mem);
 
@@ -192,6 +195,12 @@ int qsim_batch_create(int n_qubits, int batch_size, qsim_batch** out);
 int qsim_batch_destroy(qsim_batch* b);
 int qsim_batch_reset(qsim_batch* b);
 int qsim_batch_set_seed(qsim_batch* b, uint64_t seed);
+/* Trajectory sharding (SURVEY §8(e) "BatchedSimulator shards trivially by trajectory"; no
+ * reference counterpart — the reference runs every trajectory on one GPU): this object's B
+ * trajectories are trajectories [first, first + B) of a larger ensemble.  Noise draws are keyed
+ * by the global trajectory index (both noise processes), so G objects with offsets 0, B, 2B, ...
+ * and the same seed hold exactly the trajectories one object of G*B trajectories would. */
+int qsim_batch_set_trajectory_offset(qsim_batch* b, uint64_t first);
 /* Apply the circuit to every trajectory; after each gate apply every channel (reference
  * BatchedSimulator::run, src/NoiseModel.cu:815-831).  Gate semantics follow
  * src/NoiseModel.cu:717-801 when flags has QSIM_BATCH_REFERENCE_GATESET, else the full gate set.

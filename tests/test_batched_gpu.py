@@ -157,3 +157,35 @@ def test_config4_full_size_noisy_run(qsim, gpu_ready):
         assert abs(np.sum(np.abs(s.getStateVector(t)) ** 2) - 1.0) < 1e-10
     h = s.getHistogram(4)
     assert h.sum() == 4 * B
+
+
+@pytest.mark.parametrize("noise", ["physical", "reference"])
+@pytest.mark.parametrize("per_gate", [False, True])
+def test_trajectory_shards_reproduce_the_ensemble(qsim, gpu_ready, noise, per_gate):
+    """BatchedSimulator shards by trajectory.  G objects of B/G trajectories with
+    offsets 0, B/G, ... and the same seed hold exactly the trajectories of one B-trajectory
+    object (noise draws keyed by the global trajectory index), over two runs."""
+    n, B, G = 12, 8, 4
+    c = _mixed(qsim, n, 50, 9)
+    nm = _noise(qsim, n)
+    sem = qsim.BatchedNoise.Reference if noise == "reference" else qsim.BatchedNoise.Physical
+    full = qsim.BatchedSimulator(n, B, nm, noise=sem)
+    full.setSeed(21)
+    shards = []
+    for r in range(G):
+        s = qsim.BatchedSimulator(n, B // G, nm, noise=sem)
+        s.setSeed(21)
+        s.setTrajectoryOffset(r * (B // G))
+        shards.append(s)
+    for _ in range(2):
+        full.run(c, per_gate=per_gate)
+        for s in shards:
+            s.run(c, per_gate=per_gate)
+    avg = np.zeros(1 << n)
+    for r, s in enumerate(shards):
+        for t in range(B // G):
+            np.testing.assert_array_equal(s.getStateVector(t), full.getStateVector(r * (B // G) + t))
+        avg += s.getAverageProbabilities() * (B // G) / B
+    np.testing.assert_allclose(avg, full.getAverageProbabilities(), atol=1e-14, rtol=0)
+    # the draws really differ between trajectories (the offset is not a no-op)
+    assert any(np.max(np.abs(full.getStateVector(0) - full.getStateVector(t))) > 1e-6 for t in range(1, B))

@@ -87,3 +87,33 @@ def test_rendezvous_collectives_in_process():
             t.join(60)
         assert res == {r: (b"id-bytes", 3.0, 2.0) for r in range(3)}
         assert not os.path.exists(os.path.join(d, "qsim_rdzv_c"))
+
+
+@pytest.mark.parametrize("world,total", [(2, 1024), (4, 1023)])
+def test_batch_dry_run_shards_trajectories(world, total):
+    """`bench.py --workload batch --gpus N --dry-run`: N ranks take contiguous trajectory shares
+    (sizes differ by at most one, covering the ensemble), the trajectory-weighted reduction of the
+    ranks' averages is a probability vector, one JSON line."""
+    r = subprocess.run([sys.executable, BENCH, "--workload", "batch", "--gpus", str(world), "--dry-run",
+                        "--steps", "2", "--warmup", "1", "--qubits", "10", "--trajectories", str(total)],
+                       capture_output=True, text=True, timeout=300, env=_env())
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    per = out["config"]["trajectories_per_rank"]
+    assert out["n_gpus"] == world and out["dry_run"] is True and out["unit"] == "trajectory-gates/s"
+    assert sum(per) == total and max(per) - min(per) <= 1
+    assert abs(out["config"]["ensemble_probability_sum"] - 1.0) < 1e-12
+
+
+def test_split_trajectories_covers_the_ensemble():
+    sys.path.insert(0, os.path.join(ROOT, "cuda-quantum-simulator_amd"))
+    from qsim_amd.dist_bench import split_trajectories
+    for total in (1, 7, 1024, 1023):
+        for world in (1, 2, 3, 8):
+            spans = [split_trajectories(total, world, r) for r in range(world)]
+            assert spans[0][0] == 0
+            for (f0, c0), (f1, _) in zip(spans, spans[1:]):
+                assert f0 + c0 == f1
+            assert spans[-1][0] + spans[-1][1] == total
