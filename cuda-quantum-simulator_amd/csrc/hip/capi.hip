@@ -74,6 +74,14 @@ void Timer::end(int slot, hipEvent_t a, double bytes) {
     QSIM_HIPCHK(hipEventRecord(b, stream));
     pending.push_back(Pending{slot, a, b, bytes});
 }
+void Timer::begin_ext(const char* name, hipEvent_t* a_out, hipEvent_t* b_out, int* slot_out) {
+    *slot_out = slot_of(name);
+    *a_out = take_event(pool);
+    *b_out = take_event(pool);
+}
+void Timer::finish(int slot, hipEvent_t a, hipEvent_t b, double bytes) {
+    pending.push_back(Pending{slot, a, b, bytes});
+}
 void Timer::resolve() {
     for (auto& p : pending) {
         QSIM_HIPCHK(hipEventSynchronize(p.b));
@@ -140,10 +148,12 @@ DevBuf::~DevBuf() {
     }
     if (ptr) (void)hipFree(ptr);
 }
-TimedLaunch::TimedLaunch(Timer* t, const char* name, double b, hipStream_t s) : tm(t), bytes(b) {
+TimedLaunch::TimedLaunch(Timer* t, const char* name, double by, hipStream_t s, bool e)
+    : tm(t), bytes(by), ext(e) {
     if (tm && tm->enabled) {
         tm->stream = s;
-        tm->begin(name, b, &a, &slot);
+        if (ext) tm->begin_ext(name, &a, &b, &slot);
+        else tm->begin(name, by, &a, &slot);
     } else {
         tm = nullptr;
     }
@@ -151,7 +161,8 @@ TimedLaunch::TimedLaunch(Timer* t, const char* name, double b, hipStream_t s) : 
 TimedLaunch::~TimedLaunch() {
     if (tm) {
         try {
-            tm->end(slot, a, bytes);
+            if (ext) tm->finish(slot, a, b, bytes);
+            else tm->end(slot, a, bytes);
         } catch (...) {
         }
     }

@@ -16,6 +16,7 @@
 // it shares no qubit with an earlier gate that was deferred (gates on disjoint qubits commute
 // exactly).  Gate semantics are the per-gate kernels' (device_ops.hpp), i.e. src/Gates.cu.
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <algorithm>
 #include <array>
@@ -624,7 +625,7 @@ Plan plan_fused(const std::vector<Op>& ops, int n, int hmax, uint64_t avoid) {
     static const int beam_min_q = env_int("QSIM_PLAN_BEAM_MIN_QUBITS", 20);
     if (beam > 0 && heff >= 4 && n >= beam_min_q && !r0_pin && strat_pin < 0 && best.size() > 1) {
         // width shrinks with the circuit so the search stays ~O(10^8) simple steps
-        const int w = std::max(2, std::min(beam, (int)(32.0 * 256.0 / std::max<size_t>(256, ops.size()))));
+        const int w = std::max(2, (int)(beam * 256.0 / std::max<size_t>(256, ops.size())));
         std::vector<PassChoice> c = beam_passes(ops, n, heff, w, avoid);
         if (!c.empty() && c.size() < best.size()) best.swap(c);
     }
@@ -1196,7 +1197,8 @@ void launch_fused(double2* st, int n, uint64_t batch, const Plan& plan, const Ti
         a.log_tpt = lt;
         a.tpt_mask = (1ull << lt) - 1ull;
         const uint64_t blocks = batch << lt;
-        TimedLaunch tl(tm, "fused_tile", pass_bytes * (p.alg_bpa / 32.0), s);
+        TimedLaunch tl(tm, "fused_tile", pass_bytes * (p.alg_bpa / 32.0), s, true);
+        const hipEvent_t ev0 = tl.start(), ev1 = tl.stop();  // null unless profiling
         bool framed = false;  // does any op of this pass run conjugated by the Pauli frame?
         if (frames)
             for (int k = p.stage_begin; k < p.stage_end && !framed; ++k)
@@ -1206,9 +1208,9 @@ void launch_fused(double2* st, int n, uint64_t batch, const Plan& plan, const Ti
             a.frames = frames;
             a.nbatch = (int)batch;
             switch (p.h) {
-                case 4: hipLaunchKernelGGL((k_fused_staged<4, true, true>), dim3((unsigned)blocks), dim3(256), 0, s, a); break;
-                case 5: hipLaunchKernelGGL((k_fused_staged<5, true, true>), dim3((unsigned)blocks), dim3(256), 0, s, a); break;
-                default: hipLaunchKernelGGL((k_fused_staged<6, true, true>), dim3((unsigned)blocks), dim3(256), 0, s, a); break;
+                case 4: hipExtLaunchKernelGGL((k_fused_staged<4, true, true>), dim3((unsigned)blocks), dim3(256), 0, s, ev0, ev1, 0, a); break;
+                case 5: hipExtLaunchKernelGGL((k_fused_staged<5, true, true>), dim3((unsigned)blocks), dim3(256), 0, s, ev0, ev1, 0, a); break;
+                default: hipExtLaunchKernelGGL((k_fused_staged<6, true, true>), dim3((unsigned)blocks), dim3(256), 0, s, ev0, ev1, 0, a); break;
             }
             QSIM_HIPCHK(hipGetLastError());
             continue;
@@ -1218,17 +1220,19 @@ void launch_fused(double2* st, int n, uint64_t batch, const Plan& plan, const Ti
             unsigned long long stride = a.stride, tpt = a.tpt_mask, zm = a.zmask, fv = a.fix_val;
             int lt_arg = lt;
             void* args[] = {&a.st, &stride, &tpt, &lt_arg, &zm, &fv};
-            QSIM_HIPCHK(hipModuleLaunchKernel(jm->fn[pi], (unsigned)blocks, 1, 1, 256, 1, 1, 0, s,
-                                              args, nullptr));
+            if (blocks * 256ull > 0xffffffffull) fail(QSIM_ERR_RUNTIME, "pass grid too large");
+            // grid in work-items; the events (if any) time the dispatch packet itself
+            QSIM_HIPCHK(hipExtModuleLaunchKernel(jm->fn[pi], (uint32_t)(blocks * 256), 1, 1, 256, 1, 1, 0, s,
+                                                 args, nullptr, ev0, ev1, 0));
             continue;
         }
         switch (p.h) {
 #define QSIM_TILE_CASE(HH) \
-    case HH: hipLaunchKernelGGL(k_fused_tile<HH>, dim3((unsigned)blocks), dim3(256), 0, s, a); break;
+    case HH: hipExtLaunchKernelGGL(k_fused_tile<HH>, dim3((unsigned)blocks), dim3(256), 0, s, ev0, ev1, 0, a); break;
 #define QSIM_STAGED_CASE(HH) \
     case HH:                                                                                      \
-        if (nt) hipLaunchKernelGGL((k_fused_staged<HH, true>), dim3((unsigned)blocks), dim3(256), 0, s, a); \
-        else hipLaunchKernelGGL((k_fused_staged<HH, false>), dim3((unsigned)blocks), dim3(256), 0, s, a); \
+        if (nt) hipExtLaunchKernelGGL((k_fused_staged<HH, true>), dim3((unsigned)blocks), dim3(256), 0, s, ev0, ev1, 0, a); \
+        else hipExtLaunchKernelGGL((k_fused_staged<HH, false>), dim3((unsigned)blocks), dim3(256), 0, s, ev0, ev1, 0, a); \
         break;
             QSIM_TILE_CASE(0)
             QSIM_TILE_CASE(1)

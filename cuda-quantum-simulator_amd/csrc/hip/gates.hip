@@ -18,6 +18,7 @@
 // Each lane keeps U wave-items in flight (8 outstanding 16-B loads) and a 256-thread block owns
 // 4*U consecutive wave-items.
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <algorithm>
 #include <cmath>
@@ -437,12 +438,15 @@ static const Tune& tune() {
 }
 
 template <typename K>
-static void go(K kernel, const GArgs& a, int U, hipStream_t s) {
+static void go(K kernel, const GArgs& a, int U, hipStream_t s, const TimedLaunch* tl = nullptr) {
     const uint64_t per_block = 4ull * U;
     const uint64_t blocks = (a.items + per_block - 1) / per_block;
     if (blocks == 0) return;
     if (blocks > 0x7fffffffull) fail(QSIM_ERR_RUNTIME, "grid too large");
-    hipLaunchKernelGGL(kernel, dim3((unsigned)blocks), dim3(256), 0, s, a);
+    if (tl && tl->start())  // profiled: the launch times itself (no marker packets)
+        hipExtLaunchKernelGGL(kernel, dim3((unsigned)blocks), dim3(256), 0, s, tl->start(), tl->stop(), 0, a);
+    else
+        hipLaunchKernelGGL(kernel, dim3((unsigned)blocks), dim3(256), 0, s, a);
     QSIM_HIPCHK(hipGetLastError());
 }
 
@@ -499,20 +503,20 @@ void launch_op(double2* st, int n, uint64_t batch, const Op& op, hipStream_t s, 
         }                                                                           \
     } while (0)
 #define QSIM_U248(KERNEL, NTV)                                                      \
-    if (u_ <= 1) go(KERNEL<1, NTV>, a, 1, s);                                       \
-    else if (u_ <= 2) go(KERNEL<2, NTV>, a, 2, s);                                  \
-    else if (u_ <= 4) go(KERNEL<4, NTV>, a, 4, s);                                  \
-    else go(KERNEL<8, NTV>, a, 8, s);
+    if (u_ <= 1) go(KERNEL<1, NTV>, a, 1, s, &tl);                                  \
+    else if (u_ <= 2) go(KERNEL<2, NTV>, a, 2, s, &tl);                             \
+    else if (u_ <= 4) go(KERNEL<4, NTV>, a, 4, s, &tl);                             \
+    else go(KERNEL<8, NTV>, a, 8, s, &tl);
     switch (op.kind) {
         case K_M1:
             if (op.t0 >= 6) {
                 add_fix(a, op.t0);
                 finish();
-                TimedLaunch tl(tm, "m1_slice", bytes, s);
+                TimedLaunch tl(tm, "m1_slice", bytes, s, true);
                 QSIM_GO_U(k_m1_slice, T.slice_u, QSIM_U248);
             } else {
                 finish();
-                TimedLaunch tl(tm, "m1_lane", bytes, s);
+                TimedLaunch tl(tm, "m1_lane", bytes, s, true);
                 QSIM_GO_U(k_m1_lane, T.lane_u, QSIM_U248);
             }
             break;
@@ -523,7 +527,7 @@ void launch_op(double2* st, int n, uint64_t batch, const Op& op, hipStream_t s, 
             }
             finish();
             {
-                TimedLaunch tl(tm, "diag", bytes, s);
+                TimedLaunch tl(tm, "diag", bytes, s, true);
                 QSIM_GO_U(k_diag, T.diag_u, QSIM_U248);
             }
             break;
@@ -532,17 +536,17 @@ void launch_op(double2* st, int n, uint64_t batch, const Op& op, hipStream_t s, 
                 add_fix(a, op.t0);
                 add_fix(a, op.t1);
                 finish();
-                TimedLaunch tl(tm, "swap_hh", bytes, s);
-                go(k_swap_hh<4>, a, 4, s);
+                TimedLaunch tl(tm, "swap_hh", bytes, s, true);
+                go(k_swap_hh<4>, a, 4, s, &tl);
             } else if (op.t1 >= 6) {
                 add_fix(a, op.t1);
                 finish();
-                TimedLaunch tl(tm, "swap_lh", bytes, s);
-                go(k_swap_lh<4>, a, 4, s);
+                TimedLaunch tl(tm, "swap_lh", bytes, s, true);
+                go(k_swap_lh<4>, a, 4, s, &tl);
             } else {
                 finish();
-                TimedLaunch tl(tm, "swap_ll", bytes, s);
-                go(k_swap_ll<8>, a, 8, s);
+                TimedLaunch tl(tm, "swap_ll", bytes, s, true);
+                go(k_swap_ll<8>, a, 8, s, &tl);
             }
             break;
         default: fail(QSIM_ERR_RUNTIME, "bad op kind");
