@@ -5,6 +5,8 @@
 // stream, src/Simulator.cu:95-97) and every readout synchronizes it (src/StateVector.cu:204-233).
 #include <hip/hip_runtime.h>
 
+#include <atomic>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <string>
@@ -184,6 +186,12 @@ struct qsim_state {
     Timer timer;
     int last_passes = 0, last_jit_passes = 0;  // of the last fused run (qsim_state_last_run)
     Scratch scratch;
+    // Layout-aware relabeling (relabel.hip): logical qubit q lives at physical position perm[q]
+    // (empty: identity).  basis: the amplitudes are the computational basis state basis_idx
+    // (physical index) — set by create / init, cleared by anything else that writes them.
+    std::vector<int> perm;
+    bool basis = true;
+    uint64_t basis_idx = 0;
     ~qsim_state() {
         if (stream) (void)hipStreamSynchronize(stream);
         if (d) (void)hipFree(d);
@@ -221,6 +229,61 @@ static void run_fused(qsim_state* s, const std::vector<Op>& ops) {
     s->last_jit_passes = 0;
     if (jm)
         for (hipFunction_t f : jm->fn) s->last_jit_passes += f != nullptr;
+}
+
+// Relabeling policy: QSIM_RELABEL (0 off, 1 on: default), QSIM_RELABEL_MIN_QUBITS (default 26:
+// the HBM-bound sizes the layout model was measured on); qsim_set_relabel overrides both.
+static std::atomic<int> g_relabel{-1}, g_relabel_min{-1};
+static bool relabel_enabled(int n) {
+    if (g_relabel.load() < 0) {
+        const char* e = std::getenv("QSIM_RELABEL");
+        g_relabel.store(e ? std::atoi(e) : 1);
+    }
+    if (g_relabel_min.load() < 0) {
+        const char* e = std::getenv("QSIM_RELABEL_MIN_QUBITS");
+        g_relabel_min.store(e ? std::atoi(e) : 26);
+    }
+    return g_relabel.load() != 0 && n >= g_relabel_min.load();
+}
+
+// Undo the relabeling: a fused network of physical SWAPs that brings logical qubit q back to
+// position q (exact data movement), then the identity map.  Every entry that reads or writes
+// amplitudes by index calls this first.
+static void canonicalize(qsim_state* s) {
+    if (s->perm.empty()) return;
+    const int n = s->n;
+    std::vector<int> p = s->perm, inv(n);
+    for (int q = 0; q < n; ++q) inv[p[q]] = q;
+    std::vector<Op> swaps;
+    for (int q = 0; q < n; ++q) {
+        if (p[q] == q) continue;
+        const int b = p[q], r = inv[q];  // logical q sits at b, logical r at position q
+        qsim_gate g{};
+        g.type = QSIM_GATE_SWAP;
+        g.nqubits = 2;
+        g.qubits[0] = q;
+        g.qubits[1] = b;
+        swaps.push_back(lower_gate(g, n));
+        swaps.back().src = (int)swaps.size() - 1;
+        p[r] = b;
+        inv[b] = r;
+        p[q] = q;
+        inv[q] = q;
+    }
+    s->perm.clear();
+    if (!swaps.empty()) run_fused(s, swaps);
+}
+// Before an entry that reads amplitudes by index (touch: and writes them).
+static void prep(qsim_state* s, bool touch) {
+    canonicalize(s);
+    if (touch) s->basis = false;
+}
+static qsim_gate map_gate(const qsim_state* s, const qsim_gate& g) {
+    qsim_gate m = g;
+    if (!s->perm.empty())
+        for (int j = 0; j < g.nqubits && j < 3; ++j)
+            if (g.qubits[j] >= 0 && g.qubits[j] < s->n) m.qubits[j] = s->perm[g.qubits[j]];
+    return m;
 }
 
 extern "C" {
@@ -316,6 +379,8 @@ int qsim_state_num_qubits(const qsim_state* s, int* n) {
 int qsim_state_device_ptr(qsim_state* s, void** dptr) {
     return guarded([&] {
         check_state(s);
+        DeviceGuard dg(s->device);
+        prep(s, true);  // the caller may read or write through the pointer
         *dptr = s->d;
     });
 }
@@ -333,6 +398,9 @@ int qsim_state_init_zero(qsim_state* s) {
         DeviceGuard g(s->device);
         launch_init_basis(s->d, s->n, 1, 0, s->stream);
         QSIM_HIPCHK(hipStreamSynchronize(s->stream));
+        s->perm.clear();
+        s->basis = true;
+        s->basis_idx = 0;
     });
 }
 
@@ -343,6 +411,9 @@ int qsim_state_init_basis(qsim_state* s, uint64_t idx) {
         DeviceGuard g(s->device);
         launch_init_basis(s->d, s->n, 1, idx, s->stream);
         QSIM_HIPCHK(hipStreamSynchronize(s->stream));
+        s->perm.clear();
+        s->basis = true;
+        s->basis_idx = idx;
     });
 }
 
@@ -358,7 +429,9 @@ int qsim_apply_gate(qsim_state* s, const qsim_gate* g) {
         check_state(s);
         QSIM_REQUIRE(g, QSIM_ERR_INVALID_ARGUMENT, "null gate");
         DeviceGuard dg(s->device);
-        const Op op = lower_gate(*g, s->n);
+        validate_gate(*g, s->n);
+        const Op op = lower_gate(map_gate(s, *g), s->n);
+        s->basis = false;
         launch_op(s->d, s->n, 1, op, s->stream, &s->timer);
     });
 }
@@ -368,12 +441,39 @@ int qsim_run(qsim_state* s, const qsim_gate* gates, size_t count, int flags) {
         check_state(s);
         QSIM_REQUIRE(gates || count == 0, QSIM_ERR_INVALID_ARGUMENT, "null gate list");
         DeviceGuard dg(s->device);
-        std::vector<Op> ops;
-        ops.reserve(count);
-        for (size_t i = 0; i < count; ++i) {
-            ops.push_back(lower_gate(gates[i], s->n));
-            ops.back().src = (int)i;
+        for (size_t i = 0; i < count; ++i) validate_gate(gates[i], s->n);
+        auto lower_all = [&]() {
+            std::vector<Op> ops;
+            ops.reserve(count);
+            for (size_t i = 0; i < count; ++i) {
+                ops.push_back(lower_gate(map_gate(s, gates[i]), s->n));
+                ops.back().src = (int)i;
+            }
+            return ops;
+        };
+        if ((flags & QSIM_RUN_FUSED) && s->basis && s->perm.empty() && count > 0 && relabel_enabled(s->n)) {
+            // First run on a basis state: choose the qubit labels for the plan's tile layouts.
+            const std::vector<Op> lops = lower_all();
+            const Plan& lp = s->plans.get(lops, s->n, s->stream).plan;
+            double before = 0.0, after = 0.0;
+            std::vector<int> pi = choose_relabel(plan_tiles(lp), s->n, &before, &after);
+            if (!pi.empty()) {
+                const size_t lpasses = lp.passes.size();
+                s->perm = pi;
+                const Plan& pp = s->plans.get(lower_all(), s->n, s->stream).plan;
+                // keep it only if the permuted circuit plans as well (the planner sees new labels)
+                if (pp.passes.size() > lpasses || plan_layout_cost_us(pp) > before * 0.97) {
+                    s->perm.clear();
+                } else if (s->basis_idx) {  // relabel the basis state itself
+                    uint64_t k = 0;
+                    for (int q = 0; q < s->n; ++q)
+                        if ((s->basis_idx >> q) & 1ull) k |= 1ull << pi[q];
+                    launch_init_basis(s->d, s->n, 1, k, s->stream);
+                }
+            }
         }
+        const std::vector<Op> ops = lower_all();
+        s->basis = false;
         if (flags & QSIM_RUN_FUSED) {
             run_fused(s, ops);
         } else {
@@ -403,6 +503,7 @@ int qsim_apply_matrix1q(qsim_state* s, int target, const double m[8], const int*
             op.cmask |= 1ull << c;
         }
         DeviceGuard dg(s->device);
+        prep(s, true);
         launch_op(s->d, s->n, 1, op, s->stream, &s->timer);
     });
 }
@@ -425,6 +526,7 @@ int qsim_apply_matrix2q(qsim_state* s, int q0, int q1, const double m[32], const
             cm |= 1ull << c;
         }
         DeviceGuard dg(s->device);
+        prep(s, true);
         launch_matrix2q(s->d, s->n, q0, q1, m, cm, s->stream, &s->timer);
     });
 }
@@ -452,6 +554,7 @@ int qsim_apply_matrix(qsim_state* s, const int* targets, int k, const double* m,
             cm |= 1ull << c;
         }
         DeviceGuard dg(s->device);
+        prep(s, true);
         const int dim = 1 << k;
         std::vector<double> mt(2 * (size_t)dim * dim);  // transpose: mt[c][r] = M[r][c]
         for (int r = 0; r < dim; ++r)
@@ -522,6 +625,7 @@ int qsim_apply_diagonal_layer(qsim_state* s, const double* gp, uint64_t active) 
             ops.push_back(o);
         }
         DeviceGuard dg(s->device);
+        prep(s, true);
         if (!ops.empty()) run_fused(s, ops);
     });
 }
@@ -569,6 +673,43 @@ int qsim_set_jit(int mode, int min_qubits) {
     return guarded([&] {
         if (mode > 2) fail(QSIM_ERR_INVALID_ARGUMENT, "jit mode must be 0 (off), 1 (background) or 2 (inline)");
         jit_configure(mode, min_qubits);
+    });
+}
+
+int qsim_set_relabel(int mode, int min_qubits) {
+    return guarded([&] {
+        if (mode > 1) fail(QSIM_ERR_INVALID_ARGUMENT, "relabel mode must be 0 (off) or 1 (on)");
+        relabel_enabled(0);  // read the environment defaults first
+        if (mode >= 0) g_relabel.store(mode);
+        if (min_qubits >= 0) g_relabel_min.store(min_qubits);
+    });
+}
+
+int qsim_state_perm(qsim_state* s, int32_t* perm) {
+    return guarded([&] {
+        check_state(s);
+        QSIM_REQUIRE(perm, QSIM_ERR_INVALID_ARGUMENT, "null perm");
+        for (int q = 0; q < s->n; ++q) perm[q] = s->perm.empty() ? q : s->perm[q];
+    });
+}
+
+int qsim_plan_relabel(int n_qubits, const qsim_gate* gates, size_t count, int32_t* perm,
+                      double* cost_before_us, double* cost_after_us) {
+    return guarded([&] {
+        QSIM_REQUIRE(gates || count == 0, QSIM_ERR_INVALID_ARGUMENT, "null gate list");
+        if (n_qubits < QSIM_MIN_QUBITS || n_qubits > 40) fail(QSIM_ERR_INVALID_ARGUMENT, "bad qubit count");
+        std::vector<Op> ops;
+        for (size_t i = 0; i < count; ++i) {
+            ops.push_back(lower_gate(gates[i], n_qubits));
+            ops.back().src = (int)i;
+        }
+        const Plan plan = plan_fused(ops, n_qubits);
+        double before = 0.0, after = 0.0;
+        const std::vector<int> pi = choose_relabel(plan_tiles(plan), n_qubits, &before, &after);
+        if (perm)
+            for (int q = 0; q < n_qubits; ++q) perm[q] = pi.empty() ? q : pi[q];
+        if (cost_before_us) *cost_before_us = before;
+        if (cost_after_us) *cost_after_us = after;
     });
 }
 
@@ -626,6 +767,7 @@ int qsim_state_to_host(qsim_state* s, double* dst) {
         check_state(s);
         QSIM_REQUIRE(dst, QSIM_ERR_INVALID_ARGUMENT, "null destination");
         DeviceGuard dg(s->device);
+        prep(s, false);
         QSIM_HIPCHK(hipMemcpyAsync(dst, s->d, sizeof(double2) << s->n, hipMemcpyDeviceToHost,
                                    s->stream));
         QSIM_HIPCHK(hipStreamSynchronize(s->stream));
@@ -637,6 +779,8 @@ int qsim_state_from_host(qsim_state* s, const double* src) {
         check_state(s);
         QSIM_REQUIRE(src, QSIM_ERR_INVALID_ARGUMENT, "null source");
         DeviceGuard dg(s->device);
+        s->perm.clear();  // overwritten in logical order
+        s->basis = false;
         QSIM_HIPCHK(hipMemcpyAsync(s->d, src, sizeof(double2) << s->n, hipMemcpyHostToDevice,
                                    s->stream));
         QSIM_HIPCHK(hipStreamSynchronize(s->stream));
@@ -648,6 +792,7 @@ int qsim_state_probabilities(qsim_state* s, double* dst) {
         check_state(s);
         QSIM_REQUIRE(dst, QSIM_ERR_INVALID_ARGUMENT, "null destination");
         DeviceGuard dg(s->device);
+        prep(s, false);
         const uint64_t N = 1ull << s->n;
         double* d_p = (double*)s->scratch.get(N * sizeof(double), s->stream);
         launch_probabilities(s->d, N, d_p, s->stream);
@@ -671,6 +816,7 @@ int qsim_state_prob_bit_zero(qsim_state* s, int bit, double* out) {
         QSIM_REQUIRE(out, QSIM_ERR_INVALID_ARGUMENT, "null out");
         if (bit < 0 || bit >= s->n) fail(QSIM_ERR_INVALID_ARGUMENT, "bit out of range");
         DeviceGuard dg(s->device);
+        prep(s, false);
         *out = reduce_norm(s->d, s->n, bit, s->d_partials, s->d_result, s->stream);
     });
 }
@@ -681,6 +827,7 @@ int qsim_state_collapse(qsim_state* s, int bit, int result, double scale) {
         if (bit < 0 || bit >= s->n) fail(QSIM_ERR_INVALID_ARGUMENT, "bit out of range");
         if (result != 0 && result != 1) fail(QSIM_ERR_INVALID_ARGUMENT, "result must be 0 or 1");
         DeviceGuard dg(s->device);
+        prep(s, true);
         launch_collapse(s->d, s->n, bit, result, scale, s->stream);
         QSIM_HIPCHK(hipStreamSynchronize(s->stream));
     });
@@ -692,6 +839,7 @@ int qsim_state_sample(qsim_state* s, const double* uniforms, int shots, int64_t*
         if (shots <= 0) fail(QSIM_ERR_INVALID_ARGUMENT, "n_shots must be positive");
         QSIM_REQUIRE(uniforms && out, QSIM_ERR_INVALID_ARGUMENT, "null buffer");
         DeviceGuard dg(s->device);
+        prep(s, false);
         sample_indices(s->d, s->n, 1, uniforms, shots, out, s->stream, s->scratch);
     });
 }
@@ -701,6 +849,7 @@ int qsim_noise_apply(qsim_state* s, int type, int qubit, double probability, uin
     return guarded([&] {
         check_state(s);
         DeviceGuard dg(s->device);
+        prep(s, true);
         launch_noise(s->d, s->n, type, qubit, probability, seed, counter, s->stream, &s->timer);
     });
 }
@@ -714,6 +863,7 @@ int qsim_noisy_run(qsim_state* s, const qsim_gate* gates, size_t count,
         QSIM_REQUIRE(channels || n_channels == 0, QSIM_ERR_INVALID_ARGUMENT, "null channel list");
         QSIM_REQUIRE(counter, QSIM_ERR_INVALID_ARGUMENT, "null counter");
         DeviceGuard dg(s->device);
+        prep(s, true);
         std::vector<Op> ops;
         for (size_t i = 0; i < count; ++i) {
             ops.push_back(lower_gate(gates[i], s->n));
@@ -753,6 +903,7 @@ int qsim_dm_run(qsim_state* s, int n, const qsim_gate* gates, size_t count,
         QSIM_REQUIRE(gates || count == 0, QSIM_ERR_INVALID_ARGUMENT, "null gate list");
         QSIM_REQUIRE(channels || n_channels == 0, QSIM_ERR_INVALID_ARGUMENT, "null channel list");
         DeviceGuard dg(s->device);
+        prep(s, true);
         std::vector<Op> ops;
         dm_lower(n, gates, count, channels, n_channels, ops);
         if (flags & QSIM_RUN_FUSED) run_fused(s, ops);
@@ -764,6 +915,7 @@ int qsim_dm_apply_channel(qsim_state* s, int n, int type, int qubit, double p) {
     return guarded([&] {
         check_dm(s, n);
         DeviceGuard dg(s->device);
+        prep(s, true);
         std::vector<Op> ops;
         dm_lower_channel(n, type, qubit, p, ops);
         for (const Op& op : ops) launch_op(s->d, s->n, 1, op, s->stream, &s->timer);
@@ -775,6 +927,7 @@ int qsim_dm_diagonal(qsim_state* s, int n, double* dst) {
         check_dm(s, n);
         QSIM_REQUIRE(dst, QSIM_ERR_INVALID_ARGUMENT, "null destination");
         DeviceGuard dg(s->device);
+        prep(s, false);
         double* d_p = (double*)s->scratch.get(sizeof(double) << n, s->stream);
         launch_dm_diag(s->d, n, d_p, s->stream);
         QSIM_HIPCHK(hipMemcpyAsync(dst, d_p, sizeof(double) << n, hipMemcpyDeviceToHost, s->stream));
@@ -787,6 +940,7 @@ int qsim_dm_init_pure(qsim_state* s, int n, const double* psi) {
         check_dm(s, n);
         QSIM_REQUIRE(psi, QSIM_ERR_INVALID_ARGUMENT, "null state");
         DeviceGuard dg(s->device);
+        prep(s, true);
         double2* d_psi = (double2*)s->scratch.get(sizeof(double2) << n, s->stream);
         QSIM_HIPCHK(hipMemcpyAsync(d_psi, psi, sizeof(double2) << n, hipMemcpyHostToDevice, s->stream));
         launch_dm_init(s->d, d_psi, n, s->stream);
@@ -798,6 +952,7 @@ int qsim_dm_init_maximally_mixed(qsim_state* s, int n) {
     return guarded([&] {
         check_dm(s, n);
         DeviceGuard dg(s->device);
+        prep(s, true);
         launch_dm_init(s->d, nullptr, n, s->stream);
         QSIM_HIPCHK(hipStreamSynchronize(s->stream));
     });

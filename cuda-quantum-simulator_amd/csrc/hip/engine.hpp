@@ -162,6 +162,14 @@ constexpr int kTileR0 = 6;    // contiguous run bits of a staged tile (QSIM_TILE
 // hmax < 0: the process default (kTileHMax, or QSIM_TILE_HMAX for tuning runs).
 // avoid: qubits no tile may contain (ops never act on them; only tile padding is affected).
 Plan plan_fused(const std::vector<Op>& ops, int n, int hmax = -1, uint64_t avoid = 0);
+// Layout-aware qubit relabeling (relabel.hip): predicted cost of a tile (qubit mask) in
+// microseconds, the tiles of a plan's staged passes, and the permutation (logical -> physical)
+// minimising the predicted cost of `tiles` (empty: keep the identity, < min_gain better).
+double layout_cost_us(uint64_t tile);
+std::vector<uint64_t> plan_tiles(const Plan& plan);
+double plan_layout_cost_us(const Plan& plan);
+std::vector<int> choose_relabel(const std::vector<uint64_t>& tiles, int n, double* before, double* after,
+                                double min_gain = 0.03);
 // Circuit-specialised pass kernels (jit.hip): hipRTC code object of one plan on one device.
 struct JitJob;
 struct JitModule {

@@ -47,3 +47,20 @@ def jit_build(circuit: Circuit) -> int:
     n = ctypes.c_size_t(0)
     _lib.check(_lib.hip.qsim_jit_build(circuit.getNumQubits(), arr, cnt, ctypes.byref(n)))
     return n.value
+
+
+def set_relabel(mode: int = -1, min_qubits: int = -1) -> None:
+    """Layout-aware qubit relabeling of fused runs (qsim_set_relabel): mode 0 off, 1 on; states
+    below `min_qubits` are never relabeled; negative arguments leave a setting unchanged."""
+    _lib.check(_lib.hip.qsim_set_relabel(mode, min_qubits))
+
+
+def plan_relabel(circuit: Circuit):
+    """(perm, predicted_us_before, predicted_us_after): the logical -> physical qubit map the
+    engine would choose for this circuit's fused plan (identity when none pays), host only."""
+    n = circuit.getNumQubits()
+    arr, cnt = circuit.to_abi()
+    perm = (ctypes.c_int32 * n)()
+    b, a = ctypes.c_double(), ctypes.c_double()
+    _lib.check(_lib.hip.qsim_plan_relabel(n, arr, cnt, perm, ctypes.byref(b), ctypes.byref(a)))
+    return list(perm), b.value, a.value

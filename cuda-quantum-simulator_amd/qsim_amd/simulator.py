@@ -224,6 +224,12 @@ class StateVector:
         arr, n = circuit.to_abi()
         _lib.check(_lib.hip.qsim_run(self._h, arr, n, int(mode)))
 
+    def perm(self):
+        """Current logical -> physical qubit map (identity unless a fused run relabeled)."""
+        p = (_c.c_int32 * self._n)()
+        _lib.check(_lib.hip.qsim_state_perm(self._h, p))
+        return list(p)
+
     # -- profiling
     def profile(self, enable: bool = True) -> None:
         _lib.check(_lib.hip.qsim_state_profile(self._h, 1 if enable else 0))

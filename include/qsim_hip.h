@@ -147,6 +147,20 @@ int qsim_set_jit(int mode, int min_qubits);
  * registers it with atexit; the library registers it after its first compile) so no compile runs
  * while the compiler's static state is destroyed; later background requests are refused. */
 int qsim_jit_shutdown(void);
+/* Layout-aware qubit relabeling (no reference counterpart; relabel.hip).  A fused pass's speed
+ * depends on the physical qubit positions its tile spans (the memory system's address mapping).
+ * On the first fused qsim_run of a state that holds a computational basis state (after create /
+ * init), the engine may choose a logical -> physical qubit permutation for the circuit's plan and
+ * keep running the state under it; every entry that reads or writes amplitudes by index first
+ * restores the identity layout with a fused SWAP network, so results are unchanged.  mode 0 off,
+ * 1 on (default, QSIM_RELABEL); states below min_qubits (default 26, QSIM_RELABEL_MIN_QUBITS)
+ * are never relabeled; negative arguments leave a setting unchanged. */
+int qsim_set_relabel(int mode, int min_qubits);
+int qsim_state_perm(qsim_state* s, int32_t* perm);  /* current logical -> physical map, n entries */
+/* Host-only: the permutation the engine would choose for this circuit (identity when none pays)
+ * and the predicted pass-layout cost (microseconds, summed over the plan's passes) before/after. */
+int qsim_plan_relabel(int n_qubits, const qsim_gate* gates, size_t count, int32_t* perm,
+                      double* cost_before_us, double* cost_after_us);
 /* Host-only: the generated source of a circuit's plan (len = its size; buf gets up to cap-1
  * bytes + NUL), and a hipRTC compile of it for gfx950 (code_bytes = code-object size). */
 int qsim_jit_source(int n_qubits, const qsim_gate* gates, size_t count, char* buf, size_t cap,
