@@ -116,8 +116,9 @@ def cpu_baseline(circuit, n, budget):
         pass
     return {"value": done / secs if secs > 0 else None, "unit": "gates/s", "cores": 1,
             "kind": "port",
-            "sample": f"first {done} gates of the same circuit at n={n}, single thread, "
-                      f"{secs:.1f} s ({cpu_model}; host has {os.cpu_count()} logical CPUs)"}
+            "sample": f"prefix-extrapolated: first {done} gates of the same circuit at n={n}, one "
+                      f"run, single thread, {secs:.1f} s ({cpu_model}; host has {os.cpu_count()} "
+                      f"logical CPUs); value = prefix gates / prefix time"}
 
 
 def run_single(args):
