@@ -231,21 +231,6 @@ static void run_fused(qsim_state* s, const std::vector<Op>& ops) {
         for (hipFunction_t f : jm->fn) s->last_jit_passes += f != nullptr;
 }
 
-// Relabeling policy: QSIM_RELABEL (0 off, 1 on: default), QSIM_RELABEL_MIN_QUBITS (default 26:
-// the HBM-bound sizes the layout model was measured on); qsim_set_relabel overrides both.
-static std::atomic<int> g_relabel{-1}, g_relabel_min{-1};
-static bool relabel_enabled(int n) {
-    if (g_relabel.load() < 0) {
-        const char* e = std::getenv("QSIM_RELABEL");
-        g_relabel.store(e ? std::atoi(e) : 1);
-    }
-    if (g_relabel_min.load() < 0) {
-        const char* e = std::getenv("QSIM_RELABEL_MIN_QUBITS");
-        g_relabel_min.store(e ? std::atoi(e) : 26);
-    }
-    return g_relabel.load() != 0 && n >= g_relabel_min.load();
-}
-
 // Undo the relabeling: a fused network of physical SWAPs that brings logical qubit q back to
 // position q (exact data movement), then the identity map.  Every entry that reads or writes
 // amplitudes by index calls this first.
@@ -679,9 +664,7 @@ int qsim_set_jit(int mode, int min_qubits) {
 int qsim_set_relabel(int mode, int min_qubits) {
     return guarded([&] {
         if (mode > 1) fail(QSIM_ERR_INVALID_ARGUMENT, "relabel mode must be 0 (off) or 1 (on)");
-        relabel_enabled(0);  // read the environment defaults first
-        if (mode >= 0) g_relabel.store(mode);
-        if (min_qubits >= 0) g_relabel_min.store(min_qubits);
+        relabel_configure(mode, min_qubits);
     });
 }
 

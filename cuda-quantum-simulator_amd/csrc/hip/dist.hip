@@ -417,6 +417,7 @@ struct qsim_dist {
     int overlapped = 0;                 // remaps of the last run that overlapped local work
     ncclComm_t comm = nullptr;
     bool aborted = false;  // the communicator was aborted after an RCCL / HIP error or a timeout
+    bool fresh = true;     // |0..0> with the identity map (create / reset): local labels are free
     std::vector<int> perm;
     DevBuf ops, stages;
     // Plans of recent runs, keyed by (gate list, map at the start of the run): a repeated circuit
@@ -572,6 +573,7 @@ void alloc_shards(qsim_dist* d, const std::vector<int>& ranks) {
 }
 void init_zero(qsim_dist* d) {
     for (int q = 0; q < d->n; ++q) d->perm[q] = q;
+    d->fresh = true;
     for (Shard& s : d->shards) launch_init_basis(s.d, d->L, 1, s.rank == 0 ? 0 : ~0ull, d->stream);
     QSIM_HIPCHK(hipStreamSynchronize(d->stream));
 }
@@ -964,6 +966,24 @@ int qsim_dist_run(qsim_dist* d, const qsim_gate* gates, size_t count, int flags)
         need(d);
         if (!gates && count) fail(QSIM_ERR_INVALID_ARGUMENT, "null gate list");
         QSIM_HIPCHK(hipSetDevice(d->device));
+        if ((flags & QSIM_RUN_FUSED) && d->fresh && count > 0 && relabel_enabled(d->L)) {
+            // Layout-aware relabeling of the LOCAL positions (relabel.hip): |0..0> stays |0..0>
+            // under any relabeling, so the map is free to choose now.  Decided from rank 0's plan,
+            // which every rank can compute, so all ranks pick the same map (the exchanges need
+            // identical positions everywhere).  Global positions are untouched.
+            std::vector<int> p0 = d->perm;
+            const std::vector<DStep> st0 = plan_dist(gates, count, d->n, d->g, 0, p0);
+            std::vector<uint64_t> tiles;
+            for (const DStep& st : st0)
+                if (st.kind == 0 && !st.ops.empty())
+                    for (uint64_t t : plan_tiles(plan_fused(st.ops, d->L))) tiles.push_back(t);
+            double before = 0.0, after = 0.0;
+            const std::vector<int> pi = choose_relabel(tiles, d->L, &before, &after);
+            if (!pi.empty())
+                for (int q = 0; q < d->n; ++q)
+                    if (d->perm[q] < d->L) d->perm[q] = pi[d->perm[q]];
+        }
+        d->fresh = false;
         qsim_dist::RunPlan& rp = run_plan(d, gates, count);
         const auto& plans = rp.steps;
         const size_t S = d->shards.size();

@@ -165,6 +165,8 @@ Plan plan_fused(const std::vector<Op>& ops, int n, int hmax = -1, uint64_t avoid
 // Layout-aware qubit relabeling (relabel.hip): predicted cost of a tile (qubit mask) in
 // microseconds, the tiles of a plan's staged passes, and the permutation (logical -> physical)
 // minimising the predicted cost of `tiles` (empty: keep the identity, < min_gain better).
+bool relabel_enabled(int n);                        // policy (QSIM_RELABEL*, qsim_set_relabel)
+void relabel_configure(int mode, int min_qubits);   // < 0 leaves a setting unchanged
 double layout_cost_us(uint64_t tile);
 std::vector<uint64_t> plan_tiles(const Plan& plan);
 double plan_layout_cost_us(const Plan& plan);

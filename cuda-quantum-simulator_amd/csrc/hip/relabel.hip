@@ -12,6 +12,7 @@
 // amplitudes by index (capi.hip: canonicalize) — so results are exactly those of the
 // unpermuted run up to the SWAPs' data movement (which is exact).
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdlib>
 #include <random>
@@ -21,6 +22,30 @@
 #include "layout_cost.hpp"
 
 namespace qsim_hip {
+
+// Policy: QSIM_RELABEL (0 off, 1 on: default), QSIM_RELABEL_MIN_QUBITS (default 26: the HBM-bound
+// sizes the layout model was measured on; for the sharded engine the LOCAL qubit count);
+// qsim_set_relabel overrides both.
+static std::atomic<int> g_relabel{-1}, g_relabel_min{-1};
+static void relabel_defaults() {
+    if (g_relabel.load() < 0) {
+        const char* e = std::getenv("QSIM_RELABEL");
+        g_relabel.store(e ? std::atoi(e) : 1);
+    }
+    if (g_relabel_min.load() < 0) {
+        const char* e = std::getenv("QSIM_RELABEL_MIN_QUBITS");
+        g_relabel_min.store(e ? std::atoi(e) : 26);
+    }
+}
+bool relabel_enabled(int n) {
+    relabel_defaults();
+    return g_relabel.load() != 0 && n >= g_relabel_min.load();
+}
+void relabel_configure(int mode, int min_qubits) {
+    relabel_defaults();
+    if (mode >= 0) g_relabel.store(mode);
+    if (min_qubits >= 0) g_relabel_min.store(min_qubits);
+}
 
 double layout_cost_us(uint64_t tile) {
     using namespace layout_cost;
