@@ -32,7 +32,7 @@ def relabeled(c, n, pi):
     return c1
 
 seen = set()
-for n, seeds in ((30, (42, 1, 2, 3, 4)), (28, (42, 1))):
+for n, seeds in ((30, (42, 1, 2, 3, 4)), (28, (42, 1, 2, 3)), (27, (42, 5))):
     for s in seeds:
         c = q.createRandomHCCircuit(n, 100, s)
         ltiles = tiles_of(c)
