@@ -251,6 +251,10 @@ struct qsim_batch {
     Timer timer;
     Scratch scratch, scratch2;
     int last_passes = 0, last_jit_passes = 0;
+    // Layout-aware relabeling (relabel.hip) of the qubits inside every trajectory: logical q at
+    // physical perm[q] (empty: identity); basis: every trajectory is |0..0> (create / reset).
+    std::vector<int> perm;
+    bool basis = true;
     ~qsim_batch() {
         if (stream) (void)hipStreamSynchronize(stream);
         if (d) (void)hipFree(d);
@@ -279,6 +283,44 @@ int bguard(F&& f) {
 }
 void need(const qsim_batch* b) {
     if (!b) fail(QSIM_ERR_INVALID_ARGUMENT, "null batch handle");
+}
+qsim_gate map_gate(const qsim_batch* b, const qsim_gate& g) {
+    qsim_gate m = g;
+    if (!b->perm.empty())
+        for (int j = 0; j < g.nqubits && j < 3; ++j)
+            if (g.qubits[j] >= 0 && g.qubits[j] < b->n) m.qubits[j] = b->perm[g.qubits[j]];
+    return m;
+}
+// Undo the relabeling in every trajectory (fused SWAP network over the batch, exact data
+// movement) before anything reads or writes amplitudes by index.
+void canonicalize(qsim_batch* b) {
+    if (b->perm.empty()) return;
+    const int n = b->n;
+    std::vector<int> p = b->perm, inv(n);
+    for (int q = 0; q < n; ++q) inv[p[q]] = q;
+    std::vector<Op> swaps;
+    for (int q = 0; q < n; ++q) {
+        if (p[q] == q) continue;
+        const int at = p[q], r = inv[q];
+        qsim_gate g{};
+        g.type = QSIM_GATE_SWAP;
+        g.nqubits = 2;
+        g.qubits[0] = q;
+        g.qubits[1] = at;
+        swaps.push_back(lower_gate(g, n));
+        swaps.back().src = -1;
+        p[r] = at;
+        inv[at] = r;
+        p[q] = q;
+        inv[q] = q;
+    }
+    b->perm.clear();
+    if (swaps.empty()) return;
+    PlanCache::Entry& pe = b->plans.get(swaps, n, b->stream);
+    b->ops.upload(pe.plan.ops.data(), pe.plan.ops.size() * sizeof(TileOp), b->stream);
+    b->stages.upload(pe.plan.stages.data(), pe.plan.stages.size() * sizeof(Stage), b->stream);
+    launch_fused(b->d, n, (uint64_t)b->batch, pe.plan, (const TileOp*)b->ops.ptr, (const Stage*)b->stages.ptr,
+                 b->stream, &b->timer);
 }
 }  // namespace
 
@@ -316,6 +358,8 @@ int qsim_batch_reset(qsim_batch* b) {
         need(b);
         launch_init_basis(b->d, b->n, b->batch, 0, b->stream);
         QSIM_HIPCHK(hipStreamSynchronize(b->stream));
+        b->perm.clear();
+        b->basis = true;
     });
 }
 
@@ -348,6 +392,38 @@ int qsim_batch_run(qsim_batch* b, const qsim_gate* gates, size_t count,
             if (c.type == 0 || c.type == 3 || c.type == 4 || c.type == 5)
                 ch.push_back(DevChannel{c.type, c.qubit, c.probability});
         }
+        for (size_t i = 0; i < count; ++i) validate_gate(gates[i], b->n);
+        static const bool fused_env = [] {
+            const char* e = std::getenv("QSIM_BATCH_FUSED");
+            return e == nullptr || std::atoi(e) != 0;
+        }();
+        const bool fused_path = b->n >= 10 && fused_env && !(flags & QSIM_BATCH_PER_GATE) &&
+                                !(flags & QSIM_BATCH_REFERENCE_NOISE);
+        if (flags & QSIM_BATCH_REFERENCE_NOISE) canonicalize(b);  // per-pair draws name positions
+        if (fused_path && b->basis && b->perm.empty() && count > 0) {
+            // First fused run of |0..0> trajectories: relabel for the plan's tile layouts when
+            // the whole batch is HBM-sized (as the JIT threshold, it counts every trajectory).
+            int eff = b->n;
+            while ((1ll << (eff - b->n)) < (long long)b->batch) ++eff;
+            if (relabel_enabled(eff)) {
+                std::vector<Op> lops;
+                for (size_t i = 0; i < count; ++i) {
+                    const qsim_gate& g = gates[i];
+                    if ((flags & QSIM_BATCH_REFERENCE_GATESET) && !(g.type <= QSIM_GATE_H || g.type == QSIM_GATE_CNOT))
+                        continue;
+                    lops.push_back(lower_gate(g, b->n));
+                    lops.back().src = -1;
+                }
+                if (!lops.empty()) {
+                    const Plan lp = plan_fused(lops, b->n);
+                    double before = 0.0, after = 0.0;
+                    b->perm = choose_relabel(plan_tiles(lp), b->n, &before, &after);
+                }
+            }
+        }
+        b->basis = false;
+        for (DevChannel& c : ch)
+            if (!b->perm.empty()) c.qubit = b->perm[c.qubit];
         if (ch.size() > b->ch_cap) {
             if (b->d_ch) {
                 QSIM_HIPCHK(hipStreamSynchronize(b->stream));
@@ -361,7 +437,7 @@ int qsim_batch_run(qsim_batch* b, const qsim_gate* gates, size_t count,
                                        hipMemcpyHostToDevice, b->stream));
         std::vector<Op> ops;
         for (size_t i = 0; i < count; ++i) {
-            const qsim_gate& g = gates[i];
+            const qsim_gate g = map_gate(b, gates[i]);
             if (flags & QSIM_BATCH_REFERENCE_GATESET) {
                 // src/NoiseModel.cu:742-763, 808-812, 821-825: only X/Y/Z/H and CNOT act.
                 const bool ok = g.type <= QSIM_GATE_H || g.type == QSIM_GATE_CNOT;
@@ -391,10 +467,6 @@ int qsim_batch_run(qsim_batch* b, const qsim_gate* gates, size_t count,
             }
             return;
         }
-        static const bool fused_env = [] {
-            const char* e = std::getenv("QSIM_BATCH_FUSED");
-            return e == nullptr || std::atoi(e) != 0;
-        }();
         if (b->n >= 10 && fused_env && !(flags & QSIM_BATCH_PER_GATE)) {
             // Fused tile passes over all trajectories (a tile never straddles two).  Noise is
             // carried as per-trajectory Pauli frames: no noise kernel per gate, one frame build
@@ -404,7 +476,7 @@ int qsim_batch_run(qsim_batch* b, const qsim_gate* gates, size_t count,
             std::vector<StepClifford> cl(count, StepClifford{CL_NONE, 0, -1, 0});
             for (size_t i = 0; i < ops.size(); ++i) {
                 if (ops[i].kind < 0) continue;  // ignored by the reference gate set
-                const qsim_gate& g = gates[i];
+                const qsim_gate g = map_gate(b, gates[i]);
                 static const int code_of[QSIM_GATE_COUNT] = {
                     CL_X, CL_Y, CL_Z, CL_H, CL_S, CL_NONE /*T*/, CL_SDG, CL_NONE /*Tdag*/,
                     CL_NONE, CL_NONE, CL_NONE /*Rx Ry Rz*/, CL_CNOT, CL_CZ, CL_NONE, CL_NONE /*CRY CRZ*/,
@@ -490,6 +562,7 @@ int qsim_batch_run(qsim_batch* b, const qsim_gate* gates, size_t count,
 int qsim_batch_avg_probabilities(qsim_batch* b, double* dst) {
     return bguard([&] {
         need(b);
+        canonicalize(b);
         const uint64_t N = 1ull << b->n;
         double* d_p = (double*)b->scratch.get(N * sizeof(double), b->stream);
         launch_avg_probabilities(b->d, b->n, (uint64_t)b->batch, d_p, b->stream);
@@ -501,6 +574,7 @@ int qsim_batch_avg_probabilities(qsim_batch* b, double* dst) {
 int qsim_batch_traj_probabilities(qsim_batch* b, int traj, double* dst) {
     return bguard([&] {
         need(b);
+        canonicalize(b);
         if (traj < 0 || traj >= b->batch) fail(QSIM_ERR_OUT_OF_RANGE, "Invalid trajectory index");
         const uint64_t N = 1ull << b->n;
         double* d_p = (double*)b->scratch.get(N * sizeof(double), b->stream);
@@ -513,6 +587,7 @@ int qsim_batch_traj_probabilities(qsim_batch* b, int traj, double* dst) {
 int qsim_batch_sample(qsim_batch* b, const double* uniforms, int shots, int64_t* out) {
     return bguard([&] {
         need(b);
+        canonicalize(b);
         if (shots < 0) fail(QSIM_ERR_INVALID_ARGUMENT, "n_shots must be non-negative");
         if (shots > 0 && (!uniforms || !out)) fail(QSIM_ERR_INVALID_ARGUMENT, "null buffer");
         sample_indices(b->d, b->n, (uint64_t)b->batch, uniforms, shots, out, b->stream, b->scratch);
@@ -522,6 +597,7 @@ int qsim_batch_sample(qsim_batch* b, const double* uniforms, int shots, int64_t*
 int qsim_batch_histogram(qsim_batch* b, const double* uniforms, int shots, int64_t* hist) {
     return bguard([&] {
         need(b);
+        canonicalize(b);
         if (shots < 0) fail(QSIM_ERR_INVALID_ARGUMENT, "n_shots must be non-negative");
         if (!hist || (shots > 0 && !uniforms)) fail(QSIM_ERR_INVALID_ARGUMENT, "null buffer");
         const uint64_t N = 1ull << b->n, nshots = (uint64_t)shots * (uint64_t)b->batch;
@@ -546,6 +622,7 @@ int qsim_batch_histogram(qsim_batch* b, const double* uniforms, int shots, int64
 int qsim_batch_traj_state(qsim_batch* b, int traj, double* dst) {
     return bguard([&] {
         need(b);
+        canonicalize(b);
         if (traj < 0 || traj >= b->batch) fail(QSIM_ERR_OUT_OF_RANGE, "Invalid trajectory index");
         const uint64_t N = 1ull << b->n;
         QSIM_HIPCHK(hipMemcpyAsync(dst, b->d + (uint64_t)traj * N, N * sizeof(double2),
@@ -557,6 +634,8 @@ int qsim_batch_traj_state(qsim_batch* b, int traj, double* dst) {
 int qsim_batch_device_ptr(qsim_batch* b, void** dptr) {
     return bguard([&] {
         need(b);
+        canonicalize(b);
+        b->basis = false;  // the caller may write through the pointer
         *dptr = b->d;
     });
 }

@@ -189,3 +189,34 @@ def test_trajectory_shards_reproduce_the_ensemble(qsim, gpu_ready, noise, per_ga
     np.testing.assert_allclose(avg, full.getAverageProbabilities(), atol=1e-14, rtol=0)
     # the draws really differ between trajectories (the offset is not a no-op)
     assert any(np.max(np.abs(full.getStateVector(0) - full.getStateVector(t))) > 1e-6 for t in range(1, B))
+
+
+@pytest.mark.parametrize("n,B", [(12, 16), (14, 8)])
+def test_relabeled_batch_equals_per_gate(qsim, gpu_ready, n, B):
+    """Layout-aware relabeling of the trajectories' qubits (first fused run of |0..0>, threshold
+    lowered here): noise draws are keyed by channel index, so the relabeled fused run holds the
+    same trajectories as the per-gate run (which never relabels), through two runs, every
+    trajectory readout and the ensemble average."""
+    from qsim_amd.plan import set_relabel
+    c = _mixed(qsim, n, 60, 4)
+    nm = _noise(qsim, n)
+    set_relabel(1, 14)
+    try:
+        fused, ref = qsim.BatchedSimulator(n, B, nm), qsim.BatchedSimulator(n, B, nm)
+        fused.setSeed(8)
+        ref.setSeed(8)
+        for _ in range(2):
+            fused.run(c)
+            ref.run(c, per_gate=True)
+        np.testing.assert_allclose(fused.getAverageProbabilities(), ref.getAverageProbabilities(),
+                                   atol=1e-12, rtol=0)
+        for t in range(B):
+            np.testing.assert_allclose(fused.getStateVector(t), ref.getStateVector(t), atol=1e-12, rtol=0)
+        fused.reset()
+        ref.reset()
+        fused.run(c)  # relabels again from |0..0>
+        ref.run(c, per_gate=True)
+        u = np.random.default_rng(1).random((B, 64))
+        np.testing.assert_array_equal(fused.sampleWith(u), ref.sampleWith(u))
+    finally:
+        set_relabel(1, 26)
