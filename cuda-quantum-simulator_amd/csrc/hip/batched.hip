@@ -406,19 +406,20 @@ int qsim_batch_run(qsim_batch* b, const qsim_gate* gates, size_t count,
             int eff = b->n;
             while ((1ll << (eff - b->n)) < (long long)b->batch) ++eff;
             if (relabel_enabled(eff)) {
-                std::vector<Op> lops;
-                for (size_t i = 0; i < count; ++i) {
-                    const qsim_gate& g = gates[i];
-                    if ((flags & QSIM_BATCH_REFERENCE_GATESET) && !(g.type <= QSIM_GATE_H || g.type == QSIM_GATE_CNOT))
-                        continue;
-                    lops.push_back(lower_gate(g, b->n));
-                    lops.back().src = -1;
-                }
-                if (!lops.empty()) {
-                    const Plan lp = plan_fused(lops, b->n);
-                    double before = 0.0, after = 0.0;
-                    b->perm = choose_relabel(plan_tiles(lp), b->n, &before, &after);
-                }
+                auto lower_under = [&](const std::vector<int>& pi) {
+                    std::vector<Op> lops;
+                    for (size_t i = 0; i < count; ++i) {
+                        qsim_gate g = gates[i];
+                        if ((flags & QSIM_BATCH_REFERENCE_GATESET) &&
+                            !(g.type <= QSIM_GATE_H || g.type == QSIM_GATE_CNOT))
+                            continue;
+                        for (int j = 0; j < g.nqubits && j < 3; ++j) g.qubits[j] = pi[g.qubits[j]];
+                        lops.push_back(lower_gate(g, b->n));
+                        lops.back().src = -1;
+                    }
+                    return lops;
+                };
+                b->perm = choose_layout(b->n, lower_under, relabel_tries()).perm;
             }
         }
         b->basis = false;

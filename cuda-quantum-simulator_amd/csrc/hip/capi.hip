@@ -437,22 +437,27 @@ int qsim_run(qsim_state* s, const qsim_gate* gates, size_t count, int flags) {
             return ops;
         };
         if ((flags & QSIM_RUN_FUSED) && s->basis && s->perm.empty() && count > 0 && relabel_enabled(s->n)) {
-            // First run on a basis state: choose the qubit labels for the plan's tile layouts.
-            const std::vector<Op> lops = lower_all();
-            const Plan& lp = s->plans.get(lops, s->n, s->stream).plan;
-            double before = 0.0, after = 0.0;
-            std::vector<int> pi = choose_relabel(plan_tiles(lp), s->n, &before, &after);
-            if (!pi.empty()) {
-                const size_t lpasses = lp.passes.size();
-                s->perm = pi;
-                const Plan& pp = s->plans.get(lower_all(), s->n, s->stream).plan;
-                // keep it only if the permuted circuit plans as well (the planner sees new labels)
-                if (pp.passes.size() > lpasses || plan_layout_cost_us(pp) > before * 0.97) {
-                    s->perm.clear();
-                } else if (s->basis_idx) {  // relabel the basis state itself
+            // First run on a basis state: choose the qubit labels for fewer passes and faster
+            // pass layouts (relabel.hip: choose_layout).
+            auto lower_under = [&](const std::vector<int>& pi) {
+                std::vector<Op> ops;
+                ops.reserve(count);
+                for (size_t i = 0; i < count; ++i) {
+                    qsim_gate m = gates[i];
+                    for (int j = 0; j < m.nqubits && j < 3; ++j) m.qubits[j] = pi[m.qubits[j]];
+                    ops.push_back(lower_gate(m, s->n));
+                    ops.back().src = (int)i;
+                }
+                return ops;
+            };
+            LayoutChoice lc = choose_layout(s->n, lower_under, relabel_tries());
+            if (!lc.perm.empty()) {
+                s->perm = lc.perm;
+                s->plans.put(std::move(lc.ops), s->n, std::move(lc.plan), s->stream);
+                if (s->basis_idx) {  // relabel the basis state itself
                     uint64_t k = 0;
                     for (int q = 0; q < s->n; ++q)
-                        if ((s->basis_idx >> q) & 1ull) k |= 1ull << pi[q];
+                        if ((s->basis_idx >> q) & 1ull) k |= 1ull << s->perm[q];
                     launch_init_basis(s->d, s->n, 1, k, s->stream);
                 }
             }
@@ -681,18 +686,22 @@ int qsim_plan_relabel(int n_qubits, const qsim_gate* gates, size_t count, int32_
     return guarded([&] {
         QSIM_REQUIRE(gates || count == 0, QSIM_ERR_INVALID_ARGUMENT, "null gate list");
         if (n_qubits < QSIM_MIN_QUBITS || n_qubits > 40) fail(QSIM_ERR_INVALID_ARGUMENT, "bad qubit count");
-        std::vector<Op> ops;
-        for (size_t i = 0; i < count; ++i) {
-            ops.push_back(lower_gate(gates[i], n_qubits));
-            ops.back().src = (int)i;
-        }
-        const Plan plan = plan_fused(ops, n_qubits);
-        double before = 0.0, after = 0.0;
-        const std::vector<int> pi = choose_relabel(plan_tiles(plan), n_qubits, &before, &after);
+        for (size_t i = 0; i < count; ++i) validate_gate(gates[i], n_qubits);
+        auto lower_under = [&](const std::vector<int>& pi) {
+            std::vector<Op> ops;
+            for (size_t i = 0; i < count; ++i) {
+                qsim_gate m = gates[i];
+                for (int j = 0; j < m.nqubits && j < 3; ++j) m.qubits[j] = pi[m.qubits[j]];
+                ops.push_back(lower_gate(m, n_qubits));
+                ops.back().src = (int)i;
+            }
+            return ops;
+        };
+        const LayoutChoice lc = choose_layout(n_qubits, lower_under, relabel_tries());
         if (perm)
-            for (int q = 0; q < n_qubits; ++q) perm[q] = pi.empty() ? q : pi[q];
-        if (cost_before_us) *cost_before_us = before;
-        if (cost_after_us) *cost_after_us = after;
+            for (int q = 0; q < n_qubits; ++q) perm[q] = lc.perm.empty() ? q : lc.perm[q];
+        if (cost_before_us) *cost_before_us = lc.cost_before;
+        if (cost_after_us) *cost_after_us = lc.cost_after;
     });
 }
 

@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <functional>
 #include <memory>
 #include <stdexcept>
 #include <string>
@@ -172,6 +173,19 @@ std::vector<uint64_t> plan_tiles(const Plan& plan);
 double plan_layout_cost_us(const Plan& plan);
 std::vector<int> choose_relabel(const std::vector<uint64_t>& tiles, int n, double* before, double* after,
                                 double min_gain = 0.03);
+// The layout for a whole circuit: labels chosen for fewer passes first, then the cheapest pass
+// layouts (relabel.hip).  perm empty: keep the identity.  ops / plan: the circuit under perm as
+// the caller's `lower` produced it, and its plan (for the caller's plan cache).
+struct LayoutChoice {
+    std::vector<int> perm;
+    std::vector<Op> ops;
+    Plan plan;
+    size_t passes_before = 0;
+    double cost_before = 0.0, cost_after = 0.0;
+};
+LayoutChoice choose_layout(int n, const std::function<std::vector<Op>(const std::vector<int>&)>& lower,
+                           int tries);
+int relabel_tries();  // QSIM_RELABEL_TRIES (default 7): random labelings planned per choice
 // Circuit-specialised pass kernels (jit.hip): hipRTC code object of one plan on one device.
 struct JitJob;
 struct JitModule {
@@ -210,6 +224,8 @@ struct PlanCache {
     uint64_t clock = 0;
     // stream: where the owner runs this cache's plans (drained before a plan is evicted)
     Entry& get(const std::vector<Op>& ops, int n_qubits, hipStream_t stream, uint64_t avoid = 0);
+    // insert a plan computed elsewhere under `ops` (relabeling plans its candidates itself)
+    void put(std::vector<Op> ops, int n_qubits, Plan plan, hipStream_t stream);
 };
 // Which part of a plan to launch: passes [first, last) over the sub-space whose qubits in
 // fix_mask read fix_val (fix_mask = 0: the whole state).  Sub-space launches need staged passes.

@@ -582,6 +582,21 @@ PlanCache::Entry& PlanCache::get(const std::vector<Op>& ops, int n_qubits, hipSt
     return *entries.back();
 }
 
+void PlanCache::put(std::vector<Op> ops, int n_qubits, Plan plan, hipStream_t stream) {
+    if (entries.size() >= kEntries) {
+        auto lru = std::min_element(entries.begin(), entries.end(),
+                                    [](const auto& a, const auto& b) { return a->used < b->used; });
+        if ((*lru)->jit.mod) QSIM_HIPCHK(hipStreamSynchronize(stream));
+        entries.erase(lru);
+    }
+    auto e = std::make_unique<Entry>();
+    e->plan = std::move(plan);
+    e->key = std::move(ops);
+    e->n = n_qubits;
+    e->used = ++clock;
+    entries.push_back(std::move(e));
+}
+
 static int env_int(const char* k, int d) {
     const char* e = std::getenv(k);
     return e ? std::atoi(e) : d;

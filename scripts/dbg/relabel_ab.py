@@ -7,7 +7,7 @@ sys.path.insert(0, os.path.join(ROOT, "cuda-quantum-simulator_amd"))
 import qsim_amd as q
 from qsim_amd.plan import set_jit
 set_jit(2, -1)
-n = 30
+n = int(os.environ.get("N", "30"))
 c0 = q.createRandomHCCircuit(n, 100, int(os.environ.get("SEED", "42")))
 circs = {"identity": c0}
 for f in sys.argv[1:]:

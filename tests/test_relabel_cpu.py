@@ -13,15 +13,33 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
+def _relabeled(qsim, c, perm):
+    n = c.getNumQubits()
+    c1 = qsim.Circuit(n)
+    for g in c.getGates():
+        c1.append(qsim.GateOp(g.type, [perm[x] for x in g.qubits], g.parameter))
+    return c1
+
+
 @pytest.mark.parametrize("n,seed", [(26, 42), (28, 42), (30, 42), (30, 7)])
 def test_plan_relabel_is_a_valid_improving_permutation(qsim, n, seed):
-    from qsim_amd.plan import plan_relabel
-    perm, before, after = plan_relabel(qsim.createRandomHCCircuit(n, 100, seed))
+    from qsim_amd.plan import plan_fused, plan_relabel
+    c = qsim.createRandomHCCircuit(n, 100, seed)
+    perm, before, after = plan_relabel(c)
     assert sorted(perm) == list(range(n))
-    assert perm[:4] == [0, 1, 2, 3]
-    assert 0 < after <= before
-    again = plan_relabel(qsim.createRandomHCCircuit(n, 100, seed))
-    assert again[0] == perm  # deterministic (fixed annealing seeds)
+    passes0, passes1 = plan_fused(c)[2], plan_fused(_relabeled(qsim, c, perm))[2]
+    # never more passes; as many passes only with a cheaper predicted layout
+    assert passes1 < passes0 or (passes1 == passes0 and (after < before or perm == list(range(n))))
+    again = plan_relabel(c)
+    assert again[0] == perm  # deterministic (fixed seeds)
+
+
+def test_relabel_finds_fewer_passes_at_28_qubits(qsim):
+    """W-HC 28q plans into 6 passes as labelled and into 5 under the chosen labels."""
+    from qsim_amd.plan import plan_fused, plan_relabel
+    c = qsim.createRandomHCCircuit(28, 100, 42)
+    perm, _, _ = plan_relabel(c)
+    assert plan_fused(c)[2] == 6 and plan_fused(_relabeled(qsim, c, perm))[2] == 5
 
 
 def test_small_circuit_keeps_identity(qsim):
