@@ -14,6 +14,7 @@
 #include <algorithm>
 #include <atomic>
 #include <cmath>
+#include <cstdint>
 #include <cstdlib>
 #include <functional>
 #include <random>
@@ -167,11 +168,15 @@ LayoutChoice choose_layout(int n, const std::function<std::vector<Op>(const std:
         }
     }
     auto plan_cand = [&](Cand& c) {
-        const Plan p = plan_fused(lower(c.pi), n);
-        c.passes = p.passes.size();
-        c.tiles = plan_tiles(p);
-        c.cost = 0.0;
-        for (uint64_t t : c.tiles) c.cost += layout_cost_us(t);
+        try {  // (worker threads must not throw; a failed candidate just never wins)
+            const Plan p = plan_fused(lower(c.pi), n);
+            c.passes = p.passes.size();
+            c.tiles = plan_tiles(p);
+            c.cost = 0.0;
+            for (uint64_t t : c.tiles) c.cost += layout_cost_us(t);
+        } catch (...) {
+            c.passes = SIZE_MAX;
+        }
     };
     {
         std::vector<std::thread> th;
@@ -179,6 +184,7 @@ LayoutChoice choose_layout(int n, const std::function<std::vector<Op>(const std:
         for (auto& t : th) t.join();
     }
     LayoutChoice out;
+    if (cand[0].passes == SIZE_MAX) return out;  // the caller's own planning reports the error
     out.passes_before = cand[0].passes;
     out.cost_before = out.cost_after = cand[0].cost;
     size_t best_passes = cand[0].passes;
@@ -195,7 +201,11 @@ LayoutChoice choose_layout(int n, const std::function<std::vector<Op>(const std:
             th.emplace_back([&, i] {
                 const Cand& c = cand[pool[i]];
                 double b = 0.0, a = 0.0;
-                const std::vector<int> sigma = choose_relabel(c.tiles, n, &b, &a, 0.0);
+                std::vector<int> sigma;
+                try {
+                    sigma = choose_relabel(c.tiles, n, &b, &a, 0.0);
+                } catch (...) {
+                }
                 total[i] = c.pi;
                 if (!sigma.empty())
                     for (int q = 0; q < n; ++q) total[i][q] = sigma[c.pi[q]];
