@@ -419,7 +419,11 @@ int qsim_batch_run(qsim_batch* b, const qsim_gate* gates, size_t count,
                     }
                     return lops;
                 };
-                b->perm = choose_layout(b->n, lower_under, relabel_tries()).perm;
+                const int kind = 1 + (flags & QSIM_BATCH_REFERENCE_GATESET ? 1 : 0);
+                if (!layout_memo_get(b->n, kind, gates, count * sizeof(qsim_gate), b->perm)) {
+                    b->perm = choose_layout(b->n, lower_under, relabel_tries()).perm;
+                    layout_memo_put(b->n, kind, gates, count * sizeof(qsim_gate), b->perm);
+                }
             }
         }
         b->basis = false;

@@ -450,10 +450,16 @@ int qsim_run(qsim_state* s, const qsim_gate* gates, size_t count, int flags) {
                 }
                 return ops;
             };
-            LayoutChoice lc = choose_layout(s->n, lower_under, relabel_tries());
-            if (!lc.perm.empty()) {
+            std::vector<int> memo;
+            if (layout_memo_get(s->n, 0, gates, count * sizeof(qsim_gate), memo)) {
+                s->perm = memo;  // decided before for this circuit (its plan: the plan cache)
+            } else {
+                LayoutChoice lc = choose_layout(s->n, lower_under, relabel_tries());
+                layout_memo_put(s->n, 0, gates, count * sizeof(qsim_gate), lc.perm);
                 s->perm = lc.perm;
-                s->plans.put(std::move(lc.ops), s->n, std::move(lc.plan), s->stream);
+                if (!lc.perm.empty()) s->plans.put(std::move(lc.ops), s->n, std::move(lc.plan), s->stream);
+            }
+            if (!s->perm.empty()) {
                 if (s->basis_idx) {  // relabel the basis state itself
                     uint64_t k = 0;
                     for (int q = 0; q < s->n; ++q)

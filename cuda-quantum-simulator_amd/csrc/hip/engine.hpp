@@ -186,6 +186,9 @@ struct LayoutChoice {
 LayoutChoice choose_layout(int n, const std::function<std::vector<Op>(const std::vector<int>&)>& lower,
                            int tries);
 int relabel_tries();  // QSIM_RELABEL_TRIES (default 7): random labelings planned per choice
+// Process-wide memo of layout choices per circuit (kind: 0 state, 1 batched with its run flags).
+bool layout_memo_get(int n, int kind, const void* gates, size_t bytes, std::vector<int>& perm);
+void layout_memo_put(int n, int kind, const void* gates, size_t bytes, const std::vector<int>& perm);
 // Circuit-specialised pass kernels (jit.hip): hipRTC code object of one plan on one device.
 struct JitJob;
 struct JitModule {

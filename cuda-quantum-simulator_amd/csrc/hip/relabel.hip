@@ -16,7 +16,9 @@
 #include <cmath>
 #include <cstdint>
 #include <cstdlib>
+#include <cstring>
 #include <functional>
+#include <mutex>
 #include <random>
 #include <thread>
 #include <vector>
@@ -48,6 +50,41 @@ void relabel_configure(int mode, int min_qubits) {
     relabel_defaults();
     if (mode >= 0) g_relabel.store(mode);
     if (min_qubits >= 0) g_relabel_min.store(min_qubits);
+}
+
+// Process-wide memo of layout choices: the same circuit on a reset state (trajectory loops,
+// one state per shot batch, benchmark repetitions) re-uses the decision instead of planning the
+// candidates again.  Keyed by (n, kind, the exact gate bytes); LRU of kMemo entries.
+namespace {
+struct MemoEntry {
+    int n, kind;
+    std::vector<unsigned char> key;
+    std::vector<int> perm;
+    uint64_t used;
+};
+std::mutex g_memo_mu;
+std::vector<MemoEntry> g_memo;
+uint64_t g_memo_clock = 0;
+constexpr size_t kMemo = 16;
+}  // namespace
+
+bool layout_memo_get(int n, int kind, const void* gates, size_t bytes, std::vector<int>& perm) {
+    std::lock_guard<std::mutex> l(g_memo_mu);
+    for (MemoEntry& e : g_memo)
+        if (e.n == n && e.kind == kind && e.key.size() == bytes && std::memcmp(e.key.data(), gates, bytes) == 0) {
+            e.used = ++g_memo_clock;
+            perm = e.perm;
+            return true;
+        }
+    return false;
+}
+void layout_memo_put(int n, int kind, const void* gates, size_t bytes, const std::vector<int>& perm) {
+    std::lock_guard<std::mutex> l(g_memo_mu);
+    if (g_memo.size() >= kMemo)
+        g_memo.erase(std::min_element(g_memo.begin(), g_memo.end(),
+                                      [](const MemoEntry& a, const MemoEntry& b) { return a.used < b.used; }));
+    const unsigned char* p = static_cast<const unsigned char*>(gates);
+    g_memo.push_back(MemoEntry{n, kind, std::vector<unsigned char>(p, p + bytes), perm, ++g_memo_clock});
 }
 
 int relabel_tries() {
