@@ -41,7 +41,8 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--warmup", type=int, default=2)
-    p.add_argument("--qubits", type=int, default=30)
+    p.add_argument("--qubits", type=int, default=None,
+                   help="default 30 (W-HC / ref / 1q), 16 for --workload batch (W-BATCH)")
     p.add_argument("--depth", type=int, default=100)
     p.add_argument("--seed", type=int, default=42)
     p.add_argument("--mode", choices=["fused", "per-gate"], default="fused")
@@ -71,7 +72,10 @@ def parse():
                         "per rank and step, barriers and max-over-ranks timing (CPU tests)")
     p.add_argument("--pmc-json", default=None,
                    help="per-launch HBM traffic measured by rocprofv3 --pmc (see profiles/)")
-    return p.parse_args()
+    a = p.parse_args()
+    if a.qubits is None:
+        a.qubits = 16 if a.workload == "batch" else 30
+    return a
 
 
 def make_circuit(q, args):

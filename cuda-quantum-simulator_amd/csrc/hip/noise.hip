@@ -9,12 +9,16 @@
 // act on no qubit (:490-494).
 //
 // MI355X design: no per-pair curandState array (48 B x 2^(n-1), read and written by every noise
-// kernel of the reference).  A pair's uniforms come from a stateless counter hash of
-// (seed, noise-pass counter, pair index), so a flip pass costs only the pairs it modifies (the
-// lanes whose draw fires issue the loads; p = 0.01 touches ~1 % of the state) and a damping pass
-// streams the pairs once.  Realisations differ from cuRAND XORWOW (parity unpinned);
-// the per-pair distribution is the reference's: float uniform in (0, 1] (curand_uniform's range),
-// thresholds 1/3 and 2/3 as floats.  oracle/numpy_oracle.py restates the same hash for exact tests.
+// kernel of the reference).  Damping passes: a pair's uniform comes from a stateless counter hash
+// of (seed, noise-pass counter, pair index) and the pass streams the pairs once.  Flip passes
+// (X / Z / Y / depolarizing) do work in proportion to the flips, not the pairs: the global pair
+// index space is cut into blocks of 256 pairs, and one thread per block walks its flips with
+// geometric gaps (gap = floor(log u / log(1 - P)), P = the exact probability that the
+// reference's float uniform in (0, 1] falls below the double p), drawing each flip's Pauli as
+// the reference does (float uniform vs 1/3f, 2/3f).  Every pair still flips independently with
+// probability P — the reference's per-pair distribution — at p = 0.01 a pass costs ~1 % of the
+// hashes.  Realisations differ from cuRAND XORWOW (parity unpinned);
+// oracle/numpy_oracle.py restates the same streams for exact tests.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -52,6 +56,76 @@ struct NArgs {
     int target;
     double p;
 };
+
+// Flip passes by blocks of kFlipBlock global pairs: thread -> global block, geometric walk over
+// its flips (draw k of block b: nz_mix(stream_b + k * golden); stream_b = nz_mix(key ^
+// nz_mix(b ^ kBlockSalt))), applied to the pairs of this launch's range [idx0, idx0 + pairs).
+constexpr uint64_t kFlipBlockLog = 8, kFlipBlock = 1ull << kFlipBlockLog;
+constexpr uint64_t kBlockSalt = 0xb10c5a17b10c5a17ull;
+struct FArgsN {
+    double2* st;
+    uint64_t pairs, idx0;
+    int log_ppt;
+    uint64_t key;
+    int target;
+    int type;        // 0 depolarizing, 3 X, 4 Z, 5 Y
+    double lq;       // log1p(-P)
+    int always;      // P == 1: every pair flips
+};
+__global__ __launch_bounds__(256) void k_noise_flips(FArgsN a) {
+    const uint64_t b0 = a.idx0 >> kFlipBlockLog;
+    const uint64_t b1 = (a.idx0 + a.pairs - 1) >> kFlipBlockLog;
+    const uint64_t mask = (1ull << a.target) - 1ull;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t b = b0 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; b <= b1; b += stride) {
+        const uint64_t stream = nz_mix(a.key ^ nz_mix(b ^ kBlockSalt));
+        int64_t pos = -1;
+        for (uint64_t k = 0;; ++k) {
+            const uint64_t h = nz_mix(stream + k * 0x9e3779b97f4a7c15ull);
+            if (a.always) {
+                pos += 1;
+            } else {
+                const double u = (double)((h >> 11) + 1ull) * 0x1.0p-53;  // (0, 1]
+                const double gap = floor(log(u) / a.lq);
+                if (gap >= (double)kFlipBlock) break;
+                pos += (int64_t)gap + 1;
+            }
+            if (pos >= (int64_t)kFlipBlock) break;
+            const uint64_t g = (b << kFlipBlockLog) + (uint64_t)pos;  // global pair index
+            if (g < a.idx0 || g >= a.idx0 + a.pairs) continue;          // another shard's pair
+            const uint64_t idx = g - a.idx0;
+            int pauli = a.type == 3 ? 1 : (a.type == 4 ? 3 : 2);  // 1 X, 2 Y, 3 Z
+            if (a.type == 0) {
+                const float r2 = nz_uniform(nz_mix(h ^ 0x5bd1e9955bd1e995ull));
+                pauli = r2 < 1.0f / 3.0f ? 1 : (r2 < 2.0f / 3.0f ? 2 : 3);
+            }
+            const uint64_t traj = idx >> a.log_ppt, pr = idx & ((1ull << a.log_ppt) - 1ull);
+            const uint64_t i0 = (traj << (a.log_ppt + 1)) | (pr & mask) | ((pr & ~mask) << 1);
+            const uint64_t i1 = i0 | (1ull << a.target);
+            if (pauli == 3) {
+                const double2 v = a.st[i1];
+                a.st[i1] = make_double2(-v.x, -v.y);
+            } else {
+                const double2 a0 = a.st[i0], a1 = a.st[i1];
+                if (pauli == 1) {
+                    a.st[i0] = a1;
+                    a.st[i1] = a0;
+                } else {  // Y = [[0, -i], [i, 0]] (:177-178)
+                    a.st[i0] = make_double2(a1.y, -a1.x);
+                    a.st[i1] = make_double2(-a0.y, a0.x);
+                }
+            }
+        }
+    }
+}
+
+// P(float uniform in (0, 1] < p): the reference compares curand_uniform's (k + 1) / 2^24,
+// k uniform in [0, 2^24), with the double p.
+double flip_probability(double p) {
+    if (!(p > 0.0)) return 0.0;
+    const double c = std::ceil(p * 16777216.0) - 1.0;  // #{k : (k + 1) / 2^24 < p}
+    return std::min(16777216.0, std::max(0.0, c)) / 16777216.0;
+}
 
 template <int TYPE>
 __global__ __launch_bounds__(256) void k_noise(NArgs a) {
@@ -152,6 +226,25 @@ void launch_noise(double2* st, int n, int type, int qubit, double p, uint64_t se
     const double bytes = (type == 1 || type == 2) ? 32.0 * pairs
                                                   : 32.0 * pairs * std::min(1.0, std::max(0.0, p));
     TimedLaunch tl(tm, "noise", bytes, s);
+    if (type == 0 || type >= 3) {  // flips: geometric walk per block of pairs
+        FArgsN f{};
+        f.st = st;
+        f.pairs = a.pairs;
+        f.idx0 = a.idx0;
+        f.log_ppt = a.log_ppt;
+        f.key = a.key;
+        f.target = qubit;
+        f.type = type;
+        const double P = flip_probability(p);
+        if (P <= 0.0) return;
+        f.always = P >= 1.0 ? 1 : 0;
+        f.lq = f.always ? -1.0 : std::log1p(-P);
+        const uint64_t nb = ((a.idx0 + a.pairs - 1) >> kFlipBlockLog) - (a.idx0 >> kFlipBlockLog) + 1;
+        const uint64_t fb = std::min<uint64_t>((nb + 255) / 256, 256ull * 32);
+        hipLaunchKernelGGL(k_noise_flips, dim3((unsigned)fb), dim3(256), 0, s, f);
+        QSIM_HIPCHK(hipGetLastError());
+        return;
+    }
     switch (type) {
         case 0: hipLaunchKernelGGL(k_noise<0>, dim3((unsigned)blocks), dim3(256), 0, s, a); break;
         case 1: hipLaunchKernelGGL(k_noise<1>, dim3((unsigned)blocks), dim3(256), 0, s, a); break;

@@ -17,6 +17,7 @@ vectors in tests/golden/.
 from __future__ import annotations
 
 import ctypes
+import math
 import os
 from typing import Iterable, Sequence, Tuple
 
@@ -210,6 +211,65 @@ def _uniform(h):
         np.float32(1.0 / 16777216.0)
 
 
+# Flip channels (X / Z / Y / depolarizing) draw their flips per block of 256 global pair
+# indices with geometric gaps (csrc/hip/noise.hip k_noise_flips): every pair still flips
+# independently with P = P(float uniform in (0, 1] < p), the reference's per-pair law
+# (src/NoiseModel.cu:195, :857-861), but the engine does work per flip rather than per pair.
+_FLIP_BLOCK_LOG = 8
+_BLOCK_SALT = 0xb10c5a17b10c5a17
+
+
+def flip_probability(p):
+    """P(curand_uniform < p) for curand_uniform = (k + 1) / 2^24, k uniform in [0, 2^24)."""
+    if not p > 0.0:
+        return 0.0
+    c = math.ceil(p * 16777216.0) - 1.0
+    return min(16777216.0, max(0.0, c)) / 16777216.0
+
+
+def flip_events(key, idx0, pairs, p, depolarizing):
+    """(global pair indices, Pauli codes 1 X / 2 Y / 3 Z or None) of one flip pass over the
+    global pairs [idx0, idx0 + pairs), in the engine's draw order."""
+    P = flip_probability(p)
+    if P <= 0.0 or pairs == 0:
+        return np.zeros(0, np.uint64), np.zeros(0, np.int64)
+    always = P >= 1.0
+    lq = -1.0 if always else math.log1p(-P)
+    B = 1 << _FLIP_BLOCK_LOG
+    blocks = np.arange(idx0 >> _FLIP_BLOCK_LOG, ((idx0 + pairs - 1) >> _FLIP_BLOCK_LOG) + 1,
+                       dtype=np.uint64)
+    stream = _mix_np(np.uint64(key) ^ _mix_np(blocks ^ np.uint64(_BLOCK_SALT)))
+    pos = np.full(blocks.size, -1, np.int64)
+    live = np.ones(blocks.size, bool)
+    out_g, out_h = [], []
+    k = 0
+    with np.errstate(over="ignore", divide="ignore"):
+        while live.any():
+            h = _mix_np(stream + np.uint64(k) * np.uint64(0x9e3779b97f4a7c15))
+            if always:
+                step = np.ones(blocks.size, np.int64)
+            else:
+                u = ((h >> np.uint64(11)) + np.uint64(1)).astype(np.float64) * 2.0 ** -53
+                gap = np.floor(np.log(u) / lq)
+                live &= gap < B
+                step = np.where(live, np.minimum(gap, B), 0).astype(np.int64) + 1
+            pos = np.where(live, pos + step, pos)
+            live &= pos < B
+            g = (blocks << np.uint64(_FLIP_BLOCK_LOG)) + pos.astype(np.uint64)
+            keep = live & (g >= np.uint64(idx0)) & (g < np.uint64(idx0 + pairs))
+            out_g.append(g[keep])
+            out_h.append(h[keep])
+            k += 1
+    g = np.concatenate(out_g)
+    h = np.concatenate(out_h)
+    if not depolarizing:
+        return g, None
+    r2 = _uniform(_mix_np(h ^ np.uint64(0x5bd1e9955bd1e995)))
+    pauli = np.where(r2 < np.float32(1.0) / np.float32(3.0), 1,
+                     np.where(r2 < np.float32(2.0) / np.float32(3.0), 2, 3))
+    return g, pauli
+
+
 def noise_pass(state, n, ntype, q, p, seed, counter):
     """One reference noise kernel (type numbering == NoiseType) on `state` (modified copy)."""
     s = np.array(state, dtype=complex)
@@ -221,13 +281,13 @@ def noise_pass(state, n, ntype, q, p, seed, counter):
     i1 = i0 | (1 << q)
     a0, a1 = s[i0].copy(), s[i1].copy()
     if ntype in (0, 3, 4, 5):
-        fire = r1.astype(np.float64) < float(p)  # float draw promoted to double (NoiseModel.cu:195)
+        # each pair flips with P(float draw < p), the draw promoted to double (NoiseModel.cu:195)
+        g, dp = flip_events(noise_key(seed, counter), 0, 1 << (n - 1), p, ntype == 0)
+        fire = np.zeros(idx.size, bool)
+        fire[g.astype(np.int64)] = True
+        pauli = np.full(idx.size, {0: 0, 3: 1, 4: 3, 5: 2}[ntype])
         if ntype == 0:
-            r2 = _uniform(_mix_np(h ^ np.uint64(0x5bd1e9955bd1e995)))
-            pauli = np.where(r2 < np.float32(1.0) / np.float32(3.0), 1,
-                             np.where(r2 < np.float32(2.0) / np.float32(3.0), 2, 3))
-        else:
-            pauli = np.full(idx.size, {3: 1, 4: 3, 5: 2}[ntype])
+            pauli[g.astype(np.int64)] = dp
         x, y, z = fire & (pauli == 1), fire & (pauli == 2), fire & (pauli == 3)
         s[i0[x]], s[i1[x]] = a1[x], a0[x]
         s[i0[y]], s[i1[y]] = -1j * a1[y], 1j * a0[y]
@@ -289,11 +349,11 @@ def batched_depolarizing_pass(states, n, q, p, seed, counter):
     B = s.shape[0]
     npairs = 1 << (n - 1)
     idx = np.arange(B * npairs, dtype=np.uint64)
-    h = _mix_np(np.uint64(noise_key(seed, counter)) ^ _mix_np(idx))
-    fire = _uniform(h).astype(np.float64) < float(p)
-    r2 = _uniform(_mix_np(h ^ np.uint64(0x5bd1e9955bd1e995)))
-    pauli = np.where(r2 < np.float32(1.0) / np.float32(3.0), 1,
-                     np.where(r2 < np.float32(2.0) / np.float32(3.0), 2, 3))
+    g, dp = flip_events(noise_key(seed, counter), 0, B * npairs, p, True)
+    fire = np.zeros(idx.size, bool)
+    fire[g.astype(np.int64)] = True
+    pauli = np.zeros(idx.size, np.int64)
+    pauli[g.astype(np.int64)] = dp
     traj = (idx // np.uint64(npairs)).astype(np.int64)
     pr = (idx % np.uint64(npairs)).astype(np.int64)
     mask = (1 << q) - 1
