@@ -461,14 +461,13 @@ int qsim_batch_run(qsim_batch* b, const qsim_gate* gates, size_t count,
             // all B x 2^(n-1) amplitude pairs; every pair draws its own uniform (counter hash of
             // (seed, pass, global pair index) in place of its curandState) and, below p, a second
             // one picks X / Y / Z at 1/3, 2/3 — applied to that pair only (F7).
-            std::vector<const qsim_noise_channel*> dep;
+            std::vector<NoiseChan> dep;
             for (size_t i = 0; i < n_channels; ++i)
-                if (channels[i].type == 0) dep.push_back(&channels[i]);
+                if (channels[i].type == 0) dep.push_back(NoiseChan{0, channels[i].qubit, channels[i].probability});
             for (const Op& op : ops) {
                 if (op.kind >= 0) launch_op(b->d, b->n, (uint64_t)b->batch, op, b->stream, &b->timer);
-                for (const qsim_noise_channel* c : dep)
-                    launch_noise(b->d, b->n, 0, c->qubit, c->probability, b->seed, b->ncounter++,
-                                 b->stream, &b->timer, (uint64_t)b->batch, b->traj0);
+                launch_noise_after_gate(b->d, b->n, dep, b->seed, b->ncounter, b->stream, &b->timer,
+                                        (uint64_t)b->batch, b->traj0);
             }
             return;
         }

@@ -246,6 +246,15 @@ void launch_fused(double2* st, int n, uint64_t batch, const Plan& plan, const Ti
 // traj0: global trajectory index of trajectory 0 (the pair index hashed is the global one).
 void launch_noise(double2* st, int n, int type, int qubit, double p, uint64_t seed,
                   uint64_t counter, hipStream_t s, Timer* tm, uint64_t batch = 1, uint64_t traj0 = 0);
+// Every channel that follows one gate, passes counter, counter + 1, ... (counter is advanced):
+// flip channels over a large batch run in one launch (work-group per unit of trajectories),
+// otherwise one launch_noise per channel.  Same draws and results either way.
+struct NoiseChan {
+    int type, qubit;
+    double p;
+};
+void launch_noise_after_gate(double2* st, int n, const std::vector<NoiseChan>& chans, uint64_t seed,
+                             uint64_t& counter, hipStream_t s, Timer* tm, uint64_t batch, uint64_t traj0);
 
 // Density matrices as 2n-index-bit states (density.hip).
 void dm_lower(int n, const qsim_gate* gates, size_t count, const qsim_noise_channel* ch,

@@ -23,6 +23,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <string>
 
 #include "engine.hpp"
@@ -57,65 +58,125 @@ struct NArgs {
     double p;
 };
 
-// Flip passes by blocks of kFlipBlock global pairs: thread -> global block, geometric walk over
-// its flips (draw k of block b: nz_mix(stream_b + k * golden); stream_b = nz_mix(key ^
-// nz_mix(b ^ kBlockSalt))), applied to the pairs of this launch's range [idx0, idx0 + pairs).
+// Flip passes by blocks of kFlipBlock global pairs: one thread walks one block's flips (draw k of
+// block b: nz_mix(stream_b + k * golden); stream_b = nz_mix(key ^ nz_mix(b ^ kBlockSalt))) and
+// applies those inside [lo, hi), the global pairs this launch / work-group owns.
 constexpr uint64_t kFlipBlockLog = 8, kFlipBlock = 1ull << kFlipBlockLog;
 constexpr uint64_t kBlockSalt = 0xb10c5a17b10c5a17ull;
+struct FlipChan {
+    uint64_t key;
+    double lq;   // log1p(-P)
+    int target;
+    int type;    // 0 depolarizing, 3 X, 4 Z, 5 Y
+    int always;  // P == 1: every pair flips
+    int pad;
+};
+// Next flip of a block's walk inside [lo, hi): false when the block is exhausted.
+struct FlipCursor {
+    uint64_t stream, k;
+    int64_t pos;
+    bool done;
+};
+__device__ __forceinline__ bool next_flip(FlipCursor& cur, uint64_t b, uint64_t lo, uint64_t hi,
+                                          const FlipChan& c, uint64_t& g, uint64_t& h) {
+    while (!cur.done) {
+        h = nz_mix(cur.stream + cur.k * 0x9e3779b97f4a7c15ull);
+        ++cur.k;
+        if (c.always) {
+            cur.pos += 1;
+        } else {
+            const double u = (double)((h >> 11) + 1ull) * 0x1.0p-53;  // (0, 1]
+            const double gap = floor(log(u) / c.lq);
+            if (gap >= (double)kFlipBlock) {
+                cur.done = true;
+                break;
+            }
+            cur.pos += (int64_t)gap + 1;
+        }
+        if (cur.pos >= (int64_t)kFlipBlock) {
+            cur.done = true;
+            break;
+        }
+        g = (b << kFlipBlockLog) + (uint64_t)cur.pos;  // global pair index
+        if (g >= lo && g < hi) return true;           // else another shard's pair
+    }
+    return false;
+}
+
+// Walks block b and applies its flips.  (Batching several flips' loads before their stores was
+// measured: no change — the launch is bound by random-access memory throughput, not latency.)
+__device__ __forceinline__ void flip_block(double2* st, uint64_t b, uint64_t lo, uint64_t hi,
+                                           uint64_t idx0, int log_ppt, const FlipChan& c) {
+    const uint64_t mask = (1ull << c.target) - 1ull;
+    FlipCursor cur{nz_mix(c.key ^ nz_mix(b ^ kBlockSalt)), 0, -1, false};
+    uint64_t g = 0, h = 0;
+    while (next_flip(cur, b, lo, hi, c, g, h)) {
+        int pauli = c.type == 3 ? 1 : (c.type == 4 ? 3 : 2);  // 1 X, 2 Y, 3 Z
+        if (c.type == 0) {                                      // depolarizing (:191-216)
+            const float r2 = nz_uniform(nz_mix(h ^ 0x5bd1e9955bd1e995ull));
+            pauli = r2 < 1.0f / 3.0f ? 1 : (r2 < 2.0f / 3.0f ? 2 : 3);
+        }
+        // reference idx -> (traj, pair_idx) split (src/NoiseModel.cu:843-856)
+        const uint64_t idx = g - idx0;
+        const uint64_t traj = idx >> log_ppt, pr = idx & ((1ull << log_ppt) - 1ull);
+        const uint64_t i0 = (traj << (log_ppt + 1)) | (pr & mask) | ((pr & ~mask) << 1);
+        const uint64_t i1 = i0 | (1ull << c.target);
+        if (pauli == 3) {
+            const double2 v = st[i1];
+            st[i1] = make_double2(-v.x, -v.y);
+        } else {
+            const double2 a0 = st[i0], a1 = st[i1];
+            if (pauli == 1) {
+                st[i0] = a1;
+                st[i1] = a0;
+            } else {  // Y = [[0, -i], [i, 0]] (:177-178)
+                st[i0] = make_double2(a1.y, -a1.x);
+                st[i1] = make_double2(-a0.y, a0.x);
+            }
+        }
+    }
+}
+
 struct FArgsN {
     double2* st;
     uint64_t pairs, idx0;
     int log_ppt;
-    uint64_t key;
-    int target;
-    int type;        // 0 depolarizing, 3 X, 4 Z, 5 Y
-    double lq;       // log1p(-P)
-    int always;      // P == 1: every pair flips
+    FlipChan c;
 };
 __global__ __launch_bounds__(256) void k_noise_flips(FArgsN a) {
     const uint64_t b0 = a.idx0 >> kFlipBlockLog;
     const uint64_t b1 = (a.idx0 + a.pairs - 1) >> kFlipBlockLog;
-    const uint64_t mask = (1ull << a.target) - 1ull;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t b = b0 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; b <= b1; b += stride) {
-        const uint64_t stream = nz_mix(a.key ^ nz_mix(b ^ kBlockSalt));
-        int64_t pos = -1;
-        for (uint64_t k = 0;; ++k) {
-            const uint64_t h = nz_mix(stream + k * 0x9e3779b97f4a7c15ull);
-            if (a.always) {
-                pos += 1;
-            } else {
-                const double u = (double)((h >> 11) + 1ull) * 0x1.0p-53;  // (0, 1]
-                const double gap = floor(log(u) / a.lq);
-                if (gap >= (double)kFlipBlock) break;
-                pos += (int64_t)gap + 1;
-            }
-            if (pos >= (int64_t)kFlipBlock) break;
-            const uint64_t g = (b << kFlipBlockLog) + (uint64_t)pos;  // global pair index
-            if (g < a.idx0 || g >= a.idx0 + a.pairs) continue;          // another shard's pair
-            const uint64_t idx = g - a.idx0;
-            int pauli = a.type == 3 ? 1 : (a.type == 4 ? 3 : 2);  // 1 X, 2 Y, 3 Z
-            if (a.type == 0) {
-                const float r2 = nz_uniform(nz_mix(h ^ 0x5bd1e9955bd1e995ull));
-                pauli = r2 < 1.0f / 3.0f ? 1 : (r2 < 2.0f / 3.0f ? 2 : 3);
-            }
-            const uint64_t traj = idx >> a.log_ppt, pr = idx & ((1ull << a.log_ppt) - 1ull);
-            const uint64_t i0 = (traj << (a.log_ppt + 1)) | (pr & mask) | ((pr & ~mask) << 1);
-            const uint64_t i1 = i0 | (1ull << a.target);
-            if (pauli == 3) {
-                const double2 v = a.st[i1];
-                a.st[i1] = make_double2(-v.x, -v.y);
-            } else {
-                const double2 a0 = a.st[i0], a1 = a.st[i1];
-                if (pauli == 1) {
-                    a.st[i0] = a1;
-                    a.st[i1] = a0;
-                } else {  // Y = [[0, -i], [i, 0]] (:177-178)
-                    a.st[i0] = make_double2(a1.y, -a1.x);
-                    a.st[i1] = make_double2(-a0.y, a0.x);
-                }
-            }
-        }
+    for (uint64_t b = b0 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; b <= b1; b += stride)
+        flip_block(a.st, b, a.idx0, a.idx0 + a.pairs, a.idx0, a.log_ppt, a.c);
+}
+
+// All flip channels that follow one gate, in one launch.  Channel order matters only within a
+// trajectory (a pair never spans two), so each work-group owns an aligned unit of 2^log_unit
+// global pairs — whole trajectories and whole blocks — and runs the channels in order over it with
+// a work-group barrier between channels (its global writes are visible to its own waves after the
+// barrier: one CU).  Same draws and the same result as one k_noise_flips launch per channel.
+constexpr int kMaxUnitChannels = 32;
+struct UArgs {
+    double2* st;
+    uint64_t pairs, idx0;
+    int log_ppt, log_unit, nch;
+    FlipChan ch[kMaxUnitChannels];
+};
+__global__ __launch_bounds__(256) void k_noise_units(UArgs a) {
+    const uint64_t base = ((a.idx0 >> a.log_unit) + blockIdx.x) << a.log_unit;
+    const uint64_t lo = base > a.idx0 ? base : a.idx0;
+    const uint64_t end = a.idx0 + a.pairs, top = base + (1ull << a.log_unit);
+    const uint64_t hi = top < end ? top : end;
+    // only the blocks that overlap [lo, hi) (a batched-load variant of flip_block that also let
+    // lanes walk blocks wholly outside the range returned wrong states; not understood, so such
+    // lanes are never launched; tests/test_batched_refnoise_gpu.py covers ranges that start and
+    // end mid-block)
+    const uint64_t b0 = lo >> kFlipBlockLog, nb = ((hi - 1) >> kFlipBlockLog) - b0 + 1;
+    for (int c = 0; c < a.nch; ++c) {
+        if (c) __syncthreads();
+        for (uint64_t j = threadIdx.x; j < nb; j += blockDim.x)
+            flip_block(a.st, b0 + j, lo, hi, a.idx0, a.log_ppt, a.ch[c]);
     }
 }
 
@@ -127,6 +188,7 @@ double flip_probability(double p) {
     return std::min(16777216.0, std::max(0.0, c)) / 16777216.0;
 }
 
+// Damping channels: every pair draws (counter hash of the global pair index) and is rewritten.
 template <int TYPE>
 __global__ __launch_bounds__(256) void k_noise(NArgs a) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
@@ -138,27 +200,7 @@ __global__ __launch_bounds__(256) void k_noise(NArgs a) {
         const uint64_t traj = idx >> a.log_ppt, pr = idx & ((1ull << a.log_ppt) - 1ull);
         const uint64_t i0 = (traj << (a.log_ppt + 1)) | (pr & mask) | ((pr & ~mask) << 1);
         const uint64_t i1 = i0 | (1ull << a.target);
-        if constexpr (TYPE == 0 || TYPE == 3 || TYPE == 4 || TYPE == 5) {  // Pauli flips
-            if (!((double)r1 < a.p)) continue;  // float draw vs double p, as the reference (:195)
-            int pauli = TYPE == 3 ? 1 : (TYPE == 4 ? 3 : 2);  // 1 X, 2 Y, 3 Z
-            if constexpr (TYPE == 0) {                         // depolarizing (:191-216)
-                const float r2 = nz_uniform(nz_mix(h ^ 0x5bd1e9955bd1e995ull));
-                pauli = r2 < 1.0f / 3.0f ? 1 : (r2 < 2.0f / 3.0f ? 2 : 3);
-            }
-            if (pauli == 3) {
-                const double2 v = a.st[i1];
-                a.st[i1] = make_double2(-v.x, -v.y);
-            } else {
-                const double2 a0 = a.st[i0], a1 = a.st[i1];
-                if (pauli == 1) {
-                    a.st[i0] = a1;
-                    a.st[i1] = a0;
-                } else {  // Y = [[0, -i], [i, 0]] (:177-178)
-                    a.st[i0] = make_double2(a1.y, -a1.x);
-                    a.st[i1] = make_double2(-a0.y, a0.x);
-                }
-            }
-        } else if constexpr (TYPE == 1) {  // amplitude damping (:224-269)
+        if constexpr (TYPE == 1) {  // amplitude damping (:224-269)
             const double2 a0 = a.st[i0], a1 = a.st[i1];
             const double g = a.p;
             const double p1 = a1.x * a1.x + a1.y * a1.y;
@@ -206,12 +248,68 @@ uint64_t noise_key(uint64_t seed, uint64_t counter) {
     return nz_mix_host(nz_mix_host(seed) ^ (counter * 0x9e3779b97f4a7c15ull + 0x632be59bd9b4e019ull));
 }
 
-void launch_noise(double2* st, int n, int type, int qubit, double p, uint64_t seed,
-                  uint64_t counter, hipStream_t s, Timer* tm, uint64_t batch, uint64_t traj0) {
+static void check_channel(int n, int type, int qubit, double p) {
     if (type < 0 || type > 5) fail(QSIM_ERR_INVALID_ARGUMENT, "unknown noise type");
     if (qubit < 0 || qubit >= n)
         fail(QSIM_ERR_OUT_OF_RANGE, "Qubit index " + std::to_string(qubit) + " out of range");
     if (!std::isfinite(p)) fail(QSIM_ERR_INVALID_ARGUMENT, "noise probability must be finite");
+}
+
+// false when the channel never fires (P == 0)
+static bool flip_channel(int type, int qubit, double p, uint64_t key, FlipChan& c) {
+    const double P = flip_probability(p);
+    if (P <= 0.0) return false;
+    c.key = key;
+    c.target = qubit;
+    c.type = type;
+    c.always = P >= 1.0 ? 1 : 0;
+    c.lq = c.always ? -1.0 : std::log1p(-P);
+    return true;
+}
+
+void launch_noise_after_gate(double2* st, int n, const std::vector<NoiseChan>& chans, uint64_t seed,
+                             uint64_t& counter, hipStream_t s, Timer* tm, uint64_t batch, uint64_t traj0) {
+    const int log_ppt = n - 1;
+    const int log_unit = std::max(log_ppt, 16);  // whole trajectories, >= 256 blocks of 256 pairs
+    const uint64_t pairs = batch << log_ppt, idx0 = traj0 << log_ppt;
+    const uint64_t units = ((idx0 + pairs - 1) >> log_unit) - (idx0 >> log_unit) + 1;
+    bool flips = true;
+    for (const NoiseChan& c : chans) flips = flips && (c.type == 0 || c.type >= 3);
+    // QSIM_NOISE_UNIT_MIN (default 128): fewest units for the one-launch path (tests force both)
+    const char* e = std::getenv("QSIM_NOISE_UNIT_MIN");
+    const uint64_t unit_min = e ? (uint64_t)std::max(1ll, std::atoll(e)) : 128;
+    if (!flips || units < unit_min || units > 0x7fffffffull) {  // few work-groups: one launch per channel
+        for (const NoiseChan& c : chans)
+            launch_noise(st, n, c.type, c.qubit, c.p, seed, counter++, s, tm, batch, traj0);
+        return;
+    }
+    for (size_t c0 = 0; c0 < chans.size(); c0 += kMaxUnitChannels) {
+        UArgs u{};
+        u.st = st;
+        u.pairs = pairs;
+        u.idx0 = idx0;
+        u.log_ppt = log_ppt;
+        u.log_unit = log_unit;
+        double bytes = 0.0;
+        for (size_t c = c0; c < std::min(chans.size(), c0 + kMaxUnitChannels); ++c) {
+            const NoiseChan& ch = chans[c];
+            check_channel(n, ch.type, ch.qubit, ch.p);
+            const uint64_t key = noise_key(seed, counter++);
+            if (flip_channel(ch.type, ch.qubit, ch.p, key, u.ch[u.nch])) ++u.nch;
+            bytes += 32.0 * (double)pairs * std::min(1.0, std::max(0.0, ch.p));
+        }
+        if (!u.nch) continue;
+        TimedLaunch tl(tm, "noise", bytes, s);
+        // one work-group per unit (fewer work-groups looping over units measured slower: the
+        // walk is latency-bound)
+        hipLaunchKernelGGL(k_noise_units, dim3((unsigned)units), dim3(256), 0, s, u);
+        QSIM_HIPCHK(hipGetLastError());
+    }
+}
+
+void launch_noise(double2* st, int n, int type, int qubit, double p, uint64_t seed,
+                  uint64_t counter, hipStream_t s, Timer* tm, uint64_t batch, uint64_t traj0) {
+    check_channel(n, type, qubit, p);
     NArgs a{};
     a.st = st;
     a.pairs = batch << (n - 1);
@@ -232,26 +330,14 @@ void launch_noise(double2* st, int n, int type, int qubit, double p, uint64_t se
         f.pairs = a.pairs;
         f.idx0 = a.idx0;
         f.log_ppt = a.log_ppt;
-        f.key = a.key;
-        f.target = qubit;
-        f.type = type;
-        const double P = flip_probability(p);
-        if (P <= 0.0) return;
-        f.always = P >= 1.0 ? 1 : 0;
-        f.lq = f.always ? -1.0 : std::log1p(-P);
+        if (!flip_channel(type, qubit, p, a.key, f.c)) return;
         const uint64_t nb = ((a.idx0 + a.pairs - 1) >> kFlipBlockLog) - (a.idx0 >> kFlipBlockLog) + 1;
         const uint64_t fb = std::min<uint64_t>((nb + 255) / 256, 256ull * 32);
         hipLaunchKernelGGL(k_noise_flips, dim3((unsigned)fb), dim3(256), 0, s, f);
-        QSIM_HIPCHK(hipGetLastError());
-        return;
-    }
-    switch (type) {
-        case 0: hipLaunchKernelGGL(k_noise<0>, dim3((unsigned)blocks), dim3(256), 0, s, a); break;
-        case 1: hipLaunchKernelGGL(k_noise<1>, dim3((unsigned)blocks), dim3(256), 0, s, a); break;
-        case 2: hipLaunchKernelGGL(k_noise<2>, dim3((unsigned)blocks), dim3(256), 0, s, a); break;
-        case 3: hipLaunchKernelGGL(k_noise<3>, dim3((unsigned)blocks), dim3(256), 0, s, a); break;
-        case 4: hipLaunchKernelGGL(k_noise<4>, dim3((unsigned)blocks), dim3(256), 0, s, a); break;
-        default: hipLaunchKernelGGL(k_noise<5>, dim3((unsigned)blocks), dim3(256), 0, s, a); break;
+    } else if (type == 1) {
+        hipLaunchKernelGGL(k_noise<1>, dim3((unsigned)blocks), dim3(256), 0, s, a);
+    } else {
+        hipLaunchKernelGGL(k_noise<2>, dim3((unsigned)blocks), dim3(256), 0, s, a);
     }
     QSIM_HIPCHK(hipGetLastError());
 }

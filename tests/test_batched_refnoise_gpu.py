@@ -108,3 +108,40 @@ def test_reference_compatible_profile_cpp_names(qsim, gpu_ready):
     b.run(c)
     p = b.getAverageProbabilities()
     np.testing.assert_allclose(p, [0.5, 0, 0, 0.5, 0, 0, 0, 0], atol=1e-12)
+
+
+@pytest.mark.parametrize("n,B,seed,traj0", [(6, 8, 4, 0), (6, 5, 5, 3), (9, 6, 5, 2), (12, 4, 6, 0), (3, 50, 7, 3)])
+def test_reference_noise_one_launch_per_gate(qsim, oracle, gpu_ready, monkeypatch, n, B, seed, traj0):
+    """All Depolarizing passes after a gate in ONE launch (k_noise_units: a work-group per unit
+    of whole trajectories, channels in order between work-group barriers), forced here at oracle
+    sizes (QSIM_NOISE_UNIT_MIN=1), also on a trajectory shard whose pairs start mid-block."""
+    monkeypatch.setenv("QSIM_NOISE_UNIT_MIN", "1")
+    c = _circuit(qsim, n, 12, seed)
+    nm = qsim.NoiseModel()
+    nm.addDepolarizingAll(n, 0.2)
+    s = qsim.BatchedSimulator(n, B, nm, noise=qsim.BatchedNoise.Reference)
+    s.setSeed(seed)
+    s.setTrajectoryOffset(traj0)
+    s.run(c)
+    entries = [(0, q, 0.2) for q in range(n)]
+    whole, _ = oracle.batched_reference_run(n, traj0 + B, oracle.gates_of(c), entries, seed)
+    for t in range(B):
+        np.testing.assert_allclose(s.getStateVector(t), whole[traj0 + t], atol=1e-12, rtol=0)
+
+
+def test_reference_noise_one_launch_equals_per_channel_16q(qsim, gpu_ready, monkeypatch):
+    """BASELINE config-4 shape (16 qubits, 256 trajectories, depolarizing on every qubit): the
+    one-launch path (default at this size) and one launch per channel give identical states."""
+    n, B = 16, 256
+    c = qsim.createRandomHCCircuit(n, 20, 42)
+    nm = qsim.NoiseModel()
+    nm.addDepolarizingAll(n, 0.01)
+    out = []
+    for unit_min in ("128", str(1 << 40)):
+        monkeypatch.setenv("QSIM_NOISE_UNIT_MIN", unit_min)
+        s = qsim.BatchedSimulator(n, B, nm, noise=qsim.BatchedNoise.Reference)
+        s.setSeed(9)
+        s.run(c)
+        out.append(np.stack([s.getStateVector(t) for t in (0, 77, 255)]))
+    assert np.array_equal(out[0], out[1])
+    assert abs(np.sum(np.abs(out[0][1]) ** 2) - 1.0) < 1e-10
