@@ -20,10 +20,12 @@
 #include <algorithm>
 #include <chrono>
 #include <thread>
+#include <climits>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -40,33 +42,63 @@ struct DStep {
     int k = 0;
     int gpos[8] = {0}, lpos[8] = {0};
     std::vector<Op> ops;
-    // Overlap of a remap with local work (mark_overlap): an exchange with pivot >= 0 runs as two
-    // half-exchanges, one per value of local physical qubit `pivot`.  An ops step with role bit 1
-    // runs the trailing passes of its fused plan that avoid the pivot of the exchange after it
-    // per half (so half 0's transfer overlaps half 1's passes); role bit 2: the leading passes
-    // that avoid the pivot of the exchange before it run per half, each as soon as its half has
-    // landed.  The step's plan is the same one-piece fused plan either way (no extra passes).
+    // Overlap of a remap with local work (mark_overlap): an exchange with pivots (pmask != 0, up
+    // to kMaxPivots local physical positions) runs as 2^m part-exchanges, one per value of the
+    // pivot bits.  An ops step with role bit 1 runs the trailing passes of its fused plan that
+    // avoid the pivots of the exchange after it per part (so part j's transfer overlaps the later
+    // parts' passes); role bit 2: the leading passes that avoid the pivots of the exchange before
+    // it run per part, each as soon as its part has landed.  The step's plan is the same one-piece
+    // fused plan either way (no extra passes).  `pivot`: the lowest pivot (-1: none).
     int pivot = -1, role = 0;
+    uint64_t pmask = 0;
     // planning only: the circuit gates emitted into this step (rank-independent), their physical
     // qubit masks, and for each op the index of the gate (in this list) it came from
     std::vector<uint64_t> gmask;
     std::vector<int> op_gate;
 };
 
-// Choose, for every exchange between two ops steps, a pivot qubit: the local position most of the
-// trailing gates of the step before and the leading gates of the step after leave alone
-// (QSIM_DIST_OVERLAP=0 disables).  Decided from the rank-independent gate lists only, so every
-// rank picks the same pivot and runs the same exchange skeleton.  The pivot is a local physical
-// position >= 6 (never a tile's contiguous run) outside the exchanged positions.  The ops steps
-// are not split: each rank plans a step as one fused plan (tiles padded away from the pivots) and
-// runs per half only the passes at its ends that avoid them (run_step).
-static void mark_overlap(std::vector<DStep>& steps, int L) {
+constexpr int kMaxPivots = 3;
+static bool pass_avoids(const FusedPass& p, uint64_t pmask) {
+    if (p.single >= 0 || p.h < 4) return false;
+    for (int i = 0; i < 6 + p.h - p.r0; ++i)
+        if ((pmask >> p.hpos[i]) & 1ull) return false;
+    return true;
+}
+static uint64_t deposit_bits(uint64_t v, uint64_t mask) {  // bit j of v -> j-th set bit of mask
+    uint64_t r = 0;
+    for (int j = 0; mask; mask &= mask - 1, ++j) r |= ((v >> j) & 1ull) << __builtin_ctzll(mask);
+    return r;
+}
+
+// Choose, for every exchange between two ops steps, its pivots (QSIM_DIST_OVERLAP=0 disables).
+// The ops steps are not split: each rank plans a step as one fused plan (tiles padded away from
+// the pivots) and runs per part only the passes at its ends that avoid them (qsim_dist_run).
+// Time model of one remap between steps A and B (pass time 1, transfer time R, K = 2^m parts,
+// t trailing passes of A and h leading passes of B avoiding the pivots):
+//     T = max(R + (nA - t) + (nB - h) + (t + h) / K,  nA + nB + R / K)
+// with R = 50 / world (an HBM pass at ~6 TB/s over a remap that sends 1/world of the shard per
+// link at ~60 GB/s).  Pivots are local positions >= 6 (never a tile's contiguous run) outside the
+// exchanged positions, added greedily (up to kMaxPivots) while T drops; each candidate set is
+// scored by planning both steps with it avoided, in parallel, on RANK 0's ops (`ref`: the same
+// skeleton on every rank), so every rank picks the same pivots.  QSIM_DIST_PIVOTS caps m
+// (default kMaxPivots); QSIM_DIST_PIVOT_PLAN=0: one pivot by the cheaper gate-level score
+// (trailing / leading gates that do not touch the position).
+static void mark_overlap(std::vector<DStep>& steps, int L, int world, const std::vector<DStep>& ref) {
     static const int enabled = [] {
         const char* e = std::getenv("QSIM_DIST_OVERLAP");
         return e ? std::atoi(e) : 1;
     }();
+    static const int by_plan = [] {
+        const char* e = std::getenv("QSIM_DIST_PIVOT_PLAN");
+        return e ? std::atoi(e) : 1;
+    }();
+    static const int max_piv = [] {
+        const char* e = std::getenv("QSIM_DIST_PIVOTS");
+        return e ? std::max(1, std::min(kMaxPivots, std::atoi(e))) : kMaxPivots;
+    }();
     if (!enabled || L < 8) return;
     const int min_gates = 4;
+    const double R = 50.0 / std::max(2, world);
     for (size_t i = 1; i + 1 < steps.size(); ++i) {
         DStep& ex = steps[i];
         DStep& A = steps[i - 1];
@@ -75,8 +107,10 @@ static void mark_overlap(std::vector<DStep>& steps, int L) {
         uint64_t lmask = 0;
         for (int j = 0; j < ex.k; ++j) lmask |= 1ull << ex.lpos[j];
         int best_p = -1, best = 0;
+        std::vector<int> cand;
         for (int p = 6; p < L; ++p) {
             if ((lmask >> p) & 1ull) continue;
+            cand.push_back(p);
             const uint64_t bit = 1ull << p;
             int a = 0, b = 0;
             while (a < (int)A.gmask.size() && !(A.gmask[A.gmask.size() - 1 - a] & bit)) ++a;
@@ -86,8 +120,61 @@ static void mark_overlap(std::vector<DStep>& steps, int L) {
                 best = a + b;
             }
         }
-        if (best_p < 0 || best < min_gates) continue;
-        ex.pivot = best_p;
+        uint64_t pmask = best_p >= 0 && best >= min_gates ? 1ull << best_p : 0ull;
+        const DStep& rA = ref[i - 1];
+        const DStep& rB = ref[i + 1];
+        if (by_plan && !rA.ops.empty() && !rB.ops.empty() && !cand.empty()) {
+            const uint64_t avoidA0 = (rA.role & 2) ? steps[i - 2].pmask : 0ull;
+            // T of a pivot set (pass counts in units of one pass); +inf when planning failed
+            auto model = [&](uint64_t set) {
+                const Plan pA = plan_fused(rA.ops, L, -1, avoidA0 | set);
+                const Plan pB = plan_fused(rB.ops, L, -1, set);
+                const int na = (int)pA.passes.size(), nb = (int)pB.passes.size();
+                int t = 0, h = 0;
+                while (t < na && pass_avoids(pA.passes[na - 1 - t], set)) ++t;
+                while (h < nb && pass_avoids(pB.passes[h], set)) ++h;
+                const double K = (double)(1 << __builtin_popcountll(set));
+                if (t + h == 0) return 1e30;
+                return std::max(R + (na - t) + (nb - h) + (t + h) / K, na + nb + R / K);
+            };
+            auto score_all = [&](uint64_t base, const std::vector<int>& cs) {
+                std::vector<double> sc(cs.size(), 1e30);
+                std::vector<std::thread> th;
+                for (size_t c = 0; c < cs.size(); ++c)
+                    th.emplace_back([&, c] {
+                        try {  // (worker threads must not throw; a failed candidate just loses)
+                            sc[c] = model(base | (1ull << cs[c]));
+                        } catch (...) {
+                        }
+                    });
+                for (auto& t : th) t.join();
+                return sc;
+            };
+            // round 1: every single position; later rounds: the 8 best singles added to the set
+            std::vector<double> sc1 = score_all(0, cand);
+            std::vector<size_t> order(cand.size());
+            for (size_t c = 0; c < order.size(); ++c) order[c] = c;
+            std::sort(order.begin(), order.end(), [&](size_t a, size_t b) { return sc1[a] < sc1[b]; });
+            double bestT = sc1[order[0]];
+            uint64_t set = bestT < 1e29 ? 1ull << cand[order[0]] : 0ull;
+            std::vector<int> pool;
+            for (size_t c = 1; c < order.size() && pool.size() < 8; ++c)
+                if (sc1[order[c]] < 1e29) pool.push_back(cand[order[c]]);
+            for (int m = 1; set && m < max_piv && !pool.empty(); ++m) {
+                const std::vector<double> sc = score_all(set, pool);
+                size_t bi = 0;
+                for (size_t c = 1; c < sc.size(); ++c)
+                    if (sc[c] < sc[bi]) bi = c;
+                if (!(sc[bi] < bestT - 1e-9)) break;
+                bestT = sc[bi];
+                set |= 1ull << pool[bi];
+                pool.erase(pool.begin() + (long)bi);
+            }
+            if (set) pmask = set;
+        }
+        if (!pmask) continue;
+        ex.pmask = pmask;
+        ex.pivot = __builtin_ctzll(pmask);
         A.role |= 1;
         B.role |= 2;
     }
@@ -230,8 +317,8 @@ static uint64_t choose_globals(const qsim_gate* gates, size_t count, const std::
 // qubit-sharing gates have all run; when a sweep leaves gates, one remap brings in the targets
 // (choose_globals) and the next sweep continues.  W-HC at 30 qubits on 8 ranks needs one remap
 // per run this way (two in plain program order).
-static std::vector<DStep> plan_dist(const qsim_gate* gates, size_t count, int n, int g, int rank,
-                                    std::vector<int>& perm) {
+static std::vector<DStep> plan_dist_core(const qsim_gate* gates, size_t count, int n, int g, int rank,
+                                         std::vector<int>& perm) {
     const int L = n - g;
     auto rank_bit = [&](int p) { return (rank >> (p - L)) & 1; };
     std::vector<DStep> steps;
@@ -331,7 +418,64 @@ static std::vector<DStep> plan_dist(const qsim_gate* gates, size_t count, int n,
     }
     if (!framed.empty() && framed.back().kind == 1) framed.push_back(DStep());
     steps.swap(framed);
-    mark_overlap(steps, L);
+    return steps;
+}
+
+// Pivots chosen for a (gate list, start map, n, g): every shard of a virtual run, and every run
+// that starts from the same map, reuses the decision instead of re-planning the candidates.
+namespace {
+struct PivotMemo {
+    int n, g;
+    std::vector<qsim_gate> gates;
+    std::vector<int> perm;
+    std::vector<uint64_t> pmask;  // per step (0: none)
+    uint64_t used;
+};
+std::mutex g_pivot_mu;
+std::vector<PivotMemo> g_pivots;
+uint64_t g_pivot_clock = 0;
+}  // namespace
+
+static std::vector<DStep> plan_dist(const qsim_gate* gates, size_t count, int n, int g, int rank,
+                                    std::vector<int>& perm) {
+    const std::vector<int> perm_in = perm;
+    std::vector<DStep> steps = plan_dist_core(gates, count, n, g, rank, perm);
+    const int L = n - g;
+    auto same = [&](const PivotMemo& m) {
+        return m.n == n && m.g == g && m.perm == perm_in && m.gates.size() == count &&
+               (count == 0 || std::memcmp(m.gates.data(), gates, count * sizeof(qsim_gate)) == 0);
+    };
+    {
+        std::lock_guard<std::mutex> l(g_pivot_mu);
+        for (PivotMemo& m : g_pivots)
+            if (same(m) && m.pmask.size() == steps.size()) {
+                m.used = ++g_pivot_clock;
+                for (size_t k = 0; k < steps.size(); ++k)
+                    if (m.pmask[k]) {
+                        steps[k].pmask = m.pmask[k];
+                        steps[k].pivot = __builtin_ctzll(m.pmask[k]);
+                        steps[k - 1].role |= 1;
+                        steps[k + 1].role |= 2;
+                    }
+                return steps;
+            }
+    }
+    if (rank == 0) {
+        mark_overlap(steps, L, 1 << g, steps);
+    } else {
+        std::vector<int> p0 = perm_in;
+        const std::vector<DStep> ref = plan_dist_core(gates, count, n, g, 0, p0);
+        if (ref.size() != steps.size()) fail(QSIM_ERR_RUNTIME, "exchange skeleton mismatch");
+        mark_overlap(steps, L, 1 << g, ref);
+    }
+    PivotMemo m{n, g, std::vector<qsim_gate>(gates, gates + count), perm_in, {}, 0};
+    for (const DStep& st : steps) m.pmask.push_back(st.kind == 1 ? st.pmask : 0ull);
+    std::lock_guard<std::mutex> l(g_pivot_mu);
+    m.used = ++g_pivot_clock;
+    if (g_pivots.size() >= 16)
+        g_pivots.erase(std::min_element(g_pivots.begin(), g_pivots.end(),
+                                        [](const PivotMemo& a, const PivotMemo& b) { return a.used < b.used; }));
+    g_pivots.push_back(std::move(m));
     return steps;
 }
 
@@ -343,17 +487,17 @@ struct XArgs {
     int chunk_log;
     int k;
     int my_c;
-    int nsorted;        // zero-insertion positions: lpos, plus the pivot of a half exchange
-    int sorted[9];      // ascending
+    int nsorted;        // zero-insertion positions: lpos, plus the pivots of a part exchange
+    int sorted[12];     // ascending
     int lpos[8];        // chunk bit j <-> lpos[j]
-    uint64_t orval;     // half exchange: the pivot bit's value
+    uint64_t orval;     // part exchange: the pivot bits' values
 };
 
 __device__ __forceinline__ uint64_t xlocal(const XArgs& a, uint64_t e) {
     const uint64_t c = e >> a.chunk_log;
     uint64_t off = e & (a.chunk - 1);
 #pragma unroll
-    for (int j = 0; j < 9; ++j)
+    for (int j = 0; j < 12; ++j)
         if (j < a.nsorted) {
             const uint64_t lo = off & ((1ull << a.sorted[j]) - 1ull);
             off = ((off ^ lo) << 1) | lo;
@@ -413,7 +557,8 @@ struct qsim_dist {
     hipStream_t comm_stream = nullptr;  // remap transfers (RCCL or, virtual, device copies)
     hipStream_t copy_stream = nullptr;  // pack / unpack of overlapped (half) remaps
     std::vector<hipEvent_t> events;     // remap pipeline: packed part p, transferred part p
-    hipEvent_t hev[8] = {};             // overlapped remap: tail done, packed, sent, unpacked x 2 halves
+    // overlapped remap, per part h < 8: tail done (pev[h]), packed (8 + h), sent (16 + h), unpacked (24 + h)
+    hipEvent_t pev[32] = {};
     int overlapped = 0;                 // remaps of the last run that overlapped local work
     ncclComm_t comm = nullptr;
     bool aborted = false;  // the communicator was aborted after an RCCL / HIP error or a timeout
@@ -457,7 +602,7 @@ struct qsim_dist {
         for (hipEvent_t e : events)
             if (e) (void)hipEventDestroy(e);
         if (copy_stream) (void)hipStreamSynchronize(copy_stream);
-        for (hipEvent_t e : hev)
+        for (hipEvent_t e : pev)
             if (e) (void)hipEventDestroy(e);
         if (copy_stream) (void)hipStreamDestroy(copy_stream);
         if (comm_stream) (void)hipStreamDestroy(comm_stream);
@@ -582,14 +727,14 @@ struct XPlan {
     XArgs a;
     int peer_of[256];
 };
-// half < 0: the whole shard; half 0 / 1: the amplitudes whose pivot bit is 0 / 1.
-XPlan xplan(const qsim_dist* d, const Shard& sh, const DStep& ex, int half = -1) {
+// part < 0: the whole shard; part j: the amplitudes whose pivot bits hold the bits of j.
+XPlan xplan(const qsim_dist* d, const Shard& sh, const DStep& ex, int part = -1) {
     XPlan x{};
     XArgs& a = x.a;
     a.st = sh.d;
     a.k = ex.k;
-    const bool h = half >= 0;
-    a.chunk_log = d->L - ex.k - (h ? 1 : 0);
+    const bool h = part >= 0;
+    a.chunk_log = d->L - ex.k - (h ? __builtin_popcountll(ex.pmask) : 0);
     a.chunk = 1ull << a.chunk_log;
     for (int j = 0; j < ex.k; ++j) {
         a.lpos[j] = ex.lpos[j];
@@ -598,8 +743,8 @@ XPlan xplan(const qsim_dist* d, const Shard& sh, const DStep& ex, int half = -1)
     }
     a.nsorted = ex.k;
     if (h) {
-        a.sorted[a.nsorted++] = ex.pivot;
-        a.orval = (uint64_t)half << ex.pivot;
+        for (uint64_t m = ex.pmask; m; m &= m - 1) a.sorted[a.nsorted++] = __builtin_ctzll(m);
+        a.orval = deposit_bits((uint64_t)part, ex.pmask);
     }
     std::sort(a.sorted, a.sorted + a.nsorted);
     for (int c = 0; c < (1 << ex.k); ++c) {
@@ -702,32 +847,33 @@ void exchange(qsim_dist* d, const DStep& ex) {
         }
     }
 }
-// One overlapped remap: the two halves of every shard (pivot bit 0, then 1) are exchanged one
-// after the other — pack and unpack on copy_stream, transfers on comm_stream — each half waiting
-// for its local work (event hev[h], recorded on the compute stream after the role-1 step's half)
-// and signalling hev[6 + h] when unpacked (the role-2 step's half waits for it).  Half h uses
-// half h of the send / receive buffers, so both halves can be in flight.
-void exchange_halves(qsim_dist* d, const DStep& ex) {
-    const uint64_t half_amps = 1ull << (d->L - 1);
-    const uint64_t chunk = half_amps >> ex.k;
-    const double bytes = 2.0 * 16.0 * (double)(half_amps - chunk) * (double)d->shards.size();
-    for (int h = 0; h < 2; ++h) {
+// One overlapped remap: the K = 2^m parts of every shard (the values of the m pivot bits) are
+// exchanged one after the other — pack and unpack on copy_stream, transfers on comm_stream —
+// each part waiting for its local work (event pev[j], recorded on the compute stream after the
+// role-1 step's part) and signalling pev[24 + j] when unpacked (the role-2 step's part waits for
+// it).  Part j uses part j of the send / receive buffers, so all parts can be in flight.
+void exchange_parts(qsim_dist* d, const DStep& ex) {
+    const int K = 1 << __builtin_popcountll(ex.pmask);
+    const uint64_t part_amps = 1ull << (d->L - __builtin_popcountll(ex.pmask));
+    const uint64_t chunk = part_amps >> ex.k;
+    const double bytes = 2.0 * 16.0 * (double)(part_amps - chunk) * (double)d->shards.size();
+    for (int h = 0; h < K; ++h) {
         TimedLaunch tl(&d->timer, "alltoall_remap", bytes, d->copy_stream);
         std::vector<XPlan> xs;
         for (Shard& sh : d->shards) xs.push_back(xplan(d, sh, ex, h));
-        QSIM_HIPCHK(hipStreamWaitEvent(d->copy_stream, d->hev[h], 0));
+        QSIM_HIPCHK(hipStreamWaitEvent(d->copy_stream, d->pev[h], 0));
         for (size_t i = 0; i < d->shards.size(); ++i) {
             XArgs a = xs[i].a;
-            a.buf = d->shards[i].sendbuf + (uint64_t)h * half_amps;
+            a.buf = d->shards[i].sendbuf + (uint64_t)h * part_amps;
             copy_kernel(true, a, 0, xs[i].a.chunk_log, d->copy_stream);
         }
-        QSIM_HIPCHK(hipEventRecord(d->hev[2 + h], d->copy_stream));
-        QSIM_HIPCHK(hipStreamWaitEvent(d->comm_stream, d->hev[2 + h], 0));
+        QSIM_HIPCHK(hipEventRecord(d->pev[8 + h], d->copy_stream));
+        QSIM_HIPCHK(hipStreamWaitEvent(d->comm_stream, d->pev[8 + h], 0));
         if (!d->virt) {
             const Shard& sh = d->shards[0];
             const XPlan& x = xs[0];
-            double2* sb = sh.sendbuf + (uint64_t)h * half_amps;
-            double2* rb = sh.recvbuf + (uint64_t)h * half_amps;
+            double2* sb = sh.sendbuf + (uint64_t)h * part_amps;
+            double2* rb = sh.recvbuf + (uint64_t)h * part_amps;
             QSIM_NCCLCHK(ncclGroupStart());
             for (int c = 0; c < (1 << ex.k); ++c) {
                 if (c == x.a.my_c) continue;
@@ -744,21 +890,21 @@ void exchange_halves(qsim_dist* d, const DStep& ex) {
                 for (int c = 0; c < (1 << ex.k); ++c) {
                     if (c == x.a.my_c) continue;
                     Shard& dst = d->shards[x.peer_of[c]];
-                    QSIM_HIPCHK(hipMemcpyAsync(dst.recvbuf + (uint64_t)h * half_amps + (uint64_t)x.a.my_c * chunk,
-                                               d->shards[i].sendbuf + (uint64_t)h * half_amps + (uint64_t)c * chunk,
+                    QSIM_HIPCHK(hipMemcpyAsync(dst.recvbuf + (uint64_t)h * part_amps + (uint64_t)x.a.my_c * chunk,
+                                               d->shards[i].sendbuf + (uint64_t)h * part_amps + (uint64_t)c * chunk,
                                                chunk * sizeof(double2), hipMemcpyDeviceToDevice,
                                                d->comm_stream));
                 }
             }
         }
-        QSIM_HIPCHK(hipEventRecord(d->hev[4 + h], d->comm_stream));
-        QSIM_HIPCHK(hipStreamWaitEvent(d->copy_stream, d->hev[4 + h], 0));
+        QSIM_HIPCHK(hipEventRecord(d->pev[16 + h], d->comm_stream));
+        QSIM_HIPCHK(hipStreamWaitEvent(d->copy_stream, d->pev[16 + h], 0));
         for (size_t i = 0; i < d->shards.size(); ++i) {
             XArgs a = xs[i].a;
-            a.buf = d->shards[i].recvbuf + (uint64_t)h * half_amps;
+            a.buf = d->shards[i].recvbuf + (uint64_t)h * part_amps;
             copy_kernel(false, a, 0, xs[i].a.chunk_log, d->copy_stream);
         }
-        QSIM_HIPCHK(hipEventRecord(d->hev[6 + h], d->copy_stream));
+        QSIM_HIPCHK(hipEventRecord(d->pev[24 + h], d->copy_stream));
     }
 }
 
@@ -785,31 +931,25 @@ struct StepRun {
     const JitModule* jm = nullptr;
     size_t j1 = 0, j2 = 0, np = 0;
 };
-static bool pass_avoids(const FusedPass& p, int pivot) {
-    if (p.single >= 0 || p.h < 4) return false;
-    for (int i = 0; i < 6 + p.h - p.r0; ++i)
-        if (p.hpos[i] == pivot) return false;
-    return true;
-}
-StepRun prepare_step(qsim_dist* d, const std::vector<Op>& ops, int flags, PlanCache& pc, int pb, int pa) {
+StepRun prepare_step(qsim_dist* d, const std::vector<Op>& ops, int flags, PlanCache& pc, uint64_t pb,
+                     uint64_t pa) {
     StepRun r;
     if (ops.empty() || !(flags & QSIM_RUN_FUSED)) return r;
-    const uint64_t avoid = (pb >= 0 ? 1ull << pb : 0ull) | (pa >= 0 ? 1ull << pa : 0ull);
-    PlanCache::Entry& pe = pc.get(ops, d->L, d->stream, avoid);
+    PlanCache::Entry& pe = pc.get(ops, d->L, d->stream, pb | pa);
     r.plan = &pe.plan;
     r.jm = jit_for(pe.jit, pe.plan, d->L);
     r.np = pe.plan.passes.size();
-    if (pb >= 0)
+    if (pb)
         while (r.j1 < r.np && pass_avoids(pe.plan.passes[r.j1], pb)) ++r.j1;
     r.j2 = r.np;
-    if (pa >= 0)
+    if (pa)
         while (r.j2 > r.j1 && pass_avoids(pe.plan.passes[r.j2 - 1], pa)) --r.j2;
     return r;
 }
-// Launch passes [first, last) of a prepared step (half >= 0: the half whose `pivot` bit is half);
-// per-gate mode: the whole op list when called for the middle part.
+// Launch passes [first, last) of a prepared step (part >= 0: the part whose pivot bits `pmask`
+// hold the bits of part); per-gate mode: the whole op list when called for the middle part.
 void run_part(qsim_dist* d, Shard& sh, const std::vector<Op>& ops, const StepRun& r, size_t first,
-              size_t last, int pivot = -1, int half = -1) {
+              size_t last, uint64_t pmask = 0, int part = -1) {
     if (ops.empty() || first >= last) return;
     if (!r.plan) {
         for (const Op& op : ops) launch_op(sh.d, d->L, 1, op, d->stream, &d->timer);
@@ -820,9 +960,9 @@ void run_part(qsim_dist* d, Shard& sh, const std::vector<Op>& ops, const StepRun
     FusedRange rg;
     rg.first = first;
     rg.last = last;
-    if (half >= 0) {
-        rg.fix_mask = 1ull << pivot;
-        rg.fix_val = (uint64_t)half << pivot;
+    if (part >= 0) {
+        rg.fix_mask = pmask;
+        rg.fix_val = deposit_bits((uint64_t)part, pmask);
     }
     launch_fused(sh.d, d->L, 1, *r.plan, (const TileOp*)d->ops.ptr, (const Stage*)d->stages.ptr, d->stream,
                  &d->timer, r.jm, nullptr, rg);
@@ -891,7 +1031,7 @@ int qsim_dist_create(int n_qubits, int rank, int world, const void* unique_id, i
         QSIM_HIPCHK(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
         QSIM_HIPCHK(hipStreamCreateWithFlags(&d->comm_stream, hipStreamNonBlocking));
         QSIM_HIPCHK(hipStreamCreateWithFlags(&d->copy_stream, hipStreamNonBlocking));
-        for (hipEvent_t& e : d->hev) QSIM_HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        for (hipEvent_t& e : d->pev) QSIM_HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         d->timer.stream = d->stream;
         alloc_shards(d.get(), {rank});
         ncclUniqueId id;
@@ -939,7 +1079,7 @@ int qsim_dist_create_virtual(int n_qubits, int world, int device, qsim_dist** ou
         QSIM_HIPCHK(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
         QSIM_HIPCHK(hipStreamCreateWithFlags(&d->comm_stream, hipStreamNonBlocking));
         QSIM_HIPCHK(hipStreamCreateWithFlags(&d->copy_stream, hipStreamNonBlocking));
-        for (hipEvent_t& e : d->hev) QSIM_HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        for (hipEvent_t& e : d->pev) QSIM_HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         d->timer.stream = d->stream;
         std::vector<int> ranks(world);
         for (int r = 0; r < world; ++r) ranks[r] = r;
@@ -990,12 +1130,10 @@ int qsim_dist_run(qsim_dist* d, const qsim_gate* gates, size_t count, int flags)
         for (size_t i = 1; i < S; ++i)
             if (plans[i].size() != plans[0].size()) fail(QSIM_ERR_RUNTIME, "exchange skeleton mismatch");
         d->overlapped = 0;
-        bool pending = false;  // an overlapped remap's halves still to be waited for
+        int pending = 0;  // parts of an overlapped remap still to be waited for (0: none)
         auto wait_pending = [&]() {
-            if (!pending) return;
-            QSIM_HIPCHK(hipStreamWaitEvent(d->stream, d->hev[6], 0));
-            QSIM_HIPCHK(hipStreamWaitEvent(d->stream, d->hev[7], 0));
-            pending = false;
+            for (int h = 0; h < pending; ++h) QSIM_HIPCHK(hipStreamWaitEvent(d->stream, d->pev[24 + h], 0));
+            pending = 0;
         };
         // Every rank's plan has the same step skeleton (mark_overlap decides from
         // rank-independent data): walk the steps in lockstep.
@@ -1005,15 +1143,15 @@ int qsim_dist_run(qsim_dist* d, const qsim_gate* gates, size_t count, int flags)
                 if (plans[i][k].kind != s0.kind || plans[i][k].role != s0.role)
                     fail(QSIM_ERR_RUNTIME, "exchange skeleton mismatch");
             if (s0.kind == 1) {
-                if (s0.pivot >= 0) {
-                    // the ops step before (role bit 1) recorded hev[0] / hev[1] after its tail
-                    // halves; otherwise both halves are ready now
-                    if (k == 0 || !(plans[0][k - 1].role & 1)) {
-                        QSIM_HIPCHK(hipEventRecord(d->hev[0], d->stream));
-                        QSIM_HIPCHK(hipEventRecord(d->hev[1], d->stream));
-                    }
-                    exchange_halves(d, s0);
-                    pending = true;
+                if (s0.pmask) {
+                    // the ops step before (role bit 1) recorded pev[j] after its tail part j;
+                    // otherwise every part is ready now
+                    const int K = 1 << __builtin_popcountll(s0.pmask);
+                    wait_pending();
+                    if (k == 0 || !(plans[0][k - 1].role & 1))
+                        for (int h = 0; h < K; ++h) QSIM_HIPCHK(hipEventRecord(d->pev[h], d->stream));
+                    exchange_parts(d, s0);
+                    pending = K;
                     ++d->overlapped;
                 } else {
                     wait_pending();
@@ -1022,14 +1160,14 @@ int qsim_dist_run(qsim_dist* d, const qsim_gate* gates, size_t count, int flags)
                 continue;
             }
             // ops step: head per half (after the exchange before), middle, tail per half
-            const int pb = (s0.role & 2) ? plans[0][k - 1].pivot : -1;
-            const int pa = (s0.role & 1) ? plans[0][k + 1].pivot : -1;
+            const uint64_t pb = (s0.role & 2) ? plans[0][k - 1].pmask : 0ull;
+            const uint64_t pa = (s0.role & 1) ? plans[0][k + 1].pmask : 0ull;
             std::vector<StepRun> runs(S);
             for (size_t i = 0; i < S; ++i) runs[i] = prepare_step(d, plans[i][k].ops, flags, *rp.fplans[i][k], pb, pa);
-            const bool head = pb >= 0 && pending;
+            const bool head = pb && pending;
             if (head) {
-                for (int h = 0; h < 2; ++h) {
-                    QSIM_HIPCHK(hipStreamWaitEvent(d->stream, d->hev[6 + h], 0));
+                for (int h = 0; h < pending; ++h) {
+                    QSIM_HIPCHK(hipStreamWaitEvent(d->stream, d->pev[24 + h], 0));
                     for (size_t i = 0; i < S; ++i)
                         if (runs[i].plan) run_part(d, d->shards[i], plans[i][k].ops, runs[i], 0, runs[i].j1, pb, h);
                 }
@@ -1039,11 +1177,11 @@ int qsim_dist_run(qsim_dist* d, const qsim_gate* gates, size_t count, int flags)
                 if (runs[i].plan) run_part(d, d->shards[i], plans[i][k].ops, runs[i], head ? runs[i].j1 : 0, runs[i].j2);
                 else run_part(d, d->shards[i], plans[i][k].ops, runs[i], 0, 1);  // per-gate: the whole list
             }
-            if (pa >= 0) {  // the exchange after waits for hev[h]
-                for (int h = 0; h < 2; ++h) {
+            if (pa) {  // the exchange after waits for pev[h]
+                for (int h = 0; h < (1 << __builtin_popcountll(pa)); ++h) {
                     for (size_t i = 0; i < S; ++i)
                         if (runs[i].plan) run_part(d, d->shards[i], plans[i][k].ops, runs[i], runs[i].j2, runs[i].np, pa, h);
-                    QSIM_HIPCHK(hipEventRecord(d->hev[h], d->stream));
+                    QSIM_HIPCHK(hipEventRecord(d->pev[h], d->stream));
                 }
             }
         }
@@ -1215,6 +1353,7 @@ int qsim_dist_plan(int n, int world, int rank, const qsim_gate* gates, size_t co
                     o.lpos[j] = s.lpos[j];
                 }
                 o.pivot = s.pivot;
+                o.pmask = s.pmask;
                 o.role = s.role;
             }
             for (const Op& op : s.ops) {
@@ -1235,6 +1374,40 @@ int qsim_dist_plan(int n, int world, int rank, const qsim_gate* gates, size_t co
         }
         if (n_steps) *n_steps = si;
         if (n_ops) *n_ops = oi;
+        if (perm_inout)
+            for (int q = 0; q < n; ++q) perm_inout[q] = perm[q];
+    });
+}
+
+int qsim_dist_plan_passes(int n, int world, int rank, const qsim_gate* gates, size_t count,
+                          int32_t* perm_inout, int32_t* passes, size_t cap, size_t* n_steps) {
+    return dguard([&] {
+        const int g = log2_exact(world);
+        check_sizes(n, g);
+        if (rank < 0 || rank >= world) fail(QSIM_ERR_INVALID_ARGUMENT, "rank out of range");
+        std::vector<int> perm(n);
+        for (int q = 0; q < n; ++q) perm[q] = perm_inout ? perm_inout[q] : q;
+        const std::vector<DStep> st = plan_dist(gates, count, n, g, rank, perm);
+        const int L = n - g;
+        for (size_t k = 0; k < st.size(); ++k) {
+            int np = 0, head = 0, tail = 0;
+            if (st[k].kind == 0 && !st[k].ops.empty()) {  // as prepare_step plans it
+                const uint64_t pb = (st[k].role & 2) ? st[k - 1].pmask : 0ull;
+                const uint64_t pa = (st[k].role & 1) ? st[k + 1].pmask : 0ull;
+                const Plan pl = plan_fused(st[k].ops, L, -1, pb | pa);
+                np = (int)pl.passes.size();
+                if (pb)
+                    while (head < np && pass_avoids(pl.passes[head], pb)) ++head;
+                if (pa)
+                    while (tail < np - head && pass_avoids(pl.passes[np - 1 - tail], pa)) ++tail;
+            }
+            if (k < cap && passes) {
+                passes[3 * k] = st[k].kind == 1 ? -1 : np;
+                passes[3 * k + 1] = head;
+                passes[3 * k + 2] = tail;
+            }
+        }
+        if (n_steps) *n_steps = st.size();
         if (perm_inout)
             for (int q = 0; q < n; ++q) perm_inout[q] = perm[q];
     });

@@ -157,7 +157,8 @@ class qsim_op(Structure):
 
 class qsim_dist_step(Structure):
     _fields_ = [("kind", c_int32), ("k", c_int32), ("op_begin", c_int32), ("op_end", c_int32),
-                ("gpos", c_int32 * 8), ("lpos", c_int32 * 8), ("pivot", c_int32), ("role", c_int32)]
+                ("gpos", c_int32 * 8), ("lpos", c_int32 * 8), ("pivot", c_int32), ("role", c_int32),
+                ("pmask", c_uint64)]
 
 
 _sig(hip, "qsim_dist_unique_id", [_P])
@@ -180,6 +181,8 @@ _sig(hip, "qsim_dist_profile_get", [_P, c_int, c_char_p, c_size_t, POINTER(c_dou
 _sig(hip, "qsim_dist_plan", [c_int, c_int, c_int, POINTER(qsim_gate), c_size_t, POINTER(c_int32),
                              POINTER(qsim_dist_step), c_size_t, POINTER(c_size_t),
                              POINTER(qsim_op), c_size_t, POINTER(c_size_t)])
+_sig(hip, "qsim_dist_plan_passes", [c_int, c_int, c_int, POINTER(qsim_gate), c_size_t,
+                                    POINTER(c_int32), POINTER(c_int32), c_size_t, POINTER(c_size_t)])
 
 # ---- C++ API library (libqsim.so): circuit factories
 _sig(api, "qsim_circuit_make", [c_int, c_int, c_int, c_uint, POINTER(qsim_gate), c_size_t,

@@ -300,16 +300,18 @@ typedef struct qsim_op {
 } qsim_op;
 /* One plan step: kind 0 = ops[op_begin, op_end) on the local shard; kind 1 = exchange that
  * swaps global physical positions gpos[i] with local positions lpos[i], i < k.  Overlapped
- * remaps: an exchange with pivot >= 0 runs as two half-exchanges (pivot bit 0, then 1).  An ops
- * step with role bit 1 runs the trailing passes of its fused plan that avoid the pivot of the
- * exchange after it per half (each half's transfer then overlaps the other half's passes); role
- * bit 2: its leading passes that avoid the pivot of the exchange before it run per half as each
- * half lands.  The step is planned as one fused plan either way (ops steps report pivot -1). */
+ * remaps: an exchange with pivots (pmask != 0: up to 3 local physical positions; pivot = the
+ * lowest, -1 if none) runs as 2^m part-exchanges, one per value of the pivot bits.  An ops step
+ * with role bit 1 runs the trailing passes of its fused plan that avoid the pivots of the
+ * exchange after it per part (each part's transfer then overlaps the later parts' passes); role
+ * bit 2: its leading passes that avoid the pivots of the exchange before it run per part as each
+ * part lands.  The step is planned as one fused plan either way (ops steps report pivot -1). */
 typedef struct qsim_dist_step {
     int32_t kind, k;
     int32_t op_begin, op_end;
     int32_t gpos[8], lpos[8];
     int32_t pivot, role;
+    uint64_t pmask;
 } qsim_dist_step;
 
 int qsim_dist_unique_id(void* id_out);  /* ncclGetUniqueId, on rank 0 */
@@ -339,6 +341,13 @@ int qsim_dist_profile_get(qsim_dist* d, int i, char* name, size_t name_len, doub
 int qsim_dist_plan(int n_qubits, int world, int rank, const qsim_gate* gates, size_t count,
                    int32_t* perm_inout, qsim_dist_step* steps, size_t step_cap, size_t* n_steps,
                    qsim_op* ops, size_t op_cap, size_t* n_ops);
+
+/* Host-only: per step of that plan, as qsim_dist_run would plan it, three ints: fused passes
+ * (-1 for an exchange step), leading passes that run per half as the exchange before lands, and
+ * trailing passes that run per half before the exchange after (the overlapped work);
+ * `cap` counts steps.  perm_inout updated as by qsim_dist_plan. */
+int qsim_dist_plan_passes(int n_qubits, int world, int rank, const qsim_gate* gates, size_t count,
+                          int32_t* perm_inout, int32_t* passes, size_t cap, size_t* n_steps);
 
 #define QSIM_MAX_QUBITS_SINGLE 30
 #define QSIM_MIN_QUBITS 1
