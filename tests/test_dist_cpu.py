@@ -120,6 +120,31 @@ def test_plan_w_hc_30q_one_remap_per_run(qsim, seed):
         assert all(s["k"] == 3 for s in steps if s["kind"] == "exchange")
 
 
+def test_plan_pivots_rank_independent(qsim):
+    """Overlapped remaps run in 2^m parts around m <= 3 pivot positions chosen by planning the
+    neighbouring steps on rank 0's ops: every rank gets the same pivots (the part exchanges pair
+    up across ranks); pivots are local positions >= 6 outside the exchanged ones, and the steps on
+    both sides are marked to run their avoiding passes per part."""
+    import qsim_amd.dist as qd
+    n, world = 22, 8
+    c = qsim.createRandomHCCircuit(n, 100, 7)
+    perm0 = list(range(n))
+    ref = None
+    for r in range(world):
+        steps, perm = qd.plan(c, world, r, list(perm0))
+        piv = [(i, tuple(s["pivots"])) for i, s in enumerate(steps) if s["kind"] == "exchange"]
+        ref = ref or piv
+        assert piv == ref
+        for i, pv in piv:
+            s = steps[i]
+            if not pv:
+                continue
+            assert 1 <= len(pv) <= 3 and s["pivot"] == pv[0]
+            assert all(6 <= p < n - 3 and p not in s["lpos"] for p in pv)
+            assert steps[i - 1]["role"] & 1 and steps[i + 1]["role"] & 2
+    assert any(pv for _, pv in ref)
+
+
 def test_plan_reorder_is_exact(qsim, oracle):
     """The executed op sequence of every rank, mapped back through the planner's qubit maps,
     is a reordering of the circuit that only swaps gates on disjoint qubits."""
