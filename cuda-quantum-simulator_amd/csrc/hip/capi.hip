@@ -903,7 +903,7 @@ int qsim_dm_run(qsim_state* s, int n, const qsim_gate* gates, size_t count,
         DeviceGuard dg(s->device);
         prep(s, true);
         std::vector<Op> ops;
-        dm_lower(n, gates, count, channels, n_channels, ops);
+        dm_lower(n, gates, count, channels, n_channels, ops, (flags & QSIM_DM_REFERENCE_Y) != 0);
         if (flags & QSIM_RUN_FUSED) run_fused(s, ops);
         else for (const Op& op : ops) launch_op(s->d, s->n, 1, op, s->stream, &s->timer);
     });

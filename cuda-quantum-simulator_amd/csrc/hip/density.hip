@@ -90,7 +90,7 @@ static void dm_channel(std::vector<Op>& out, int n, int type, int q, double p) {
 }
 
 void dm_lower(int n, const qsim_gate* gates, size_t count, const qsim_noise_channel* ch,
-              size_t nch, std::vector<Op>& out) {
+              size_t nch, std::vector<Op>& out, bool reference_y) {
     for (size_t c = 0; c < nch; ++c) {
         if (ch[c].type < 0 || ch[c].type > 5) fail(QSIM_ERR_INVALID_ARGUMENT, "unknown noise type");
         if (ch[c].qubit < -1 || ch[c].qubit >= n)
@@ -104,6 +104,16 @@ void dm_lower(int n, const qsim_gate* gates, size_t count, const qsim_noise_chan
         o.src = (int)i;
         out.push_back(dm_row(o, n));
         out.push_back(dm_col(o));
+        if (reference_y && g.type == QSIM_GATE_Y) {  // dmApplyY's extra sign (-Y rho Y^dag)
+            Op neg;
+            neg.kind = K_DIAG;
+            neg.sub = S_GEN;
+            neg.t0 = 0;
+            neg.d0_one = false;
+            neg.m[0] = neg.m[2] = -1.0;
+            neg.src = (int)i;
+            out.push_back(neg);
+        }
         for (int k = 0; k < g.nqubits; ++k)
             for (size_t c = 0; c < nch; ++c)
                 if (ch[c].qubit < 0 || ch[c].qubit == g.qubits[k])

@@ -258,7 +258,7 @@ void launch_noise_after_gate(double2* st, int n, const std::vector<NoiseChan>& c
 
 // Density matrices as 2n-index-bit states (density.hip).
 void dm_lower(int n, const qsim_gate* gates, size_t count, const qsim_noise_channel* ch,
-              size_t nch, std::vector<Op>& out);
+              size_t nch, std::vector<Op>& out, bool reference_y = false);
 void dm_lower_channel(int n, int type, int qubit, double p, std::vector<Op>& out);
 void launch_dm_diag(const double2* rho, int n, double* out, hipStream_t s);
 void launch_dm_init(double2* rho, const double2* psi, int n, hipStream_t s);

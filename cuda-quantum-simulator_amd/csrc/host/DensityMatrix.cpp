@@ -62,12 +62,13 @@ void DensityMatrixSimulator::run(const Circuit& circuit) {
         for (int q : c.qubits) ch.push_back(qsim_noise_channel{static_cast<int>(c.type), q, c.probability});
     }
     check(qsim_dm_run(rho_.state().handle(), rho_.getNumQubits(), gates.data(), gates.size(),
-                      ch.data(), ch.size(), QSIM_RUN_FUSED));
+                      ch.data(), ch.size(), QSIM_RUN_FUSED | (reference_y_ ? QSIM_DM_REFERENCE_Y : 0)));
 }
 
 void DensityMatrixSimulator::applyGate(const GateOp& gate) {
     const qsim_gate g = detail::toAbi(gate);
-    check(qsim_dm_run(rho_.state().handle(), rho_.getNumQubits(), &g, 1, nullptr, 0, QSIM_RUN_PER_GATE));
+    check(qsim_dm_run(rho_.state().handle(), rho_.getNumQubits(), &g, 1, nullptr, 0,
+                      QSIM_RUN_PER_GATE | (reference_y_ ? QSIM_DM_REFERENCE_Y : 0)));
 }
 
 int DensityMatrixSimulator::measureQubit(int qubit) {

@@ -24,6 +24,7 @@ QSIM_ERR_DEVICE = 4
 
 QSIM_RUN_PER_GATE = 0
 QSIM_RUN_FUSED = 1
+QSIM_DM_REFERENCE_Y = 8  # qsim_dm_run flag
 QSIM_BATCH_FULL_GATESET = 0
 QSIM_BATCH_REFERENCE_GATESET = 1
 QSIM_BATCH_PER_GATE = 2

@@ -76,10 +76,11 @@ class DensityMatrix:
 
 class DensityMatrixSimulator:
     def __init__(self, n_qubits: int, noise: Optional[NoiseModel] = None,
-                 mode: RunMode = RunMode.Fused):
+                 mode: RunMode = RunMode.Fused, reference_y: bool = False):
         self._rho = DensityMatrix(n_qubits)
         self._noise = noise or NoiseModel()
         self._mode = RunMode(mode)
+        self._ref_y = bool(reference_y)
         self._rng = np.random.default_rng(int.from_bytes(os.urandom(4), "little"))
 
     @property
@@ -87,6 +88,13 @@ class DensityMatrixSimulator:
         return self._rho
 
     def setSeed(self, seed: int) -> None: self._rng = np.random.default_rng(seed)
+
+    def setReferenceCompatible(self, on: bool = True) -> None:
+        """Y as the reference's dmApplyY (-Y rho Y^dag, src/DensityMatrix.cu:507-546)."""
+        self._ref_y = bool(on)
+
+    def _flags(self) -> int:
+        return int(self._mode) | (_lib.QSIM_DM_REFERENCE_Y if self._ref_y else 0)
     def reset(self) -> None: self._rho.reset()
 
     def _channels(self):
@@ -105,14 +113,14 @@ class DensityMatrixSimulator:
         g, ng = circuit.to_abi()
         ch, nch = self._channels()
         _lib.check(_lib.hip.qsim_dm_run(self._rho.state.handle, self._rho.getNumQubits(), g, ng,
-                                        ch, nch, int(self._mode)))
+                                        ch, nch, self._flags()))
 
     def applyGate(self, op: GateOp) -> None:
         c = Circuit(self._rho.getNumQubits())
         c.append(op)
         g, ng = c.to_abi()
         _lib.check(_lib.hip.qsim_dm_run(self._rho.state.handle, self._rho.getNumQubits(), g, ng,
-                                        None, 0, int(self._mode)))
+                                        None, 0, self._flags()))
 
     def applyChannel(self, type, qubit: int, p: float) -> None:
         _lib.check(_lib.hip.qsim_dm_apply_channel(self._rho.state.handle, self._rho.getNumQubits(),

@@ -64,11 +64,17 @@ public:
 
     void setSeed(unsigned int seed) { rng_.seed(seed); }
     DensityMatrix& density() { return rho_; }
+    // Reference results: Y as src/DensityMatrix.cu:507-546 computes it (-Y rho Y^dag); the
+    // default is the physical Y rho Y^dag.  (Amplitude damping has no switch: the reference's
+    // kernel reads rho11 while another thread rescales it, :1023-1036, so its result is not
+    // deterministic; this engine uses the pre-channel rho11, the race-free reading.)
+    void setReferenceCompatible(bool on = true) { reference_y_ = on; }
 
 private:
     DensityMatrix rho_;
     NoiseModel noise_model_;
     std::mt19937 rng_;
+    bool reference_y_ = false;
 };
 
 }  // namespace qsim

@@ -272,7 +272,12 @@ int qsim_noisy_run(qsim_state* s, const qsim_gate* gates, size_t count,
 #define QSIM_DM_MAX_QUBITS 15
 /* DensityMatrixSimulator::run (src/DensityMatrix.cu:201-212): each gate as U rho U^dag, then for
  * each of its qubits every channel entry on that qubit or with qubit = -1 (a global channel).
- * CRY/CRZ/Toffoli -> QSIM_ERR_RUNTIME (:264-266).  flags = QSIM_RUN_*.  Asynchronous. */
+ * CRY/CRZ/Toffoli -> QSIM_ERR_RUNTIME (:264-266).  flags = QSIM_RUN_* | QSIM_DM_REFERENCE_Y.
+ * Asynchronous. */
+/* QSIM_DM_REFERENCE_Y: Y acts as the reference's dmApplyY, rho -> -Y rho Y^dag
+ * (src/DensityMatrix.cu:507-546: its phases are those of Y rho Y^dag times -1, so the trace
+ * changes sign); default: Y rho Y^dag. */
+#define QSIM_DM_REFERENCE_Y 8
 int qsim_dm_run(qsim_state* rho, int n_qubits, const qsim_gate* gates, size_t count,
                 const qsim_noise_channel* channels, size_t n_channels, int flags);
 /* One channel (applyDepolarizing ... applyBitPhaseFlip, :298-356) on `qubit`. */

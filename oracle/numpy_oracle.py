@@ -419,14 +419,18 @@ def dm_channel(rho, n, ntype, q, p):
     return out
 
 
-def dm_run(n, gates, channels=(), rho=None):
-    """DensityMatrixSimulator::run (src/DensityMatrix.cu:201-212); channel qubit -1 = global."""
+def dm_run(n, gates, channels=(), rho=None, reference_y=False):
+    """DensityMatrixSimulator::run (src/DensityMatrix.cu:201-212); channel qubit -1 = global.
+    reference_y: Y as dmApplyY computes it, -Y rho Y^dag (src/DensityMatrix.cu:540-544: the
+    element (r, c) <- phase2 * rho[r^1][c^1] with phase2 = +-1 opposite to Y rho Y^dag's)."""
     d = 1 << n
     if rho is None:
         rho = np.zeros((d, d), complex)
         rho[0, 0] = 1.0
     for g in gates:
         rho = dm_apply_gate(rho, n, g)
+        if reference_y and g[0] == 1:
+            rho = -rho
         for q in g[1]:
             for (t, cq, p) in channels:
                 if cq < 0 or cq == q:

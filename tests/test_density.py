@@ -134,3 +134,55 @@ def test_density_matrix_api(qsim, gpu_ready):
     assert sim.measureQubit(1) == m0
     p = sim.getProbabilities()
     assert abs(p[3 * m0] - 1) < 1e-12 and abs(sim.getPurity() - 1) < 1e-12
+
+
+def _dm_apply_y_reference_loop(rho, n, target):
+    """Element loop of dmApplyY (src/DensityMatrix.cu:507-546) on a host array: the pair
+    (row, col) <-> (row ^ m, col ^ m), written once from the lower index."""
+    out = rho.copy()
+    dim = 1 << n
+    m = 1 << target
+    for row in range(dim):
+        for col in range(dim):
+            nr, nc = row ^ m, col ^ m
+            if row < nr or (row == nr and col < nc):
+                rb, cb = (row >> target) & 1, (col >> target) & 1
+                ph1 = (1 if rb else -1) * (-1 if cb else 1)
+                ph2 = (1 if not rb else -1) * (-1 if not cb else 1)
+                v1, v2 = rho[row, col], rho[nr, nc]
+                out[row, col] = ph2 * v2
+                out[nr, nc] = ph1 * v1
+    return out
+
+
+@pytest.mark.parametrize("n,target", [(1, 0), (2, 1), (3, 0)])
+def test_oracle_reference_y_is_the_kernel_formula(oracle, n, target):
+    """The oracle's reference_y (-Y rho Y^dag) equals dmApplyY's element formula."""
+    rng = np.random.default_rng(n + target)
+    d = 1 << n
+    a = rng.normal(size=(d, d)) + 1j * rng.normal(size=(d, d))
+    rho = a @ a.conj().T
+    rho /= np.trace(rho)
+    want = _dm_apply_y_reference_loop(rho, n, target)
+    got = oracle.dm_run(n, [(1, [target], 0.0)], rho=rho, reference_y=True)
+    np.testing.assert_allclose(got, want, atol=1e-14)
+    phys = oracle.dm_run(n, [(1, [target], 0.0)], rho=rho)
+    np.testing.assert_allclose(phys, -want, atol=1e-14)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,seed", [(2, 5), (5, 6)])
+def test_reference_compatible_y(qsim, oracle, gpu_ready, n, seed):
+    """setReferenceCompatible(): Y as the reference computes it (-Y rho Y^dag); every other gate
+    and channel unchanged.  Fused and per-gate."""
+    c = _circuit(qsim, n, 30, seed)
+    c.y(0)
+    channels = [(0, -1, 0.05), (3, 0, 0.1)]
+    want = oracle.dm_run(n, oracle.gates_of(c), channels, reference_y=True)
+    for mode in (qsim.RunMode.Fused, qsim.RunMode.PerGate):
+        sim = qsim.DensityMatrixSimulator(n, _noise(qsim, channels), mode=mode)
+        sim.setReferenceCompatible()
+        sim.run(c)
+        np.testing.assert_allclose(sim.getDensityMatrix(), want, atol=1e-12, rtol=0)
+    ny = sum(1 for g in c.getGates() if g.type == qsim.GateType.Y)
+    assert abs(np.trace(want).real - (-1) ** ny) < 1e-10
