@@ -166,12 +166,13 @@ __device__ __forceinline__ void clifford_update(const StepClifford& c, uint64_t&
     }
 }
 
+// carry: start from the frame in fin_xz / fin_e (the last run's, not materialised) instead of 1.
 __global__ void k_frame_build(int count, int batch, uint64_t* frames, const int* ephase,
-                              const StepClifford* cl, uint64_t* fin_xz, int* fin_e) {
+                              const StepClifford* cl, uint64_t* fin_xz, int* fin_e, int carry) {
     const int b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= batch) return;
-    uint64_t F = 0, G = 0;
-    int E = 0;
+    uint64_t F = carry ? fin_xz[2 * b] : 0ull, G = carry ? fin_xz[2 * b + 1] : 0ull;
+    int E = carry ? fin_e[b] : 0;
     for (int s = 0; s < count; ++s) {
         const uint64_t i = (uint64_t)s * batch + b;
         uint64_t* fr = frames + 2 * i;
@@ -255,6 +256,11 @@ struct qsim_batch {
     // physical perm[q] (empty: identity); basis: every trajectory is |0..0> (create / reset).
     std::vector<int> perm;
     bool basis = true;
+    // The Pauli frames of the last fused noisy run (d_xz, d_e; physical positions) are not yet
+    // materialised: every trajectory's state is Phi * stored vector.  The next fused run starts
+    // its frame build from them (frames compose: no Pauli pass per run); everything that reads
+    // or writes amplitudes otherwise materialises them first (materialize), and so does sync.
+    bool frame_pending = false;
     ~qsim_batch() {
         if (stream) (void)hipStreamSynchronize(stream);
         if (d) (void)hipFree(d);
@@ -291,9 +297,22 @@ qsim_gate map_gate(const qsim_batch* b, const qsim_gate& g) {
             if (g.qubits[j] >= 0 && g.qubits[j] < b->n) m.qubits[j] = b->perm[g.qubits[j]];
     return m;
 }
+// Apply the carried Pauli frames to the stored vectors (one pass), frames back to 1.
+void materialize(qsim_batch* b) {
+    if (!b->frame_pending) return;
+    b->frame_pending = false;
+    const uint64_t N = 1ull << b->n;
+    const uint64_t items_per_traj = N / 2 > 0 ? N / 2 : 1;
+    const uint64_t total = items_per_traj * (uint64_t)b->batch;
+    TimedLaunch tl(&b->timer, "pauli_apply", 0.0, b->stream);
+    hipLaunchKernelGGL(k_pauli_apply, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, b->stream, b->d, b->n,
+                       b->d_xz, b->d_e, items_per_traj);
+    QSIM_HIPCHK(hipGetLastError());
+}
 // Undo the relabeling in every trajectory (fused SWAP network over the batch, exact data
-// movement) before anything reads or writes amplitudes by index.
+// movement) before anything reads or writes amplitudes by index; carried frames first.
 void canonicalize(qsim_batch* b) {
+    materialize(b);
     if (b->perm.empty()) return;
     const int n = b->n;
     std::vector<int> p = b->perm, inv(n);
@@ -358,6 +377,7 @@ int qsim_batch_reset(qsim_batch* b) {
         need(b);
         launch_init_basis(b->d, b->n, b->batch, 0, b->stream);
         QSIM_HIPCHK(hipStreamSynchronize(b->stream));
+        b->frame_pending = false;
         b->perm.clear();
         b->basis = true;
     });
@@ -400,6 +420,8 @@ int qsim_batch_run(qsim_batch* b, const qsim_gate* gates, size_t count,
         const bool fused_path = b->n >= 10 && fused_env && !(flags & QSIM_BATCH_PER_GATE) &&
                                 !(flags & QSIM_BATCH_REFERENCE_NOISE);
         if (flags & QSIM_BATCH_REFERENCE_NOISE) canonicalize(b);  // per-pair draws name positions
+        const bool frame_path = fused_path && b->n >= 10;  // (as the branch below)
+        if (!frame_path) materialize(b);  // per-gate paths act on the plain vectors
         if (fused_path && b->basis && b->perm.empty() && count > 0) {
             // First fused run of |0..0> trajectories: relabel for the plan's tile layouts when
             // the whole batch is HBM-sized (as the JIT threshold, it counts every trajectory).
@@ -475,7 +497,8 @@ int qsim_batch_run(qsim_batch* b, const qsim_gate* gates, size_t count,
             // Fused tile passes over all trajectories (a tile never straddles two).  Noise is
             // carried as per-trajectory Pauli frames: no noise kernel per gate, one frame build
             // before and one materialising Pauli pass after the circuit.
-            const bool noisy = !ch.empty() && count > 0;
+            // a carried frame must be propagated (Cliffords) and conjugated (the rest) like noise
+            const bool noisy = (!ch.empty() || b->frame_pending) && count > 0;
             std::vector<Op> fops;
             std::vector<StepClifford> cl(count, StepClifford{CL_NONE, 0, -1, 0});
             for (size_t i = 0; i < ops.size(); ++i) {
@@ -511,7 +534,7 @@ int qsim_batch_run(qsim_batch* b, const qsim_gate* gates, size_t count,
                 b->cliff.upload(cl.data(), cl.size() * sizeof(StepClifford), b->stream);
                 hipLaunchKernelGGL(k_frame_build, dim3((b->batch + 63) / 64), dim3(64), 0, b->stream,
                                    (int)count, b->batch, b->d_frames, b->d_fe,
-                                   (const StepClifford*)b->cliff.ptr, b->d_xz, b->d_e);
+                                   (const StepClifford*)b->cliff.ptr, b->d_xz, b->d_e, b->frame_pending ? 1 : 0);
                 QSIM_HIPCHK(hipGetLastError());
             }
             if (!fops.empty()) {
@@ -533,12 +556,8 @@ int qsim_batch_run(qsim_batch* b, const qsim_gate* gates, size_t count,
                     for (hipFunction_t f : jm->fn) b->last_jit_passes += f != nullptr;
             }
             if (noisy) {
-                b->step += count;
-                const uint64_t total = items_per_traj * (uint64_t)b->batch;
-                TimedLaunch tl(&b->timer, "pauli_apply", 0.0, b->stream);
-                hipLaunchKernelGGL(k_pauli_apply, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
-                                   b->stream, b->d, b->n, b->d_xz, b->d_e, items_per_traj);
-                QSIM_HIPCHK(hipGetLastError());
+                if (!ch.empty()) b->step += count;
+                b->frame_pending = true;  // materialised by the next reader (or composed by the next run)
             }
             return;
         }
@@ -655,6 +674,7 @@ int qsim_batch_last_run(qsim_batch* b, int* passes, int* jit_passes) {
 int qsim_batch_sync(qsim_batch* b) {
     return bguard([&] {
         need(b);
+        materialize(b);  // the carried frames are queued work too
         QSIM_HIPCHK(hipStreamSynchronize(b->stream));
     });
 }

@@ -62,6 +62,38 @@ def test_frames_equal_per_gate(qsim, gpu_ready, n, B, seed):
     assert abs(avg.sum() - 1.0) < 1e-10
 
 
+def test_carried_frames_through_mixed_runs(qsim, gpu_ready):
+    """A fused noisy run leaves its Pauli frames unmaterialised: the next fused run composes them
+    (also a noise-free one, whose non-Clifford gates are then conjugated by the carried frame),
+    a per-gate run and every reader materialise them first, and sync() does too.  Against the
+    per-gate execution (one Pauli pass per step) with the same seed."""
+    n, B = 11, 6
+    c1, c2 = _mixed(qsim, n, 40, 11), _mixed(qsim, n, 30, 12)
+    nm, quiet = _noise(qsim, n), qsim.NoiseModel()
+    fused, ref = qsim.BatchedSimulator(n, B, nm), qsim.BatchedSimulator(n, B, nm)
+    for s in (fused, ref):
+        s.setSeed(5)
+    fused.run(c1)
+    ref.run(c1, per_gate=True)
+    for s in (fused, ref):
+        s.setNoiseModel(quiet)
+    fused.run(c2)  # noise-free, carried frame
+    ref.run(c2, per_gate=True)
+    for s in (fused, ref):
+        s.setNoiseModel(nm)
+    fused.run(c1, per_gate=True)  # per-gate run: materialises first
+    ref.run(c1, per_gate=True)
+    fused.run(c2)
+    ref.run(c2, per_gate=True)
+    fused.synchronize()
+    fused.run(c1)
+    ref.run(c1, per_gate=True)
+    for t in range(B):
+        np.testing.assert_allclose(fused.getStateVector(t), ref.getStateVector(t), atol=1e-12, rtol=0)
+    np.testing.assert_allclose(fused.getAverageProbabilities(), ref.getAverageProbabilities(),
+                               atol=1e-12, rtol=0)
+
+
 def test_frames_reference_gateset(qsim, gpu_ready):
     n, B = 11, 8
     c = _mixed(qsim, n, 80, 7)
