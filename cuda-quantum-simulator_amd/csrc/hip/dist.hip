@@ -664,12 +664,12 @@ void comm_settle(ncclComm_t comm, const char* what, double timeout_s) {
     }
 }
 void comm_settle(qsim_dist* d, const char* what) {
-    if (!d->virt && d->comm) comm_settle(d->comm, what, env_seconds("QSIM_DIST_TIMEOUT", 600.0));
+    if (d->comm) comm_settle(d->comm, what, env_seconds("QSIM_DIST_TIMEOUT", 600.0));
 }
 // hipStreamSynchronize with a watchdog: while the stream drains, a communicator error or
 // QSIM_DIST_TIMEOUT seconds fail (and abort the communicator) instead of blocking forever.
 void stream_wait(qsim_dist* d, hipStream_t s) {
-    if (d->virt || !d->comm) {
+    if (!d->comm) {
         QSIM_HIPCHK(hipStreamSynchronize(s));
         return;
     }
@@ -781,6 +781,19 @@ static int pipeline_parts(uint64_t chunk) {
 // Qubit remap: rank r sends its amplitudes with local bits lpos == c to the rank whose bits at
 // gpos are c, and stores what that rank sends at local bits == c (the swap of the two qubit
 // sets, SURVEY §8(e) "global<->local qubit swap by all-to-all").
+// Virtual mode: move one slab between two shards of this process — a device copy, or, with a
+// world-1 communicator attached (qsim_dist_virtual_rccl), an ncclSend / ncclRecv pair to rank 0
+// itself inside the caller's group (RCCL matches them in issue order), which runs the same RCCL
+// call sequence as the multi-rank path on one GPU.
+void virt_move(qsim_dist* d, double2* dst, const double2* src, uint64_t amps) {
+    if (!d->comm) {
+        QSIM_HIPCHK(hipMemcpyAsync(dst, src, amps * sizeof(double2), hipMemcpyDeviceToDevice, d->comm_stream));
+        return;
+    }
+    QSIM_NCCLCHK(ncclSend(src, (size_t)amps * 2, ncclDouble, 0, d->comm, d->comm_stream));
+    QSIM_NCCLCHK(ncclRecv(dst, (size_t)amps * 2, ncclDouble, 0, d->comm, d->comm_stream));
+}
+
 void exchange(qsim_dist* d, const DStep& ex) {
     if (ex.k == 0) return;
     const uint64_t total = 1ull << d->L;
@@ -824,16 +837,19 @@ void exchange(qsim_dist* d, const DStep& ex) {
             QSIM_NCCLCHK(ncclGroupEnd());
             comm_settle(d, "remap send/recv");
         } else {  // shard r's slab c goes to shard peer(c), into that shard's slot my_c(r)
+            if (d->comm) QSIM_NCCLCHK(ncclGroupStart());
             for (size_t i = 0; i < d->shards.size(); ++i) {
                 const XPlan& x = xs[i];
                 for (int c = 0; c < (1 << ex.k); ++c) {
                     if (c == x.a.my_c) continue;
                     Shard& dst = d->shards[x.peer_of[c]];
-                    QSIM_HIPCHK(hipMemcpyAsync(dst.recvbuf + (uint64_t)x.a.my_c * chunk + off,
-                                               d->shards[i].sendbuf + (uint64_t)c * chunk + off,
-                                               sub * sizeof(double2), hipMemcpyDeviceToDevice,
-                                               d->comm_stream));
+                    virt_move(d, dst.recvbuf + (uint64_t)x.a.my_c * chunk + off,
+                              d->shards[i].sendbuf + (uint64_t)c * chunk + off, sub);
                 }
+            }
+            if (d->comm) {
+                QSIM_NCCLCHK(ncclGroupEnd());
+                comm_settle(d, "virtual remap send/recv");
             }
         }
         QSIM_HIPCHK(hipEventRecord(d->events[parts + p], d->comm_stream));
@@ -885,16 +901,19 @@ void exchange_parts(qsim_dist* d, const DStep& ex) {
             QSIM_NCCLCHK(ncclGroupEnd());
             comm_settle(d, "overlapped remap send/recv");
         } else {
+            if (d->comm) QSIM_NCCLCHK(ncclGroupStart());
             for (size_t i = 0; i < d->shards.size(); ++i) {
                 const XPlan& x = xs[i];
                 for (int c = 0; c < (1 << ex.k); ++c) {
                     if (c == x.a.my_c) continue;
                     Shard& dst = d->shards[x.peer_of[c]];
-                    QSIM_HIPCHK(hipMemcpyAsync(dst.recvbuf + (uint64_t)h * part_amps + (uint64_t)x.a.my_c * chunk,
-                                               d->shards[i].sendbuf + (uint64_t)h * part_amps + (uint64_t)c * chunk,
-                                               chunk * sizeof(double2), hipMemcpyDeviceToDevice,
-                                               d->comm_stream));
+                    virt_move(d, dst.recvbuf + (uint64_t)h * part_amps + (uint64_t)x.a.my_c * chunk,
+                              d->shards[i].sendbuf + (uint64_t)h * part_amps + (uint64_t)c * chunk, chunk);
                 }
+            }
+            if (d->comm) {
+                QSIM_NCCLCHK(ncclGroupEnd());
+                comm_settle(d, "virtual overlapped remap send/recv");
             }
         }
         QSIM_HIPCHK(hipEventRecord(d->pev[16 + h], d->comm_stream));
@@ -909,7 +928,8 @@ void exchange_parts(qsim_dist* d, const DStep& ex) {
 }
 
 double allreduce_sum(qsim_dist* d, double local) {
-    if (d->virt) return local;
+    if (!d->comm) return local;  // virtual: `local` already sums every shard (with a world-1
+                                 // communicator the all-reduce below runs anyway, as an identity)
     QSIM_HIPCHK(hipMemcpyAsync(d->d_result, &local, sizeof(double), hipMemcpyHostToDevice, d->stream));
     QSIM_NCCLCHK(ncclAllReduce(d->d_result, d->d_result, 1, ncclDouble, ncclSum, d->comm, d->stream));
     comm_settle(d, "all-reduce");
@@ -1086,6 +1106,33 @@ int qsim_dist_create_virtual(int n_qubits, int world, int device, qsim_dist** ou
         alloc_shards(d.get(), ranks);
         init_zero(d.get());
         *out = d.release();
+    });
+}
+
+int qsim_dist_virtual_rccl(qsim_dist* d, const void* unique_id) {
+    return dguard([&] {
+        need(d);
+        if (!d->virt || d->comm) fail(QSIM_ERR_INVALID_ARGUMENT, "needs a virtual object without a communicator");
+        if (!unique_id) fail(QSIM_ERR_INVALID_ARGUMENT, "null argument");
+        QSIM_HIPCHK(hipSetDevice(d->device));
+        ncclUniqueId id;
+        std::memcpy(&id, unique_id, sizeof(id));
+        const char* bl = std::getenv("QSIM_RCCL_BLOCKING");
+        ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+        cfg.blocking = bl && std::atoi(bl) != 0 ? 1 : 0;
+        const ncclResult_t ir = ncclCommInitRankConfig(&d->comm, 1, id, 0, &cfg);
+        if (ir != ncclSuccess && ir != ncclInProgress) {
+            if (d->comm) (void)ncclCommAbort(d->comm);
+            d->comm = nullptr;
+            fail(QSIM_ERR_DEVICE, std::string("RCCL error: ") + ncclGetErrorString(ir));
+        }
+        try {
+            comm_settle(d->comm, "communicator init", env_seconds("QSIM_DIST_INIT_TIMEOUT", 300.0));
+        } catch (...) {
+            (void)ncclCommAbort(d->comm);
+            d->comm = nullptr;
+            throw;
+        }
     });
 }
 

@@ -165,6 +165,7 @@ class qsim_dist_step(Structure):
 _sig(hip, "qsim_dist_unique_id", [_P])
 _sig(hip, "qsim_dist_create", [c_int, c_int, c_int, _P, c_int, POINTER(_P)])
 _sig(hip, "qsim_dist_create_virtual", [c_int, c_int, c_int, POINTER(_P)])
+_sig(hip, "qsim_dist_virtual_rccl", [_P, c_char_p])
 _sig(hip, "qsim_dist_destroy", [_P])
 _sig(hip, "qsim_dist_run", [_P, POINTER(qsim_gate), c_size_t, c_int])
 _sig(hip, "qsim_dist_sync", [_P])

@@ -45,8 +45,16 @@ class DistributedSimulator:
                                                  _c.byref(self._h)))
 
     @classmethod
-    def virtual(cls, num_qubits: int, world: int, device: int = 0) -> "DistributedSimulator":
-        return cls(num_qubits, 0, world, None, device, _virtual=True)
+    def virtual(cls, num_qubits: int, world: int, device: int = 0,
+                rccl: bool = False) -> "DistributedSimulator":
+        """`world` shards in this process on one GPU.  rccl: move the slabs with ncclSend /
+        ncclRecv pairs to rank 0 of a world-1 communicator (qsim_dist_virtual_rccl) instead of
+        device copies — the multi-rank RCCL call sequence, on one GPU."""
+        sim = cls(num_qubits, 0, world, None, device, _virtual=True)
+        if rccl:
+            buf = _c.create_string_buffer(unique_id(), UNIQUE_ID_BYTES)
+            _lib.check(_lib.hip.qsim_dist_virtual_rccl(sim._h, buf))
+        return sim
 
     def __del__(self):
         self.close()

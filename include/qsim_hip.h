@@ -325,6 +325,11 @@ int qsim_dist_create(int n_qubits, int rank, int world, const void* unique_id, i
 /* Virtual ranks: all `world` shards in this process on one GPU, exchanged by device copies
  * (same planner and pack/unpack kernels, no RCCL) — for testing the sharded path on one GPU. */
 int qsim_dist_create_virtual(int n_qubits, int world, int device, qsim_dist** out);
+/* Attach a world-1 RCCL communicator (unique id from qsim_dist_unique_id) to a virtual object:
+ * its slab moves then run as ncclSend / ncclRecv pairs to rank 0 itself in the same groups, and
+ * its all-reduces through RCCL — the multi-rank call sequence (non-blocking init, groups,
+ * settle, watchdog) on one GPU (tests). */
+int qsim_dist_virtual_rccl(qsim_dist* d, const void* unique_id);
 int qsim_dist_destroy(qsim_dist* d);
 int qsim_dist_run(qsim_dist* d, const qsim_gate* gates, size_t count, int flags);
 int qsim_dist_sync(qsim_dist* d);

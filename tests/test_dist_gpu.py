@@ -132,3 +132,24 @@ def test_relabeled_local_positions_match(qsim, oracle, gpu_ready, world, n):
     finally:
         set_relabel(1, 26)
     assert maps[0] != maps[1]
+
+
+@pytest.mark.parametrize("world,n,fused", [(8, 16, True), (4, 18, True), (2, 14, True),
+                                           (8, 10, True), (8, 16, False)])
+def test_virtual_shards_over_rccl(qsim, oracle, gpu_ready, world, n, fused):
+    """Virtual shards whose slabs move as ncclSend / ncclRecv pairs to rank 0 of a world-1 RCCL
+    communicator (non-blocking init, grouped calls, settle, watchdog, all-reduce): the RCCL call
+    sequence of the multi-rank path, run on one GPU, for part-exchanges (n >= 14 here) and plain
+    pipelined remaps (n = 10: 7 local qubits, no overlap)."""
+    from qsim_amd.dist import DistributedSimulator
+    c = qsim.createRandomHCCircuit(n, 100, 3)
+    d = DistributedSimulator.virtual(n, world, rccl=True)
+    s = qsim.Simulator(n)
+    for _ in range(2):
+        d.run(c, fused=fused)
+        s.run(c)
+    got = d.getStateVector()
+    np.testing.assert_allclose(got, s.getStateVector(), atol=1e-12, rtol=0)
+    assert abs(d.getTotalProbability() - 1.0) < 1e-10
+    g = oracle.gates_of(c)
+    np.testing.assert_allclose(got, oracle.run_cpu(n, g + g), atol=1e-12, rtol=0)
