@@ -7,6 +7,7 @@
 
 #include <atomic>
 #include <cstdlib>
+#include <cstdio>
 #include <cstring>
 #include <memory>
 #include <string>
@@ -263,6 +264,61 @@ static void prep(qsim_state* s, bool touch) {
     canonicalize(s);
     if (touch) s->basis = false;
 }
+// Time the layout choice and its alternatives with their own circuit-specialised kernels on this
+// device (each candidate's whole plan, the faster of two runs, the basis state restored after
+// each) and keep the fastest: the cost model ranks layouts from probes of other boxes, and real
+// pass times differ by a few per cent between devices.  Their plans stay cached (compiled).
+static bool calibrate_layout(qsim_state* s, LayoutChoice& lc) {
+    const size_t ncand = 1 + lc.alts.size();
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    QSIM_HIPCHK(hipEventCreate(&e0));
+    QSIM_HIPCHK(hipEventCreate(&e1));
+    size_t best = 0;
+    float best_ms = 3.0e38f;
+    try {
+        for (size_t k = 0; k < ncand; ++k) {
+            const std::vector<Op>& ops = k ? lc.alts[k - 1].ops : lc.ops;
+            s->plans.put(ops, s->n, k ? lc.alts[k - 1].plan : lc.plan, s->stream);
+            PlanCache::Entry& pe = s->plans.get(ops, s->n, s->stream);
+            const JitModule* jm = jit_for(pe.jit, pe.plan, s->n);
+            s->ops.upload(pe.plan.ops.data(), pe.plan.ops.size() * sizeof(TileOp), s->stream);
+            s->stages.upload(pe.plan.stages.data(), pe.plan.stages.size() * sizeof(Stage), s->stream);
+            float ms = 3.0e38f;
+            for (int rep = 0; rep < 2; ++rep) {
+                QSIM_HIPCHK(hipEventRecord(e0, s->stream));
+                launch_fused(s->d, s->n, 1, pe.plan, (const TileOp*)s->ops.ptr, (const Stage*)s->stages.ptr,
+                             s->stream, nullptr, jm);
+                QSIM_HIPCHK(hipEventRecord(e1, s->stream));
+                QSIM_HIPCHK(hipEventSynchronize(e1));
+                float t = 0.0f;
+                QSIM_HIPCHK(hipEventElapsedTime(&t, e0, e1));
+                ms = std::min(ms, t);
+            }
+            launch_init_basis(s->d, s->n, 1, s->basis_idx, s->stream);  // the state as it was
+            static const bool dbg = std::getenv("QSIM_RELABEL_DEBUG") != nullptr;
+            if (dbg) std::fprintf(stderr, "[calibrate] candidate %zu: %.3f ms per run\n", k, ms);
+            if (ms < best_ms) {
+                best = k;
+                best_ms = ms;
+            }
+        }
+    } catch (...) {
+        (void)hipEventDestroy(e0);
+        (void)hipEventDestroy(e1);
+        throw;
+    }
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    QSIM_HIPCHK(hipStreamSynchronize(s->stream));
+    if (best > 0) {
+        LayoutChoice::Alt& a = lc.alts[best - 1];
+        lc.perm = std::move(a.perm);
+        lc.ops = std::move(a.ops);
+        lc.plan = std::move(a.plan);
+    }
+    return true;
+}
+
 static qsim_gate map_gate(const qsim_state* s, const qsim_gate& g) {
     qsim_gate m = g;
     if (!s->perm.empty())
@@ -283,6 +339,10 @@ int qsim_state_last_run(qsim_state* s, int* passes, int* jit_passes) {
     });
 }
 int qsim_abi_version(void) { return QSIM_ABI_VERSION; }
+
+int qsim_set_calibrate(int mode, int min_qubits) {
+    return guarded([&] { calibrate_configure(mode, min_qubits); });
+}
 
 int qsim_set_device(int device) {
     return guarded([&] {
@@ -454,10 +514,11 @@ int qsim_run(qsim_state* s, const qsim_gate* gates, size_t count, int flags) {
             if (layout_memo_get(s->n, 0, gates, count * sizeof(qsim_gate), memo)) {
                 s->perm = memo;  // decided before for this circuit (its plan: the plan cache)
             } else {
-                LayoutChoice lc = choose_layout(s->n, lower_under, relabel_tries());
+                LayoutChoice lc = choose_layout(s->n, lower_under, relabel_tries(), relabel_calibrate(s->n) ? 2 : 0);
+                const bool cached = !lc.alts.empty() && calibrate_layout(s, lc);  // (plans cached)
                 layout_memo_put(s->n, 0, gates, count * sizeof(qsim_gate), lc.perm);
                 s->perm = lc.perm;
-                if (!lc.perm.empty()) s->plans.put(std::move(lc.ops), s->n, std::move(lc.plan), s->stream);
+                if (!lc.perm.empty() && !cached) s->plans.put(std::move(lc.ops), s->n, std::move(lc.plan), s->stream);
             }
             if (!s->perm.empty()) {
                 if (s->basis_idx) {  // relabel the basis state itself

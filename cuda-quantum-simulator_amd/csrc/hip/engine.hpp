@@ -182,9 +182,21 @@ struct LayoutChoice {
     Plan plan;
     size_t passes_before = 0;
     double cost_before = 0.0, cost_after = 0.0;
+    // want_alts > 0: the next acceptable candidates (same pass count), predicted-cost order
+    struct Alt {
+        std::vector<int> perm;
+        std::vector<Op> ops;
+        Plan plan;
+    };
+    std::vector<Alt> alts;
 };
 LayoutChoice choose_layout(int n, const std::function<std::vector<Op>(const std::vector<int>&)>& lower,
-                           int tries);
+                           int tries, size_t want_alts = 0);
+// QSIM_RELABEL_CALIBRATE (default 1) / QSIM_RELABEL_CALIBRATE_MIN_QUBITS (default 28): with
+// inline compilation (QSIM_JIT=2) the first run of a basis state times the model's choice and
+// its alternatives with their circuit-specialised kernels and keeps the fastest (capi.hip).
+bool relabel_calibrate(int n);
+void calibrate_configure(int mode, int min_qubits);  // negative: unchanged
 int relabel_tries();  // QSIM_RELABEL_TRIES (default 7): random labelings planned per choice
 // Process-wide memo of layout choices per circuit (kind: 0 state, 1 batched with its run flags).
 bool layout_memo_get(int n, int kind, const void* gates, size_t bytes, std::vector<int>& perm);

@@ -87,6 +87,24 @@ void layout_memo_put(int n, int kind, const void* gates, size_t bytes, const std
     g_memo.push_back(MemoEntry{n, kind, std::vector<unsigned char>(p, p + bytes), perm, ++g_memo_clock});
 }
 
+static std::atomic<int> g_calib{-1}, g_calib_min{-1};
+bool relabel_calibrate(int n) {
+    if (g_calib.load() < 0) {
+        const char* e = std::getenv("QSIM_RELABEL_CALIBRATE");
+        g_calib.store(e ? std::atoi(e) : 1);
+    }
+    if (g_calib_min.load() < 0) {
+        const char* e = std::getenv("QSIM_RELABEL_CALIBRATE_MIN_QUBITS");
+        g_calib_min.store(e ? std::atoi(e) : 28);
+    }
+    return g_calib.load() != 0 && n >= g_calib_min.load() && jit_mode() == 2;
+}
+void calibrate_configure(int mode, int min_qubits) {
+    relabel_calibrate(0);  // defaults first
+    if (mode >= 0) g_calib.store(mode);
+    if (min_qubits >= 0) g_calib_min.store(min_qubits);
+}
+
 int relabel_tries() {
     static const int v = [] {
         const char* e = std::getenv("QSIM_RELABEL_TRIES");
@@ -188,7 +206,7 @@ std::vector<int> choose_relabel(const std::vector<uint64_t>& tiles, int n, doubl
 // >= 3 % cheaper.  `lower` maps the caller's gates through a permutation and lowers them exactly
 // as the caller will (so the returned plan can be cached under the same key).
 LayoutChoice choose_layout(int n, const std::function<std::vector<Op>(const std::vector<int>&)>& lower,
-                           int tries) {
+                           int tries, size_t want_alts) {
     struct Cand {
         std::vector<int> pi;
         size_t passes = 0;
@@ -253,6 +271,7 @@ LayoutChoice choose_layout(int n, const std::function<std::vector<Op>(const std:
     std::vector<size_t> order(pool.size());
     for (size_t i = 0; i < order.size(); ++i) order[i] = i;
     std::sort(order.begin(), order.end(), [&](size_t a, size_t b) { return pred[a] < pred[b]; });
+    bool chosen = false;  // the first acceptable candidate; then up to want_alts alternatives
     for (size_t i : order) {
         // the annealed labels may steer the planner differently: verify, else the candidate as is
         for (int variant = 0; variant < 2; ++variant) {
@@ -266,12 +285,18 @@ LayoutChoice choose_layout(int n, const std::function<std::vector<Op>(const std:
             bool identity = true;
             for (int q = 0; q < n; ++q) identity = identity && pi[q] == q;
             if (identity) return out;
-            out.perm = pi;
-            out.ops = std::move(ops);
-            out.plan = std::move(plan);
-            out.cost_after = cost;
-            return out;
+            if (!chosen) {
+                out.perm = pi;
+                out.ops = std::move(ops);
+                out.plan = std::move(plan);
+                out.cost_after = cost;
+                chosen = true;
+            } else if (plan.passes.size() == out.plan.passes.size() && pi != out.perm) {
+                out.alts.push_back(LayoutChoice::Alt{pi, std::move(ops), std::move(plan)});
+            }
+            break;
         }
+        if (chosen && out.alts.size() >= want_alts) break;
     }
     return out;
 }

@@ -55,6 +55,12 @@ def set_relabel(mode: int = -1, min_qubits: int = -1) -> None:
     _lib.check(_lib.hip.qsim_set_relabel(mode, min_qubits))
 
 
+def set_calibrate(mode: int = -1, min_qubits: int = -1) -> None:
+    """Time the layout model's top candidates on the device at a basis state's first run and
+    keep the fastest (qsim_set_calibrate; needs set_jit(2)): mode 0 off, 1 on."""
+    _lib.check(_lib.hip.qsim_set_calibrate(mode, min_qubits))
+
+
 def plan_relabel(circuit: Circuit):
     """(perm, predicted_us_before, predicted_us_after): the logical -> physical qubit map the
     engine would choose for this circuit's fused plan (identity when none pays), host only."""

@@ -157,6 +157,11 @@ int qsim_jit_shutdown(void);
  * are never relabeled; negative arguments leave a setting unchanged. */
 int qsim_set_relabel(int mode, int min_qubits);
 int qsim_state_perm(qsim_state* s, int32_t* perm);  /* current logical -> physical map, n entries */
+/* Layout calibration (with QSIM_JIT = 2, from min_qubits; defaults QSIM_RELABEL_CALIBRATE = 1,
+ * QSIM_RELABEL_CALIBRATE_MIN_QUBITS = 28): the first run of a basis state times the layout
+ * model's choice and two alternatives with their compiled pass kernels (the basis state is
+ * restored after each) and keeps the fastest.  Negative arguments leave a setting unchanged. */
+int qsim_set_calibrate(int mode, int min_qubits);
 /* Host-only: the permutation the engine would choose for this circuit (identity when none pays)
  * and the predicted pass-layout cost (microseconds, summed over the plan's passes) before/after. */
 int qsim_plan_relabel(int n_qubits, const qsim_gate* gates, size_t count, int32_t* perm,

@@ -117,3 +117,32 @@ def test_relabel_off_is_identity(qsim, gpu_ready):
         assert sim.state.perm() == list(range(n))
     finally:
         set_relabel(1, 26)
+
+
+def test_calibrated_choice_matches_oracle(qsim, oracle, gpu_ready, relabel_low):
+    """Layout calibration (inline compilation): the first run times the model's choice and its
+    alternatives on the device — running each candidate's plan on the basis state and restoring
+    it — then runs the circuit under the fastest.  The result is exact, also from a non-zero
+    basis state."""
+    from qsim_amd.plan import set_calibrate, set_jit
+    set_jit(2, -1)
+    set_calibrate(1, 14)
+    try:
+        n = 18
+        c = qsim.createRandomHCCircuit(n, 100, 2)
+        g = oracle.gates_of(c)
+        sim = qsim.Simulator(n)
+        sim.run(c)
+        assert sim.state.perm() != list(range(n))
+        assert _err(sim.getStateVector(), oracle.run_cpu(n, g)) < 1e-12
+        k = 0b110010101100111010
+        start = np.zeros(1 << n, dtype=np.complex128)
+        start[k] = 1.0
+        sv = qsim.StateVector(n)
+        sv.initializeBasis(k)
+        sv.run(c, qsim.RunMode.Fused)
+        sv.run(c, qsim.RunMode.Fused)
+        assert _err(sv.toHost(), oracle.run_cpu(n, g + g, state=start)) < 1e-12
+    finally:
+        set_calibrate(1, 28)
+        set_jit(1, -1)
