@@ -514,7 +514,11 @@ int qsim_run(qsim_state* s, const qsim_gate* gates, size_t count, int flags) {
             if (layout_memo_get(s->n, 0, gates, count * sizeof(qsim_gate), memo)) {
                 s->perm = memo;  // decided before for this circuit (its plan: the plan cache)
             } else {
-                LayoutChoice lc = choose_layout(s->n, lower_under, relabel_tries(), relabel_calibrate(s->n) ? 2 : 0);
+                static const size_t alts = [] {  // QSIM_RELABEL_CALIBRATE_CANDIDATES (default 3)
+                    const char* e = std::getenv("QSIM_RELABEL_CALIBRATE_CANDIDATES");
+                    return (size_t)std::max(1, e ? std::atoi(e) : 3) - 1;
+                }();
+                LayoutChoice lc = choose_layout(s->n, lower_under, relabel_tries(), relabel_calibrate(s->n) ? alts : 0);
                 const bool cached = !lc.alts.empty() && calibrate_layout(s, lc);  // (plans cached)
                 layout_memo_put(s->n, 0, gates, count * sizeof(qsim_gate), lc.perm);
                 s->perm = lc.perm;
