@@ -340,6 +340,10 @@ int qsim_state_last_run(qsim_state* s, int* passes, int* jit_passes) {
 }
 int qsim_abi_version(void) { return QSIM_ABI_VERSION; }
 
+int qsim_set_tile_height(int h) {
+    return guarded([&] { tile_height_configure(h); });
+}
+
 int qsim_set_calibrate(int mode, int min_qubits) {
     return guarded([&] { calibrate_configure(mode, min_qubits); });
 }

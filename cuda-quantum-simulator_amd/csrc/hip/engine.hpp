@@ -99,7 +99,7 @@ struct FusedPass {
     int single = -1;       // >= 0: not a tile pass but one per-gate op, Plan::singles[single]
     int h = 0;             // tile = 64 << h amplitudes (tile bits 0 .. 5 + h)
     int r0 = 6;            // tile bits 0 .. r0-1 are qubits 0 .. r0-1 (2^r0-amplitude HBM runs)
-    int hpos[8] = {0};     // ascending physical qubits of tile bits r0 .. 5 + h (all >= r0)
+    int hpos[10] = {0};    // ascending physical qubits of tile bits r0 .. 5 + h (all >= r0)
     int op_begin = 0, op_end = 0;  // range in the pass-op buffer (unstaged kernel)
     int stage_begin = 0, stage_end = 0;  // range in Plan::stages (staged kernel, h >= 4)
     int hu_count = 0;      // unnormalized H butterflies in the pass: store scales by 2^(-k/2)
@@ -158,11 +158,19 @@ struct Plan {
     size_t fused_gate_count = 0;
     size_t tile_passes = 0;
 };
-constexpr int kTileHMax = 6;  // 64 << 6 = 4096 amplitudes = 64 KiB of LDS per workgroup
+constexpr int kTileHMax = 7;  // 64 << 7 = 8192 amplitudes = 128 KiB of LDS per workgroup
+constexpr int kTileHDefault = 6;  // 12-qubit tiles unless QSIM_TILE_HMAX / qsim_set_tile_hmax
+constexpr int kHposMax = 10;  // tile bits above the run: 6 + h - r0 <= 9
+// Register bits per thread of a staged pass: 16 amplitudes per thread; 256 threads per workgroup
+// up to h = 6, 512 at h = 7 (one 128 KiB workgroup per CU, the same 8 waves per CU).
+constexpr int stage_rb(int h) { return h >= 6 ? 4 : h - 2; }
+constexpr int stage_threads(int h) { return (64 << h) >> stage_rb(h); }
 constexpr int kTileR0 = 6;    // contiguous run bits of a staged tile (QSIM_TILE_R0 in 4..6)
-// hmax < 0: the process default (kTileHMax, or QSIM_TILE_HMAX for tuning runs).
+// hmax < 0: the process default (kTileHDefault, or QSIM_TILE_HMAX up to kTileHMax).
 // avoid: qubits no tile may contain (ops never act on them; only tile padding is affected).
 Plan plan_fused(const std::vector<Op>& ops, int n, int hmax = -1, uint64_t avoid = 0);
+int tile_height_default();             // the h that hmax < 0 means
+void tile_height_configure(int h);     // qsim_set_tile_height: h < 0 restores the env default
 // Layout-aware qubit relabeling (relabel.hip): predicted cost of a tile (qubit mask) in
 // microseconds, the tiles of a plan's staged passes, and the permutation (logical -> physical)
 // minimising the predicted cost of `tiles` (empty: keep the identity, < min_gain better).
@@ -214,6 +222,7 @@ struct JitState {
     bool failed = false;
 };
 int jit_mode();        // 0 off, 1 background compile (default), 2 compile on first use
+bool jit_pass_pipelined(const FusedPass& p);  // persistent software-pipelined pass kernel (jit.hip)
 int jit_min_qubits();  // smaller states never JIT (QSIM_JIT_MIN_QUBITS, default 20)
 void jit_configure(int mode, int min_qubits);  // < 0 leaves a setting unchanged
 void jit_shutdown();  // stop the background compiler (queued jobs dropped, running one joined)
@@ -227,7 +236,7 @@ const JitModule* jit_for(JitState& js, const Plan& plan, int n);
 // once compiled, runs the specialised kernels.
 struct PlanCache {
     struct Entry {
-        int n = -1;
+        int n = -1, h = -1;  // h: the tile height the plan was made for
         uint64_t avoid = 0;
         std::vector<Op> key;
         Plan plan;

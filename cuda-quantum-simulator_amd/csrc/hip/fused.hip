@@ -15,6 +15,7 @@
 // Planner rule (both levels): a gate moves into the current pass/stage when its qubits fit and
 // it shares no qubit with an earlier gate that was deferred (gates on disjoint qubits commute
 // exactly).  Gate semantics are the per-gate kernels' (device_ops.hpp), i.e. src/Gates.cu.
+#include <atomic>
 #include <hip/hip_runtime.h>
 #include <hip/hip_ext.h>
 
@@ -558,7 +559,8 @@ static bool same_op(const Op& a, const Op& b) {
 PlanCache::Entry& PlanCache::get(const std::vector<Op>& ops, int n_qubits, hipStream_t stream,
                                  uint64_t avoid) {
     for (auto& e : entries) {
-        bool hit = e->n == n_qubits && e->avoid == avoid && e->key.size() == ops.size();
+        bool hit = e->n == n_qubits && e->h == tile_height_default() && e->avoid == avoid &&
+                   e->key.size() == ops.size();
         for (size_t i = 0; hit && i < ops.size(); ++i) hit = same_op(e->key[i], ops[i]);
         if (hit) {
             e->used = ++clock;
@@ -576,6 +578,7 @@ PlanCache::Entry& PlanCache::get(const std::vector<Op>& ops, int n_qubits, hipSt
     e->plan = plan_fused(ops, n_qubits, -1, avoid);
     e->key = ops;
     e->n = n_qubits;
+    e->h = tile_height_default();
     e->avoid = avoid;
     e->used = ++clock;
     entries.push_back(std::move(e));
@@ -593,6 +596,7 @@ void PlanCache::put(std::vector<Op> ops, int n_qubits, Plan plan, hipStream_t st
     e->plan = std::move(plan);
     e->key = std::move(ops);
     e->n = n_qubits;
+    e->h = tile_height_default();
     e->used = ++clock;
     entries.push_back(std::move(e));
 }
@@ -602,11 +606,20 @@ static int env_int(const char* k, int d) {
     return e ? std::atoi(e) : d;
 }
 
+static std::atomic<int> g_tile_h{-1};
+int tile_height_default() {
+    const int h = g_tile_h.load();
+    if (h >= 0) return h;
+    static const int def = std::min(kTileHMax, std::max(0, env_int("QSIM_TILE_HMAX", kTileHDefault)));
+    return def;
+}
+void tile_height_configure(int h) {
+    if (h > kTileHMax) fail(QSIM_ERR_INVALID_ARGUMENT, "tile height out of range (0..7)");
+    g_tile_h.store(h < 0 ? -1 : h);
+}
+
 Plan plan_fused(const std::vector<Op>& ops, int n, int hmax, uint64_t avoid) {
-    if (hmax < 0) {
-        static const int def = std::min(kTileHMax, std::max(0, env_int("QSIM_TILE_HMAX", kTileHMax)));
-        hmax = def;
-    }
+    if (hmax < 0) hmax = tile_height_default();
     Plan plan;
     auto add_single = [&](const Op& op) {
         FusedPass p;
@@ -687,7 +700,7 @@ Plan plan_fused(const std::vector<Op>& ops, int n, int hmax, uint64_t avoid) {
             tsrc.push_back(op.src);
         }
         if (heff >= 4) {
-            plan_stages(tops, tsrc, 6 + heff, heff - 2, plan, p);
+            plan_stages(tops, tsrc, 6 + heff, stage_rb(heff), plan, p);
         } else {
             p.op_begin = (int)plan.ops.size();
             for (size_t i = 0; i < tops.size(); ++i) {
@@ -715,7 +728,7 @@ struct FArgs {
     int log_tpt;
     int op_begin, op_end;
     int stage_begin, stage_end;
-    int hpos[8];
+    int hpos[kHposMax];
     int r0;              // run bits (tile bits 0..r0-1 = qubits 0..r0-1); hpos covers the rest
     double scale;        // applied at the store: (1/sqrt2)^(unnormalized H butterflies)
     // Pauli frames of a batched noisy run: frames[2 * (step * nbatch + traj)] = {F, G}, the
@@ -727,17 +740,17 @@ struct FArgs {
     uint64_t fix_mask, fix_val, zmask;
 };
 
-// Runtime-count forms for the staged kernel (count = tile bits above the run, <= 8).
+// Runtime-count forms for the staged kernel (count = tile bits above the run, < kHposMax).
 __device__ __forceinline__ uint64_t spread_n(uint32_t x, const int* hpos, int cnt) {
     uint64_t r = 0;
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
+    for (int i = 0; i < kHposMax; ++i)
         if (i < cnt) r |= (uint64_t)((x >> i) & 1u) << hpos[i];
     return r;
 }
 __device__ __forceinline__ uint64_t deposit_n(uint64_t k, const int* hpos, int cnt) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
+    for (int i = 0; i < kHposMax; ++i) {
         if (i < cnt) {
             const uint64_t lo = k & ((1ull << hpos[i]) - 1ull);
             k = ((k ^ lo) << 1) | lo;
@@ -1102,9 +1115,9 @@ __device__ __forceinline__ uint32_t stage_jb(const Stage& st) {
 // instruction); only the stages in between round-trip through LDS (read, ops, write, barrier).
 // A pass whose ops fit one such stage never touches LDS.
 template <int H, bool NT, bool FR = false>
-__global__ __launch_bounds__(256, 2) void k_fused_staged(FArgs a) {  // 2 WGs/CU (LDS-bound)
+__global__ __launch_bounds__(stage_threads(H), H >= 7 ? 1 : 2) void k_fused_staged(FArgs a) {  // LDS-bound: 2 WGs/CU (h <= 6), 1 at h = 7
     constexpr int T = 64 << H;
-    constexpr int RB = H - 2;
+    constexpr int RB = stage_rb(H);
     constexpr int R = 1 << RB;
     __shared__ double2 tile[T];
     const uint64_t tile_id = blockIdx.x;
@@ -1172,6 +1185,20 @@ static bool fused_nt() {
     return v;
 }
 
+// Workgroups of a persistent pass kernel: every CU's resident share (one 128 KiB-LDS workgroup per
+// CU at h = 7, two 64 KiB ones below; QSIM_JIT_PIPE_WG overrides the per-CU count).
+static uint64_t pipe_workgroups(int h) {
+    static const int cus = [] {
+        int dev = 0, c = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c <= 0)
+            c = 256;
+        return c;
+    }();
+    static const int per = env_int("QSIM_JIT_PIPE_WG", 0);
+    return (uint64_t)cus * (uint64_t)(per > 0 ? per : (h >= 7 ? 1 : 2));
+}
+
 void launch_fused(double2* st, int n, uint64_t batch, const Plan& plan, const TileOp* d_ops,
                   const Stage* d_stages, hipStream_t s, Timer* tm, const JitModule* jm,
                   const uint64_t* frames, const FusedRange& range) {
@@ -1200,7 +1227,7 @@ void launch_fused(double2* st, int n, uint64_t batch, const Plan& plan, const Ti
         a.stage_end = p.stage_end;
         // (1/sqrt2)^k: exact power of two for even k, one rounding for odd k
         a.scale = std::ldexp(1.0, -(p.hu_count / 2)) * ((p.hu_count & 1) ? kInvSqrt2 : 1.0);
-        for (int i = 0; i < 8; ++i) a.hpos[i] = p.hpos[i];
+        for (int i = 0; i < kHposMax; ++i) a.hpos[i] = p.hpos[i];
         a.r0 = p.r0;
         uint64_t hmask = 0;
         for (int i = 0; i < 6 + p.h - p.r0; ++i) hmask |= 1ull << p.hpos[i];
@@ -1225,19 +1252,23 @@ void launch_fused(double2* st, int n, uint64_t batch, const Plan& plan, const Ti
             switch (p.h) {
                 case 4: hipExtLaunchKernelGGL((k_fused_staged<4, true, true>), dim3((unsigned)blocks), dim3(256), 0, s, ev0, ev1, 0, a); break;
                 case 5: hipExtLaunchKernelGGL((k_fused_staged<5, true, true>), dim3((unsigned)blocks), dim3(256), 0, s, ev0, ev1, 0, a); break;
-                default: hipExtLaunchKernelGGL((k_fused_staged<6, true, true>), dim3((unsigned)blocks), dim3(256), 0, s, ev0, ev1, 0, a); break;
+                case 6: hipExtLaunchKernelGGL((k_fused_staged<6, true, true>), dim3((unsigned)blocks), dim3(256), 0, s, ev0, ev1, 0, a); break;
+                default: hipExtLaunchKernelGGL((k_fused_staged<7, true, true>), dim3((unsigned)blocks), dim3(stage_threads(7)), 0, s, ev0, ev1, 0, a); break;
             }
             QSIM_HIPCHK(hipGetLastError());
             continue;
         }
         const size_t pi = pidx;
         if (jm && pi < jm->fn.size() && jm->fn[pi]) {  // circuit-specialised kernel (jit.hip)
-            unsigned long long stride = a.stride, tpt = a.tpt_mask, zm = a.zmask, fv = a.fix_val;
+            unsigned long long stride = a.stride, tpt = a.tpt_mask, zm = a.zmask, fv = a.fix_val, ntiles = blocks;
             int lt_arg = lt;
-            void* args[] = {&a.st, &stride, &tpt, &lt_arg, &zm, &fv};
-            if (blocks * 256ull > 0xffffffffull) fail(QSIM_ERR_RUNTIME, "pass grid too large");
+            void* args[] = {&a.st, &stride, &tpt, &lt_arg, &zm, &fv, &ntiles};
+            const unsigned nthr = (unsigned)stage_threads(p.h);
+            // a pipelined (persistent) kernel gets the resident workgroups only and walks its tiles
+            const uint64_t grid = jit_pass_pipelined(p) ? std::min<uint64_t>(blocks, pipe_workgroups(p.h)) : blocks;
+            if (grid * nthr > 0xffffffffull) fail(QSIM_ERR_RUNTIME, "pass grid too large");
             // grid in work-items; the events (if any) time the dispatch packet itself
-            QSIM_HIPCHK(hipExtModuleLaunchKernel(jm->fn[pi], (uint32_t)(blocks * 256), 1, 1, 256, 1, 1, 0, s,
+            QSIM_HIPCHK(hipExtModuleLaunchKernel(jm->fn[pi], (uint32_t)(grid * nthr), 1, 1, nthr, 1, 1, 0, s,
                                                  args, nullptr, ev0, ev1, 0));
             continue;
         }
@@ -1246,8 +1277,8 @@ void launch_fused(double2* st, int n, uint64_t batch, const Plan& plan, const Ti
     case HH: hipExtLaunchKernelGGL(k_fused_tile<HH>, dim3((unsigned)blocks), dim3(256), 0, s, ev0, ev1, 0, a); break;
 #define QSIM_STAGED_CASE(HH) \
     case HH:                                                                                      \
-        if (nt) hipExtLaunchKernelGGL((k_fused_staged<HH, true>), dim3((unsigned)blocks), dim3(256), 0, s, ev0, ev1, 0, a); \
-        else hipExtLaunchKernelGGL((k_fused_staged<HH, false>), dim3((unsigned)blocks), dim3(256), 0, s, ev0, ev1, 0, a); \
+        if (nt) hipExtLaunchKernelGGL((k_fused_staged<HH, true>), dim3((unsigned)blocks), dim3(stage_threads(HH)), 0, s, ev0, ev1, 0, a); \
+        else hipExtLaunchKernelGGL((k_fused_staged<HH, false>), dim3((unsigned)blocks), dim3(stage_threads(HH)), 0, s, ev0, ev1, 0, a); \
         break;
             QSIM_TILE_CASE(0)
             QSIM_TILE_CASE(1)
@@ -1256,6 +1287,7 @@ void launch_fused(double2* st, int n, uint64_t batch, const Plan& plan, const Ti
             QSIM_STAGED_CASE(4)
             QSIM_STAGED_CASE(5)
             QSIM_STAGED_CASE(6)
+            QSIM_STAGED_CASE(7)
 #undef QSIM_TILE_CASE
 #undef QSIM_STAGED_CASE
             default: fail(QSIM_ERR_RUNTIME, "unsupported tile height");

@@ -212,6 +212,16 @@ struct Gen {
     }
 };
 
+}  // namespace
+// Multi-stage passes as persistent, software-pipelined kernels (QSIM_JIT_PIPE: 0 never, 1 for
+// 13-qubit tiles only (default), 2 for every multi-stage pass).  Decided from the pass alone, so
+// the generator and the launch (grid = resident workgroups) agree.
+bool jit_pass_pipelined(const FusedPass& p) {
+    static const int v = env_or("QSIM_JIT_PIPE", 1);
+    if (p.single >= 0 || p.stage_end - p.stage_begin < 2) return false;
+    return v >= 2 || (v == 1 && p.h >= 7);
+}
+namespace {
 // Thread index spread over the tile bits that are not register bits of stage `st`.
 std::string jb_expr(const Stage& st, int rb) {
     std::string e = "tid";
@@ -247,8 +257,9 @@ std::string tile_id_expr() {
 }
 
 void gen_pass(std::ostringstream& out, const Plan& plan, const FusedPass& p, int idx) {
-    const int H = p.h, RB = H - 2, R = 1 << RB, T = 64 << H;
+    const int H = p.h, RB = stage_rb(H), R = 1 << RB, T = 64 << H;
     const int r0 = p.r0, nh = 6 + H - r0;
+    const bool pipe = jit_pass_pipelined(p);
     Gen g;
     g.R = R;
     g.RB = RB;
@@ -257,62 +268,126 @@ void gen_pass(std::ostringstream& out, const Plan& plan, const FusedPass& p, int
     // zmask: positions the tile-id bits skip — the tile's own qubits above the run, plus (for a
     // sub-space launch of the sharded engine) fixed qubits whose values fix_val supplies.  Zero
     // insertion in ascending position order, uniform per workgroup (scalar ALU).
-    o << "extern \"C\" __global__ void __launch_bounds__(256, 2)\nqk" << idx
+    auto tile_base = [&](const std::string& tid_var, const std::string& base_var) {
+        o << "  { unsigned long long k = (" << tid_var << " & tpt_mask) << " << r0 << ";\n"
+          << "    for (unsigned long long m = zmask; m; m &= m - 1ull) {\n"
+          << "      const unsigned long long lo = k & ((1ull << __builtin_ctzll(m)) - 1ull);\n"
+          << "      k = ((k ^ lo) << 1) | lo;\n    }\n"
+          << "    " << base_var << " = (" << tid_var << " >> log_tpt) * stride + (k | fix_val); }\n";
+    };
+    // thread part of a stage's HBM address (the tile base is OR-ed in)
+    auto gthread = [&](const Stage& st) {
+        std::string e = "(unsigned long long)(jb & " + std::to_string((1u << r0) - 1u) + "u)";
+        for (int i = 0; i < nh; ++i)
+            e += " | ((unsigned long long)((jb >> " + std::to_string(r0 + i) + ") & 1u) << " +
+                 std::to_string(p.hpos[i]) + ")";
+        (void)st;
+        return e;
+    };
+    o << "extern \"C\" __global__ void __launch_bounds__(" << stage_threads(H) << ", " << (H >= 7 ? 1 : 2)
+      << ")\nqk" << idx
       << "(double2* __restrict__ st, unsigned long long stride, unsigned long long tpt_mask, int log_tpt,"
-         " unsigned long long zmask, unsigned long long fix_val) {\n"
+         " unsigned long long zmask, unsigned long long fix_val, unsigned long long ntiles) {\n"
       << "  __shared__ double2 tile[" << T << "];\n"
       << "  char* const lds = reinterpret_cast<char*>(tile);\n"
-      << "  const unsigned tid = threadIdx.x;\n"
-      << tile_id_expr()
-      << "  unsigned long long k = (tile_id & tpt_mask) << " << r0 << ";\n"
-      << "  for (unsigned long long m = zmask; m; m &= m - 1ull) {\n"
-      << "    const unsigned long long lo = k & ((1ull << __builtin_ctzll(m)) - 1ull);\n"
-      << "    k = ((k ^ lo) << 1) | lo;\n  }\n";
-    o << "  const unsigned long long base = (tile_id >> log_tpt) * stride + (k | fix_val);\n";
+      << "  const unsigned tid = threadIdx.x;\n";
     o << "  double2";
     for (int r = 0; r < R; ++r) o << (r ? ", v" : " v") << r;
     o << ";\n";
     const int sb = p.stage_begin, se = p.stage_end;
-    for (int s = sb; s < se; ++s) {
-        const Stage& st = plan.stages[s];
-        o << "  {\n  const unsigned jb = " << jb_expr(st, RB) << ";\n";
-        auto gaddr = [&]() {
-            std::string e = "base | (unsigned long long)(jb & " + std::to_string((1u << r0) - 1u) + "u)";
-            for (int i = 0; i < nh; ++i)
-                e += " | ((unsigned long long)((jb >> " + std::to_string(r0 + i) + ") & 1u) << " +
-                     std::to_string(p.hpos[i]) + ")";
-            return e;
-        };
-        if (s == sb || s == se - 1) o << "  const unsigned long long gb = " << gaddr() << ";\n";
-        auto sigma_expr = [](const uint32_t* trow) {
-            std::string e = "jb";
-            for (int i = 0; i < 4; ++i)
-                e += " ^ ((__builtin_popcount(jb & " + std::to_string(trow[i]) + "u) & 1u) << " +
-                     std::to_string(i) + ")";
-            return e;
-        };
-        if (s != sb) o << "  const unsigned lb = 16u * (" << sigma_expr(st.trow_in) << ");\n";
-        if (s != se - 1) o << "  const unsigned lbw = 16u * (" << sigma_expr(st.trow_out) << ");\n";
-        if (s == sb) {
-            for (int r = 0; r < R; ++r) o << "  " << g.v(r) << " = qld(st + (gb | " << hexu(st.goff[r]) << "));\n";
-        } else {
-            for (int r = 0; r < R; ++r)
-                o << "  " << g.v(r) << " = *reinterpret_cast<const double2*>(lds + (lb ^ " << st.lds[r] << "u));\n";
-        }
-        for (int i = st.op_begin; i < st.op_end; ++i) g.op(plan.ops[i]);
-        if (s == se - 1) {
-            const double sc = std::ldexp(1.0, -(p.hu_count / 2)) * ((p.hu_count & 1) ? kInvSqrt2 : 1.0);
-            for (int r = 0; r < R; ++r) {
-                std::string val = g.v(r);
-                if (sc != 1.0) val = "make_double2(" + val + ".x * " + lit(sc) + ", " + val + ".y * " + lit(sc) + ")";
-                o << "  qst(st + (gb | " << hexu(st.goff[r]) << "), " << val << ");\n";
-            }
-        } else {
-            for (int r = 0; r < R; ++r)
-                o << "  *reinterpret_cast<double2*>(lds + (lbw ^ " << st.lds_w[r] << "u)) = " << g.v(r) << ";\n";
-            o << "  __syncthreads();\n";
-        }
+    if (pipe) {
+        // Persistent, software-pipelined: each workgroup walks tiles it = 0, 1, ... of its share
+        // (each XCD streams one contiguous eighth when the counts allow); the HBM loads of the
+        // next tile are issued right after the first stage's LDS write, so they are in flight
+        // during the LDS stages and the stores of the current tile (one big-LDS workgroup per CU
+        // otherwise leaves HBM idle between its load and store phases).
+        o << "  double2";
+        for (int r = 0; r < R; ++r) o << (r ? ", w" : " w") << r;
+        o << ";\n"
+          << "  const unsigned long long G = gridDim.x, b = blockIdx.x;\n"
+          << "  const bool xo = ((ntiles & 7ull) == 0ull) && ((G & 7ull) == 0ull);\n"
+          << "  const unsigned long long per = ntiles >> 3, gx = G >> 3;\n"
+          << "  unsigned long long it = 0;\n"
+          << "  auto tile_at = [&](unsigned long long i) { return xo ? (b & 7ull) * per + i * gx + (b >> 3) : i * G + b; };\n"
+          << "  auto tile_ok = [&](unsigned long long i) { return xo ? (i * gx + (b >> 3) < per) : (i * G + b < ntiles); };\n"
+          << "  if (!tile_ok(0)) return;\n"
+          << "  unsigned long long base, nbase = 0;\n"
+          << "  { const unsigned long long t0 = tile_at(0);\n";
+        tile_base("t0", "base");
         o << "  }\n";
+        {
+            const Stage& st0 = plan.stages[sb];
+            o << "  const unsigned long long gth0 = [&] { const unsigned jb = " << jb_expr(st0, RB) << "; return "
+              << gthread(st0) << "; }();\n";
+            for (int r = 0; r < R; ++r) o << "  v" << r << " = qld(st + (base | gth0 | " << hexu(st0.goff[r]) << "));\n";
+        }
+        // the tile body is emitted twice: a peeled first tile, then the loop, so the loop head is
+        // reached only with the previous tile's stores outstanding behind the prefetch (a single
+        // loop merges that state with the prologue's and waits for the stores too)
+    } else {
+        o << tile_id_expr() << "  unsigned long long base;\n";
+        tile_base("tile_id", "base");
+    }
+    auto body = [&]() {
+        for (int r = 0; r < R; ++r) g.nm[r] = r;
+        if (pipe) o << "  const bool more = tile_ok(it + 1);\n";
+        for (int s = sb; s < se; ++s) {
+            const Stage& st = plan.stages[s];
+            o << "  {\n  const unsigned jb = " << jb_expr(st, RB) << ";\n";
+            if (s == sb && pipe) o << "  const unsigned long long gb = base | gth0;\n";
+            else if (s == sb || s == se - 1) o << "  const unsigned long long gb = base | " << gthread(st) << ";\n";
+            auto sigma_expr = [](const uint32_t* trow) {
+                std::string e = "jb";
+                for (int i = 0; i < 4; ++i)
+                    e += " ^ ((__builtin_popcount(jb & " + std::to_string(trow[i]) + "u) & 1u) << " +
+                         std::to_string(i) + ")";
+                return e;
+            };
+            if (s != sb) o << "  const unsigned lb = 16u * (" << sigma_expr(st.trow_in) << ");\n";
+            if (s != se - 1) o << "  const unsigned lbw = 16u * (" << sigma_expr(st.trow_out) << ");\n";
+            if (s == sb) {
+                if (!pipe)
+                    for (int r = 0; r < R; ++r) o << "  " << g.v(r) << " = qld(st + (gb | " << hexu(st.goff[r]) << "));\n";
+            } else {
+                for (int r = 0; r < R; ++r)
+                    o << "  " << g.v(r) << " = *reinterpret_cast<const double2*>(lds + (lb ^ " << st.lds[r] << "u));\n";
+            }
+            for (int i = st.op_begin; i < st.op_end; ++i) g.op(plan.ops[i]);
+            if (s == se - 1) {
+                const double sc = std::ldexp(1.0, -(p.hu_count / 2)) * ((p.hu_count & 1) ? kInvSqrt2 : 1.0);
+                for (int r = 0; r < R; ++r) {
+                    std::string val = g.v(r);
+                    if (sc != 1.0) val = "make_double2(" + val + ".x * " + lit(sc) + ", " + val + ".y * " + lit(sc) + ")";
+                    o << "  qst(st + (gb | " << hexu(st.goff[r]) << "), " << val << ");\n";
+                }
+            } else {
+                for (int r = 0; r < R; ++r)
+                    o << "  *reinterpret_cast<double2*>(lds + (lbw ^ " << st.lds_w[r] << "u)) = " << g.v(r) << ";\n";
+                o << "  __syncthreads();\n";
+                if (pipe && s == sb) {  // prefetch the next tile's first-stage registers (the last
+                                        // tile re-reads itself: no branch around the loads)
+                    o << "  {\n    const unsigned long long tn = tile_at(more ? it + 1 : it);\n";
+                    tile_base("tn", "nbase");
+                    for (int r = 0; r < R; ++r)
+                        o << "    w" << r << " = qld(st + (nbase | gth0 | " << hexu(plan.stages[sb].goff[r]) << "));\n";
+                    o << "  }\n";
+                }
+            }
+            o << "  }\n";
+        }
+        if (pipe) {
+            o << "  if (!more) return;\n  __syncthreads();  // the last stage's LDS reads precede the next tile's writes\n"
+              << "  base = nbase;\n  ++it;\n";
+            for (int r = 0; r < R; ++r) o << "  v" << r << " = w" << r << ";\n";
+        }
+    };
+    if (pipe) {
+        body();
+        o << "  for (;;) {\n";
+        body();
+        o << "  }\n";
+    } else {
+        body();
     }
     o << "}\n";
     out << o.str();

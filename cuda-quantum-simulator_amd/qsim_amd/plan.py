@@ -61,6 +61,12 @@ def set_calibrate(mode: int = -1, min_qubits: int = -1) -> None:
     _lib.check(_lib.hip.qsim_set_calibrate(mode, min_qubits))
 
 
+def set_tile_height(h: int = -1) -> None:
+    """Tile height of fused passes planned from now on (qsim_set_tile_height): tiles of 6 + h
+    qubits, h in 0..7 (default 6); h < 0 restores the default."""
+    _lib.check(_lib.hip.qsim_set_tile_height(h))
+
+
 def plan_relabel(circuit: Circuit):
     """(perm, predicted_us_before, predicted_us_after): the logical -> physical qubit map the
     engine would choose for this circuit's fused plan (identity when none pays), host only."""

@@ -162,6 +162,12 @@ int qsim_state_perm(qsim_state* s, int32_t* perm);  /* current logical -> physic
  * model's choice and two alternatives with their compiled pass kernels (the basis state is
  * restored after each) and keeps the fastest.  Negative arguments leave a setting unchanged. */
 int qsim_set_calibrate(int mode, int min_qubits);
+/* Tile height of fused passes planned from now on (no reference counterpart): a tile spans 6 + h
+ * qubits (64 << h amplitudes in LDS).  h = 6 (12 qubits, 64 KiB, two workgroups per CU) is the
+ * default; h = 7 (13 qubits, 128 KiB, one 512-thread workgroup per CU, persistent pipelined
+ * kernels) needs fewer passes on some circuits but streams slower.  h < 0 restores
+ * the default (QSIM_TILE_HMAX); plans already cached for a circuit keep their height. */
+int qsim_set_tile_height(int h);
 /* Host-only: the permutation the engine would choose for this circuit (identity when none pays)
  * and the predicted pass-layout cost (microseconds, summed over the plan's passes) before/after. */
 int qsim_plan_relabel(int n_qubits, const qsim_gate* gates, size_t count, int32_t* perm,

@@ -103,7 +103,8 @@ def test_random_factory_on_one_qubit_uses_h_for_cnot(qsim):
 
 @pytest.mark.parametrize("n,depth,seed,hmax", [(8, 60, 1, 6), (12, 200, 2, 6), (20, 100, 42, 6),
                                                (20, 100, 7, 3), (30, 100, 42, 6), (9, 80, 5, 0),
-                                               (5, 40, 3, 6), (14, 150, 11, 4)])
+                                               (5, 40, 3, 6), (14, 150, 11, 4),
+                                               (14, 150, 11, 7), (20, 100, 1, 7), (30, 100, 42, 7)])
 def test_planner_reordering_preserves_circuit(qsim, oracle, n, depth, seed, hmax):
     from qsim_amd.plan import plan_fused
     c = qsim.createRandomCircuit(n, depth, seed) if n <= 14 else qsim.createRandomHCCircuit(n, depth, seed)
