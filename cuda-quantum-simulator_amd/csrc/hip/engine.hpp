@@ -169,8 +169,18 @@ constexpr int kTileR0 = 6;    // contiguous run bits of a staged tile (QSIM_TILE
 // hmax < 0: the process default (kTileHDefault, or QSIM_TILE_HMAX up to kTileHMax).
 // avoid: qubits no tile may contain (ops never act on them; only tile padding is affected).
 Plan plan_fused(const std::vector<Op>& ops, int n, int hmax = -1, uint64_t avoid = 0);
-int tile_height_default();             // the h that hmax < 0 means
+int tile_height_default();             // the h that hmax < 0 means (scope, setting, env, 6)
+int tile_height_for(int n);            // a single-GPU state's height (the setting, or by size)
 void tile_height_configure(int h);     // qsim_set_tile_height: h < 0 restores the env default
+// Plans made by this thread while the scope lives default to height h (qsim_run of a state).
+struct TileHeightScope {
+    explicit TileHeightScope(int h);
+    ~TileHeightScope();
+    TileHeightScope(const TileHeightScope&) = delete;
+    TileHeightScope& operator=(const TileHeightScope&) = delete;
+  private:
+    int prev_;
+};
 // Layout-aware qubit relabeling (relabel.hip): predicted cost of a tile (qubit mask) in
 // microseconds, the tiles of a plan's staged passes, and the permutation (logical -> physical)
 // minimising the predicted cost of `tiles` (empty: keep the identity, < min_gain better).

@@ -606,13 +606,31 @@ static int env_int(const char* k, int d) {
     return e ? std::atoi(e) : d;
 }
 
-static std::atomic<int> g_tile_h{-1};
+static std::atomic<int> g_tile_h{-1};  // qsim_set_tile_height (-1: not set)
+static thread_local int t_tile_h = -1;  // TileHeightScope of the calling thread
+static int env_tile_h() {                // QSIM_TILE_HMAX (-1: not set)
+    static const int v = std::getenv("QSIM_TILE_HMAX") ? std::min(kTileHMax, std::max(0, env_int("QSIM_TILE_HMAX", 6))) : -1;
+    return v;
+}
 int tile_height_default() {
+    if (t_tile_h >= 0) return t_tile_h;
     const int h = g_tile_h.load();
     if (h >= 0) return h;
-    static const int def = std::min(kTileHMax, std::max(0, env_int("QSIM_TILE_HMAX", kTileHDefault)));
-    return def;
+    const int e = env_tile_h();
+    return e >= 0 ? e : kTileHDefault;
 }
+// Single-GPU states without an explicit height: 13-qubit tiles from 26 to 28 qubits, where their
+// fewer passes outrun the slower streaming (W-HC 26q +23 %, 27q +15 %, 28q +5 %; 29q -3 %, 30q
+// -2 %: profiles/r02/h7s/).  QSIM_TILE_AUTO=0 keeps 12-qubit tiles everywhere.
+int tile_height_for(int n) {
+    const int h = g_tile_h.load();
+    if (h >= 0) return h;
+    if (env_tile_h() >= 0) return env_tile_h();
+    static const bool on = env_int("QSIM_TILE_AUTO", 1) != 0;
+    return on && n >= 26 && n <= 28 ? 7 : kTileHDefault;
+}
+TileHeightScope::TileHeightScope(int h) : prev_(t_tile_h) { t_tile_h = h; }
+TileHeightScope::~TileHeightScope() { t_tile_h = prev_; }
 void tile_height_configure(int h) {
     if (h > kTileHMax) fail(QSIM_ERR_INVALID_ARGUMENT, "tile height out of range (0..7)");
     g_tile_h.store(h < 0 ? -1 : h);

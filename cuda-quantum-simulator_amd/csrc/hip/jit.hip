@@ -308,8 +308,15 @@ void gen_pass(std::ostringstream& out, const Plan& plan, const FusedPass& p, int
           << "  const bool xo = ((ntiles & 7ull) == 0ull) && ((G & 7ull) == 0ull);\n"
           << "  const unsigned long long per = ntiles >> 3, gx = G >> 3;\n"
           << "  unsigned long long it = 0;\n"
-          << "  auto tile_at = [&](unsigned long long i) { return xo ? (b & 7ull) * per + i * gx + (b >> 3) : i * G + b; };\n"
-          << "  auto tile_ok = [&](unsigned long long i) { return xo ? (i * gx + (b >> 3) < per) : (i * G + b < ntiles); };\n"
+          ;
+        if (env_or("QSIM_JIT_PIPE_ORDER", 1) == 1)  // each workgroup streams one contiguous range (default)
+            o << "  const bool cw = (ntiles % G) == 0ull;\n  const unsigned long long tpw = ntiles / G;\n"
+              << "  auto tile_at = [&](unsigned long long i) { return cw ? b * tpw + i : i * G + b; };\n"
+              << "  auto tile_ok = [&](unsigned long long i) { return cw ? i < tpw : (i * G + b < ntiles); };\n";
+        else
+            o << "  auto tile_at = [&](unsigned long long i) { return xo ? (b & 7ull) * per + i * gx + (b >> 3) : i * G + b; };\n"
+              << "  auto tile_ok = [&](unsigned long long i) { return xo ? (i * gx + (b >> 3) < per) : (i * G + b < ntiles); };\n";
+        o
           << "  if (!tile_ok(0)) return;\n"
           << "  unsigned long long base, nbase = 0;\n"
           << "  { const unsigned long long t0 = tile_at(0);\n";

@@ -209,6 +209,7 @@ std::vector<int> choose_relabel(const std::vector<uint64_t>& tiles, int n, doubl
 // as the caller will (so the returned plan can be cached under the same key).
 LayoutChoice choose_layout(int n, const std::function<std::vector<Op>(const std::vector<int>&)>& lower,
                            int tries, size_t want_alts) {
+    const int h = tile_height_default();  // the calling thread's height, for the worker threads too
     struct Cand {
         std::vector<int> pi;
         size_t passes = 0;
@@ -226,7 +227,7 @@ LayoutChoice choose_layout(int n, const std::function<std::vector<Op>(const std:
     }
     auto plan_cand = [&](Cand& c) {
         try {  // (worker threads must not throw; a failed candidate just never wins)
-            const Plan p = plan_fused(lower(c.pi), n);
+            const Plan p = plan_fused(lower(c.pi), n, h);
             c.passes = p.passes.size();
             c.tiles = plan_tiles(p);
             c.cost = 0.0;
@@ -279,7 +280,7 @@ LayoutChoice choose_layout(int n, const std::function<std::vector<Op>(const std:
         for (int variant = 0; variant < 2; ++variant) {
             const std::vector<int>& pi = variant == 0 ? total[i] : cand[pool[i]].pi;
             std::vector<Op> ops = lower(pi);
-            Plan plan = plan_fused(ops, n);
+            Plan plan = plan_fused(ops, n, h);
             const double cost = plan_layout_cost_us(plan);
             const bool fewer = plan.passes.size() < out.passes_before;
             const bool cheaper = plan.passes.size() == out.passes_before && cost < out.cost_before * 0.97;
