@@ -500,7 +500,8 @@ int qsim_run(qsim_state* s, const qsim_gate* gates, size_t count, int flags) {
             }
             return ops;
         };
-        const TileHeightScope tile_h(tile_height_for(s->n));  // plans of this run (and its layout choice)
+        const int th = tile_height_for(s->n);
+        const TileHeightScope tile_h(th, tile_rb_for(s->n, th));  // plans of this run (and its layout choice)
         if ((flags & QSIM_RUN_FUSED) && s->basis && s->perm.empty() && count > 0 && relabel_enabled(s->n)) {
             // First run on a basis state: choose the qubit labels for fewer passes and faster
             // pass layouts (relabel.hip: choose_layout).

@@ -100,6 +100,7 @@ struct FusedPass {
     int h = 0;             // tile = 64 << h amplitudes (tile bits 0 .. 5 + h)
     int r0 = 6;            // tile bits 0 .. r0-1 are qubits 0 .. r0-1 (2^r0-amplitude HBM runs)
     int hpos[10] = {0};    // ascending physical qubits of tile bits r0 .. 5 + h (all >= r0)
+    int rb = 4;            // staged: register bits per stage (threads per workgroup = 64 << h >> rb)
     int op_begin = 0, op_end = 0;  // range in the pass-op buffer (unstaged kernel)
     int stage_begin = 0, stage_end = 0;  // range in Plan::stages (staged kernel, h >= 4)
     int hu_count = 0;      // unnormalized H butterflies in the pass: store scales by 2^(-k/2)
@@ -172,14 +173,17 @@ Plan plan_fused(const std::vector<Op>& ops, int n, int hmax = -1, uint64_t avoid
 int tile_height_default();             // the h that hmax < 0 means (scope, setting, env, 6)
 int tile_height_for(int n);            // a single-GPU state's height (the setting, or by size)
 void tile_height_configure(int h);     // qsim_set_tile_height: h < 0 restores the env default
-// Plans made by this thread while the scope lives default to height h (qsim_run of a state).
+int tile_rb_default(int heff);         // register bits per stage of a staged pass of height heff
+int tile_rb_for(int n, int h);         // a single-GPU state's stage width (-1: stage_rb(h))
+// Plans made by this thread while the scope lives default to height h and, for 12-qubit tiles,
+// rb register bits per stage (qsim_run of a state).
 struct TileHeightScope {
-    explicit TileHeightScope(int h);
+    explicit TileHeightScope(int h, int rb = -1);
     ~TileHeightScope();
     TileHeightScope(const TileHeightScope&) = delete;
     TileHeightScope& operator=(const TileHeightScope&) = delete;
   private:
-    int prev_;
+    int prev_, prev_rb_;
 };
 // Layout-aware qubit relabeling (relabel.hip): predicted cost of a tile (qubit mask) in
 // microseconds, the tiles of a plan's staged passes, and the permutation (logical -> physical)

@@ -629,8 +629,25 @@ int tile_height_for(int n) {
     static const bool on = env_int("QSIM_TILE_AUTO", 1) != 0;
     return on && n >= 26 && n <= 28 ? 7 : kTileHDefault;
 }
-TileHeightScope::TileHeightScope(int h) : prev_(t_tile_h) { t_tile_h = h; }
-TileHeightScope::~TileHeightScope() { t_tile_h = prev_; }
+static thread_local int t_tile_rb = -1;
+// Small states (12-qubit tiles, at most 2^14 tiles... i.e. n <= 20): 256 tiles of 256 threads
+// leave one 4-wave workgroup per CU, so the passes are latency-bound; 8 amplitudes per thread
+// (512 threads) doubles the waves for the same tile (QSIM_TILE_RB overrides: 2..4).
+int tile_rb_for(int n, int h) {
+    if (h != 6) return -1;
+    static const int env = env_int("QSIM_TILE_RB", 0);
+    if (env >= 2 && env <= 4) return env;
+    return n >= 12 && n <= 20 ? 3 : -1;
+}
+int tile_rb_default(int heff) { return heff == 6 && t_tile_rb >= 2 ? t_tile_rb : stage_rb(heff); }
+TileHeightScope::TileHeightScope(int h, int rb) : prev_(t_tile_h), prev_rb_(t_tile_rb) {
+    t_tile_h = h;
+    t_tile_rb = rb;
+}
+TileHeightScope::~TileHeightScope() {
+    t_tile_h = prev_;
+    t_tile_rb = prev_rb_;
+}
 void tile_height_configure(int h) {
     if (h > kTileHMax) fail(QSIM_ERR_INVALID_ARGUMENT, "tile height out of range (0..7)");
     g_tile_h.store(h < 0 ? -1 : h);
@@ -718,7 +735,8 @@ Plan plan_fused(const std::vector<Op>& ops, int n, int hmax, uint64_t avoid) {
             tsrc.push_back(op.src);
         }
         if (heff >= 4) {
-            plan_stages(tops, tsrc, 6 + heff, stage_rb(heff), plan, p);
+            p.rb = tile_rb_default(heff);
+            plan_stages(tops, tsrc, 6 + heff, p.rb, plan, p);
         } else {
             p.op_begin = (int)plan.ops.size();
             for (size_t i = 0; i < tops.size(); ++i) {
@@ -1132,10 +1150,10 @@ __device__ __forceinline__ uint32_t stage_jb(const Stage& st) {
 // register bits, so a wave still moves 64 consecutive amplitudes = one 1 KiB run per
 // instruction); only the stages in between round-trip through LDS (read, ops, write, barrier).
 // A pass whose ops fit one such stage never touches LDS.
-template <int H, bool NT, bool FR = false>
-__global__ __launch_bounds__(stage_threads(H), H >= 7 ? 1 : 2) void k_fused_staged(FArgs a) {  // LDS-bound: 2 WGs/CU (h <= 6), 1 at h = 7
+template <int H, bool NT, bool FR = false, int RBT = stage_rb(H)>
+__global__ __launch_bounds__((64 << H) >> RBT, H >= 7 ? 1 : 2) void k_fused_staged(FArgs a) {  // LDS-bound: 2 WGs/CU (h <= 6), 1 at h = 7
     constexpr int T = 64 << H;
-    constexpr int RB = stage_rb(H);
+    constexpr int RB = RBT;
     constexpr int R = 1 << RB;
     __shared__ double2 tile[T];
     const uint64_t tile_id = blockIdx.x;
@@ -1281,13 +1299,25 @@ void launch_fused(double2* st, int n, uint64_t batch, const Plan& plan, const Ti
             unsigned long long stride = a.stride, tpt = a.tpt_mask, zm = a.zmask, fv = a.fix_val, ntiles = blocks;
             int lt_arg = lt;
             void* args[] = {&a.st, &stride, &tpt, &lt_arg, &zm, &fv, &ntiles};
-            const unsigned nthr = (unsigned)stage_threads(p.h);
+            const unsigned nthr = (unsigned)((64 << p.h) >> p.rb);
             // a pipelined (persistent) kernel gets the resident workgroups only and walks its tiles
             const uint64_t grid = jit_pass_pipelined(p) ? std::min<uint64_t>(blocks, pipe_workgroups(p.h)) : blocks;
             if (grid * nthr > 0xffffffffull) fail(QSIM_ERR_RUNTIME, "pass grid too large");
             // grid in work-items; the events (if any) time the dispatch packet itself
             QSIM_HIPCHK(hipExtModuleLaunchKernel(jm->fn[pi], (uint32_t)(grid * nthr), 1, 1, nthr, 1, 1, 0, s,
                                                  args, nullptr, ev0, ev1, 0));
+            continue;
+        }
+        if (p.h >= 4 && p.rb != stage_rb(p.h)) {  // narrower stages (small states): 512 / 1024 threads
+            if (p.h != 6 || p.rb < 2 || p.rb > 3) fail(QSIM_ERR_RUNTIME, "unsupported stage width");
+            if (p.rb == 3) {
+                if (nt) hipExtLaunchKernelGGL((k_fused_staged<6, true, false, 3>), dim3((unsigned)blocks), dim3(512), 0, s, ev0, ev1, 0, a);
+                else hipExtLaunchKernelGGL((k_fused_staged<6, false, false, 3>), dim3((unsigned)blocks), dim3(512), 0, s, ev0, ev1, 0, a);
+            } else {
+                if (nt) hipExtLaunchKernelGGL((k_fused_staged<6, true, false, 2>), dim3((unsigned)blocks), dim3(1024), 0, s, ev0, ev1, 0, a);
+                else hipExtLaunchKernelGGL((k_fused_staged<6, false, false, 2>), dim3((unsigned)blocks), dim3(1024), 0, s, ev0, ev1, 0, a);
+            }
+            QSIM_HIPCHK(hipGetLastError());
             continue;
         }
         switch (p.h) {

@@ -257,7 +257,7 @@ std::string tile_id_expr() {
 }
 
 void gen_pass(std::ostringstream& out, const Plan& plan, const FusedPass& p, int idx) {
-    const int H = p.h, RB = stage_rb(H), R = 1 << RB, T = 64 << H;
+    const int H = p.h, RB = p.rb, R = 1 << RB, T = 64 << H;
     const int r0 = p.r0, nh = 6 + H - r0;
     const bool pipe = jit_pass_pipelined(p);
     Gen g;
@@ -284,7 +284,7 @@ void gen_pass(std::ostringstream& out, const Plan& plan, const FusedPass& p, int
         (void)st;
         return e;
     };
-    o << "extern \"C\" __global__ void __launch_bounds__(" << stage_threads(H) << ", " << (H >= 7 ? 1 : 2)
+    o << "extern \"C\" __global__ void __launch_bounds__(" << (T >> RB) << ", " << (H >= 7 ? 1 : 2)
       << ")\nqk" << idx
       << "(double2* __restrict__ st, unsigned long long stride, unsigned long long tpt_mask, int log_tpt,"
          " unsigned long long zmask, unsigned long long fix_val, unsigned long long ntiles) {\n"
