@@ -630,9 +630,9 @@ int tile_height_for(int n) {
     return on && n >= 26 && n <= 28 ? 7 : kTileHDefault;
 }
 static thread_local int t_tile_rb = -1;
-// Small states (12-qubit tiles, at most 2^14 tiles... i.e. n <= 20): 256 tiles of 256 threads
-// leave one 4-wave workgroup per CU, so the passes are latency-bound; 8 amplitudes per thread
-// (512 threads) doubles the waves for the same tile (QSIM_TILE_RB overrides: 2..4).
+// Small states (12-qubit tiles, n <= 20: at most 256 tiles, i.e. at most one 4-wave workgroup
+// per CU): 8 amplitudes per thread (512 threads) doubles the waves for the same tile — W-HC 18q
+// +14 %, 20q unchanged (profiles/r02/rb/).  QSIM_TILE_RB overrides (2..4).
 int tile_rb_for(int n, int h) {
     if (h != 6) return -1;
     static const int env = env_int("QSIM_TILE_RB", 0);
