@@ -697,9 +697,29 @@ Plan plan_fused(const std::vector<Op>& ops, int n, int hmax, uint64_t avoid) {
             add_single(ch.ops.front());
             continue;
         }
-        const int r0 = ch.r0;
-        const int nfree = 6 + heff - r0;
+        int r0 = ch.r0, hp = heff;
         uint64_t hi = ch.hi;
+        // Mixed heights: a pass of a 13-qubit plan whose gates fit a 12-qubit tile runs as one
+        // (two workgroups per CU stream faster than one big one; the pass count is unchanged).
+        // Longer runs first.  QSIM_TILE_MIX=0 keeps every pass at the plan's height.
+        static const bool mix = env_int("QSIM_TILE_MIX", 1) != 0;
+        if (heff == 7 && mix) {
+            uint64_t need = 0;
+            for (const Op& op : ch.ops) {
+                need |= op.cmask | (1ull << op.t0);
+                if (op.kind == K_SWAP) need |= 1ull << op.t1;
+            }
+            for (int r = 6; r >= 4; --r) {
+                const uint64_t above = need & ~((1ull << r) - 1ull);
+                if (__builtin_popcountll(above) <= 12 - r) {
+                    hp = 6;
+                    r0 = r;
+                    hi = above;
+                    break;
+                }
+            }
+        }
+        const int nfree = 6 + hp - r0;
         // Pad the tile to nfree chosen qubits (uniform tile size / occupancy).
         for (int q = r0; q < n && __builtin_popcountll(hi) < nfree; ++q)
             if (!((avoid >> q) & 1ull)) hi |= 1ull << q;
@@ -708,7 +728,7 @@ Plan plan_fused(const std::vector<Op>& ops, int n, int hmax, uint64_t avoid) {
         // the whole shard)
         for (int q = r0; q < n && __builtin_popcountll(hi) < nfree; ++q) hi |= 1ull << q;
         FusedPass p;
-        p.h = heff;
+        p.h = hp;
         p.r0 = r0;
         double bpa = 0.0;
         for (const Op& op : ch.ops) bpa += op_alg_bytes(op, 1.0);
@@ -734,9 +754,9 @@ Plan plan_fused(const std::vector<Op>& ops, int n, int hmax, uint64_t avoid) {
             tops.back().step = op.src;
             tsrc.push_back(op.src);
         }
-        if (heff >= 4) {
-            p.rb = tile_rb_default(heff);
-            plan_stages(tops, tsrc, 6 + heff, p.rb, plan, p);
+        if (hp >= 4) {
+            p.rb = tile_rb_default(hp);
+            plan_stages(tops, tsrc, 6 + hp, p.rb, plan, p);
         } else {
             p.op_begin = (int)plan.ops.size();
             for (size_t i = 0; i < tops.size(); ++i) {

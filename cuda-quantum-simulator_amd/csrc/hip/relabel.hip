@@ -128,6 +128,16 @@ double layout_cost_us(uint64_t tile) {
         c += kW1[q[i]];
         for (int j = i + 1; j < k; ++j) c += kW2[q[i]][q[j]];
     }
+    // The model was fitted on 12-qubit tiles; a 13-qubit tile (one 128 KiB workgroup per CU,
+    // persistent pipelined kernel) streams ~1.2-1.3x slower per pass (profiles/r02/h7s/).
+    // QSIM_LAYOUT_T13 scales its predicted cost, steering the label search toward plans whose
+    // passes fit 12-qubit tiles (mixed heights): 1.25 gave W-HC 30q seed 42 at h = 7 4 224 gates/s
+    // but 28q 16.2 k instead of 18.3 k (profiles/r02/mix2/), so the default stays 1.
+    static const double t13 = [] {
+        const char* e = std::getenv("QSIM_LAYOUT_T13");
+        return e ? std::atof(e) : 1.0;
+    }();
+    if (__builtin_popcountll(tile) >= 13) c *= t13;
     return c;
 }
 

@@ -32,7 +32,8 @@ def test_generated_kernels_are_persistent_at_h7(qsim, tile7):
     from qsim_amd.plan import jit_source
     src = jit_source(qsim.createRandomHCCircuit(30, 100, 42))
     kernels = re.findall(r"__launch_bounds__\((\d+), (\d+)\)\nqk\d+", src)
-    assert kernels and all(k == ("512", "1") for k in kernels)
+    # 13-qubit passes, plus passes whose gates fit 12 qubits (mixed heights, QSIM_TILE_MIX)
+    assert ("512", "1") in kernels and all(k in (("512", "1"), ("256", "2")) for k in kernels)
     assert "__shared__ double2 tile[8192]" in src
     # multi-stage passes walk their tiles (peeled first tile + loop) and prefetch the next one
     assert "for (;;)" in src and "tile_at(more ? it + 1 : it)" in src
