@@ -13,3 +13,7 @@ for n in (26, 27, 28, 29, 30):
     d = json.load(open('$O/bench%d.json' % n)); r = d['roofline']
     print(n, d['value'], d['ms_per_step'], round(r['frac'], 4), r['launches'], r['avg_launch_ms'])
 PY
+for NT in 0 1; do
+  QSIM_JIT_NT=$NT timeout -k 10 300 python bench.py --qubits 20 --cpu-budget 0 > $O/bench20_nt$NT.json 2> $O/bench20_nt$NT.err || exit 1
+  python -c "import json; d=json.load(open('$O/bench20_nt$NT.json')); print('20q NT=$NT', d['value'], d['roofline']['avg_launch_ms'])"
+done
