@@ -303,11 +303,17 @@ def run_batch(args):
 def main():
     args = parse()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
-        # No launcher around us: start the N rank processes ourselves (before anything here
-        # touches the GPU) and relay rank 0's JSON line (qsim_amd/launch.py).
-        from qsim_amd.launch import launch_ranks
-        sys.exit(launch_ranks(os.path.abspath(__file__), sys.argv[1:], args.gpus,
-                              timeout_s=args.launch_timeout))
+        # No launcher around us: start the N rank processes ourselves and relay rank 0's JSON
+        # line (qsim_amd/launch.py).  launch.py is loaded by file path, not through the package:
+        # importing qsim_amd would load libqsim_hip.so (and RCCL / hipRTC) into this parent,
+        # which never uses the GPU.
+        import importlib.util
+        spec = importlib.util.spec_from_file_location(
+            "qsim_launch", os.path.join(ROOT, "cuda-quantum-simulator_amd", "qsim_amd", "launch.py"))
+        launch = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(launch)
+        sys.exit(launch.launch_ranks(os.path.abspath(__file__), sys.argv[1:], args.gpus,
+                                     timeout_s=args.launch_timeout))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if args.workload == "batch":
         if world > 1 or args.dry_run:

@@ -152,7 +152,7 @@ DevBuf::~DevBuf() {
     if (ptr) (void)hipFree(ptr);
 }
 TimedLaunch::TimedLaunch(Timer* t, const char* name, double by, hipStream_t s, bool e)
-    : tm(t), bytes(by), ext(e) {
+    : tm(t), bytes(by), ext(e), stream(s) {
     if (tm && tm->enabled) {
         tm->stream = s;
         if (ext) tm->begin_ext(name, &a, &b, &slot);
@@ -164,6 +164,7 @@ TimedLaunch::TimedLaunch(Timer* t, const char* name, double by, hipStream_t s, b
 TimedLaunch::~TimedLaunch() {
     if (tm) {
         try {
+            tm->stream = stream;  // a nested launch on another stream may have moved it
             if (ext) tm->finish(slot, a, b, bytes);
             else tm->end(slot, a, bytes);
         } catch (...) {
@@ -305,6 +306,14 @@ static bool calibrate_layout(qsim_state* s, LayoutChoice& lc) {
     } catch (...) {
         (void)hipEventDestroy(e0);
         (void)hipEventDestroy(e1);
+        // a candidate may have run partway: put the basis state back (best effort) or, if even
+        // that fails, stop treating the amplitudes as that basis state (no relabeling later)
+        try {
+            launch_init_basis(s->d, s->n, 1, s->basis_idx, s->stream);
+            QSIM_HIPCHK(hipStreamSynchronize(s->stream));
+        } catch (...) {
+            s->basis = false;
+        }
         throw;
     }
     (void)hipEventDestroy(e0);

@@ -22,8 +22,10 @@
 #include <thread>
 #include <climits>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -80,7 +82,10 @@ static uint64_t deposit_bits(uint64_t v, uint64_t mask) {  // bit j of v -> j-th
 // link at ~60 GB/s).  Pivots are local positions >= 6 (never a tile's contiguous run) outside the
 // exchanged positions, added greedily (up to kMaxPivots) while T drops; each candidate set is
 // scored by planning both steps with it avoided, in parallel, on RANK 0's ops (`ref`: the same
-// skeleton on every rank), so every rank picks the same pivots.  QSIM_DIST_PIVOTS caps m
+// skeleton on every rank), so every rank picks the same pivots.  Everything else the score reads
+// is rank-independent too: the positions the step before must also avoid come from this rank's
+// own marks (`steps`, set by the same decisions on every rank), never from `ref`'s roles (which
+// are only marked when `ref` aliases `steps`, i.e. on rank 0).  QSIM_DIST_PIVOTS caps m
 // (default kMaxPivots); QSIM_DIST_PIVOT_PLAN=0: one pivot by the cheaper gate-level score
 // (trailing / leading gates that do not touch the position).
 static void mark_overlap(std::vector<DStep>& steps, int L, int world, const std::vector<DStep>& ref) {
@@ -124,7 +129,7 @@ static void mark_overlap(std::vector<DStep>& steps, int L, int world, const std:
         const DStep& rA = ref[i - 1];
         const DStep& rB = ref[i + 1];
         if (by_plan && !rA.ops.empty() && !rB.ops.empty() && !cand.empty()) {
-            const uint64_t avoidA0 = (rA.role & 2) ? steps[i - 2].pmask : 0ull;
+            const uint64_t avoidA0 = (A.role & 2) ? steps[i - 2].pmask : 0ull;
             // T of a pivot set (pass counts in units of one pass); +inf when planning failed
             auto model = [&](uint64_t set) {
                 const Plan pA = plan_fused(rA.ops, L, -1, avoidA0 | set);
@@ -493,7 +498,10 @@ struct XArgs {
     uint64_t orval;     // part exchange: the pivot bits' values
 };
 
-__device__ __forceinline__ uint64_t xlocal(const XArgs& a, uint64_t e) {
+// Local amplitude index of element e of the slab buffer (slab c = e >> chunk_log): the offset's
+// bits are spread around the zero-inserted positions, then slab bits go to lpos and the part's
+// pivot values are or-ed in.  Host and device: qsim_dist_slab_map exports the same map.
+__host__ __device__ __forceinline__ uint64_t xlocal(const XArgs& a, uint64_t e) {
     const uint64_t c = e >> a.chunk_log;
     uint64_t off = e & (a.chunk - 1);
 #pragma unroll
@@ -544,12 +552,24 @@ struct Shard {
     double2* recvbuf = nullptr;
 };
 
-// Real mode: one shard per process, peers reached through an RCCL communicator.
-// Virtual mode (qsim_dist_create_virtual): all W shards in this process on one GPU, exchanged by
-// device copies — the same planner, per-rank lowering and pack/unpack kernels, no RCCL.
+// Every mode runs the same per-shard code (planning per rank, pack / unpack, the slab posts of
+// one remap part); only the transport that carries the posts differs:
+//   T_RCCL    one shard per process, grouped ncclSend / ncclRecv over xGMI (production);
+//   T_VIRTUAL all W shards in this process on one GPU (qsim_dist_create_virtual): the posts of
+//             the W shards are paired by RCCL's matching rule and moved by device copies, or by
+//             ncclSend / ncclRecv to rank 0 of a world-1 communicator (qsim_dist_virtual_rccl);
+//   T_HOSTED  one shard per process, the posts staged through host memory and handed to a
+//             caller-supplied function (qsim_dist_create_hosted: multi-process runs without RCCL,
+//             e.g. several ranks on one GPU in tests).
 struct qsim_dist {
+    enum Transport { T_RCCL = 0, T_VIRTUAL = 1, T_HOSTED = 2 };
     int n = 0, g = 0, L = 0, world = 1, device = 0;
     bool virt = false;
+    Transport transport = T_RCCL;
+    qsim_dist_transport_fn host_fn = nullptr;
+    void* host_ctx = nullptr;
+    char* h_stage = nullptr;  // hosted: pinned staging (send half, receive half), grow-only
+    size_t h_stage_bytes = 0;
     std::vector<Shard> shards;
     double* d_partials = nullptr;
     double* d_result = nullptr;
@@ -607,7 +627,10 @@ struct qsim_dist {
         if (copy_stream) (void)hipStreamDestroy(copy_stream);
         if (comm_stream) (void)hipStreamDestroy(comm_stream);
         if (stream) (void)hipStreamDestroy(stream);
+        if (h_stage) (void)hipHostFree(h_stage);
     }
+    // this rank's remap traffic in the last run (bytes sent; the same are received)
+    double sent_bytes = 0.0;
 };
 
 namespace {
@@ -723,23 +746,25 @@ void init_zero(qsim_dist* d) {
     QSIM_HIPCHK(hipStreamSynchronize(d->stream));
 }
 
+// The slab layout of one remap (or one part of an overlapped remap) on one rank: the pack /
+// unpack map (XArgs) and the rank each slab goes to and comes from.  Host-only and rank-local;
+// qsim_dist_slab_map exports it for the CPU tests.
 struct XPlan {
     XArgs a;
     int peer_of[256];
 };
 // part < 0: the whole shard; part j: the amplitudes whose pivot bits hold the bits of j.
-XPlan xplan(const qsim_dist* d, const Shard& sh, const DStep& ex, int part = -1) {
+XPlan xplan(int L, int rank, const DStep& ex, int part = -1) {
     XPlan x{};
     XArgs& a = x.a;
-    a.st = sh.d;
     a.k = ex.k;
     const bool h = part >= 0;
-    a.chunk_log = d->L - ex.k - (h ? __builtin_popcountll(ex.pmask) : 0);
+    a.chunk_log = L - ex.k - (h ? __builtin_popcountll(ex.pmask) : 0);
     a.chunk = 1ull << a.chunk_log;
     for (int j = 0; j < ex.k; ++j) {
         a.lpos[j] = ex.lpos[j];
         a.sorted[j] = ex.lpos[j];
-        a.my_c |= ((sh.rank >> (ex.gpos[j] - d->L)) & 1) << j;
+        a.my_c |= ((rank >> (ex.gpos[j] - L)) & 1) << j;
     }
     a.nsorted = ex.k;
     if (h) {
@@ -748,13 +773,18 @@ XPlan xplan(const qsim_dist* d, const Shard& sh, const DStep& ex, int part = -1)
     }
     std::sort(a.sorted, a.sorted + a.nsorted);
     for (int c = 0; c < (1 << ex.k); ++c) {
-        int peer = sh.rank;
+        int peer = rank;
         for (int j = 0; j < ex.k; ++j) {
-            const int b = ex.gpos[j] - d->L;
+            const int b = ex.gpos[j] - L;
             peer = (peer & ~(1 << b)) | (((c >> j) & 1) << b);
         }
         x.peer_of[c] = peer;
     }
+    return x;
+}
+XPlan xplan(const qsim_dist* d, const Shard& sh, const DStep& ex, int part = -1) {
+    XPlan x = xplan(d->L, sh.rank, ex, part);
+    x.a.st = sh.d;
     return x;
 }
 void copy_kernel(bool pack, XArgs a, uint64_t lo, int sub_log, hipStream_t s) {
@@ -781,10 +811,31 @@ static int pipeline_parts(uint64_t chunk) {
 // Qubit remap: rank r sends its amplitudes with local bits lpos == c to the rank whose bits at
 // gpos are c, and stores what that rank sends at local bits == c (the swap of the two qubit
 // sets, SURVEY §8(e) "global<->local qubit swap by all-to-all").
-// Virtual mode: move one slab between two shards of this process — a device copy, or, with a
+//
+// One point-to-point transfer posted by a shard: `amps` amplitudes at `send` go to rank `peer`
+// and `amps` amplitudes from `peer` land at `recv` — one ncclSend / ncclRecv pair of a group on
+// the multi-rank path.  Posts pair up by RCCL's rule: the k-th post of rank r naming q matches
+// the k-th post of rank q naming r (and must carry the same count).
+struct Post {
+    int rank, peer;
+    const double2* send;
+    double2* recv;
+    uint64_t amps;
+};
+// The posts of one remap part of shard `sh`: slab c (c != my_c) is the `amps` amplitudes at
+// base + c * stride of the send / receive buffers; it goes to and comes from rank peer_of[c].
+// Every transport runs this same per-shard loop (one shard per process, or all of them).
+void slab_posts(std::vector<Post>& out, const Shard& sh, const XPlan& x, int k, uint64_t base,
+                uint64_t stride, uint64_t amps) {
+    for (int c = 0; c < (1 << k); ++c) {
+        if (c == x.a.my_c) continue;
+        const uint64_t at = base + (uint64_t)c * stride;
+        out.push_back({sh.rank, x.peer_of[c], sh.sendbuf + at, sh.recvbuf + at, amps});
+    }
+}
+// Virtual transport: move one matched slab inside this process — a device copy, or, with a
 // world-1 communicator attached (qsim_dist_virtual_rccl), an ncclSend / ncclRecv pair to rank 0
-// itself inside the caller's group (RCCL matches them in issue order), which runs the same RCCL
-// call sequence as the multi-rank path on one GPU.
+// itself inside the caller's group (RCCL matches them in issue order).
 void virt_move(qsim_dist* d, double2* dst, const double2* src, uint64_t amps) {
     if (!d->comm) {
         QSIM_HIPCHK(hipMemcpyAsync(dst, src, amps * sizeof(double2), hipMemcpyDeviceToDevice, d->comm_stream));
@@ -792,6 +843,91 @@ void virt_move(qsim_dist* d, double2* dst, const double2* src, uint64_t amps) {
     }
     QSIM_NCCLCHK(ncclSend(src, (size_t)amps * 2, ncclDouble, 0, d->comm, d->comm_stream));
     QSIM_NCCLCHK(ncclRecv(dst, (size_t)amps * 2, ncclDouble, 0, d->comm, d->comm_stream));
+}
+// Hosted transport: hand host-staged copies of this rank's posts to the caller's function (which
+// must move them between the rank processes with the same matching rule) and copy what arrived
+// back.  Synchronous on the comm stream; for tests, not for speed.
+void host_call(qsim_dist* d, const std::vector<qsim_dist_post>& hp, const char* what) {
+    const int rc = d->host_fn(d->host_ctx, hp.data(), hp.size());
+    if (rc != 0) fail(QSIM_ERR_DEVICE, std::string("host transport failed (") + std::to_string(rc) + ") during " + what);
+}
+char* host_stage(qsim_dist* d, size_t bytes) {
+    if (bytes > d->h_stage_bytes) {
+        if (d->h_stage) QSIM_HIPCHK(hipHostFree(d->h_stage));
+        d->h_stage = nullptr;
+        d->h_stage_bytes = 0;
+        QSIM_HIPCHK(hipHostMalloc((void**)&d->h_stage, bytes, hipHostMallocDefault));
+        d->h_stage_bytes = bytes;
+    }
+    return d->h_stage;
+}
+void host_transfers(qsim_dist* d, const std::vector<Post>& posts, const char* what) {
+    size_t total = 0;
+    for (const Post& p : posts) total += p.amps * sizeof(double2);
+    char* snd = host_stage(d, 2 * total);
+    char* rcv = snd + total;
+    std::vector<qsim_dist_post> hp(posts.size());
+    size_t at = 0;
+    for (size_t i = 0; i < posts.size(); ++i) {
+        const size_t b = posts[i].amps * sizeof(double2);
+        QSIM_HIPCHK(hipMemcpyAsync(snd + at, posts[i].send, b, hipMemcpyDeviceToHost, d->comm_stream));
+        hp[i] = {posts[i].peer, 0, (uint64_t)b, snd + at, rcv + at};
+        at += b;
+    }
+    QSIM_HIPCHK(hipStreamSynchronize(d->comm_stream));
+    host_call(d, hp, what);
+    at = 0;
+    for (size_t i = 0; i < posts.size(); ++i) {
+        const size_t b = posts[i].amps * sizeof(double2);
+        QSIM_HIPCHK(hipMemcpyAsync(posts[i].recv, rcv + at, b, hipMemcpyHostToDevice, d->comm_stream));
+        at += b;
+    }
+    QSIM_HIPCHK(hipStreamSynchronize(d->comm_stream));
+}
+// Carry the posts of one remap part on d->comm_stream (which has already waited for the packs).
+void post_transfers(qsim_dist* d, const std::vector<Post>& posts, const char* what) {
+    if (posts.empty()) return;
+    double sent = 0.0;
+    for (const Post& p : posts) sent += (double)p.amps * sizeof(double2);
+    d->sent_bytes += sent / (double)d->shards.size();
+    TimedLaunch tl(&d->timer, "xgmi_transfer", 2.0 * sent / (double)d->shards.size(), d->comm_stream);
+    switch (d->transport) {
+        case qsim_dist::T_RCCL:
+            QSIM_NCCLCHK(ncclGroupStart());
+            for (const Post& p : posts) {
+                QSIM_NCCLCHK(ncclSend(p.send, (size_t)p.amps * 2, ncclDouble, p.peer, d->comm, d->comm_stream));
+                QSIM_NCCLCHK(ncclRecv(p.recv, (size_t)p.amps * 2, ncclDouble, p.peer, d->comm, d->comm_stream));
+            }
+            QSIM_NCCLCHK(ncclGroupEnd());
+            comm_settle(d, what);
+            return;
+        case qsim_dist::T_HOSTED:
+            host_transfers(d, posts, what);
+            return;
+        case qsim_dist::T_VIRTUAL: {
+            // pair shard r's k-th post naming q with shard q's k-th post naming r; what r sends
+            // lands where q receives (a mismatch is exactly what would hang a multi-rank run)
+            std::map<std::pair<int, int>, std::vector<size_t>> by_pair;
+            for (size_t i = 0; i < posts.size(); ++i) by_pair[{posts[i].rank, posts[i].peer}].push_back(i);
+            if (d->comm) QSIM_NCCLCHK(ncclGroupStart());
+            for (const auto& kv : by_pair) {
+                const auto it = by_pair.find({kv.first.second, kv.first.first});
+                if (it == by_pair.end() || it->second.size() != kv.second.size())
+                    fail(QSIM_ERR_RUNTIME, std::string("unmatched slab transfer during ") + what);
+                for (size_t j = 0; j < kv.second.size(); ++j) {
+                    const Post& s = posts[kv.second[j]];
+                    const Post& r = posts[it->second[j]];
+                    if (s.amps != r.amps) fail(QSIM_ERR_RUNTIME, std::string("slab size mismatch during ") + what);
+                    virt_move(d, r.recv, s.send, s.amps);
+                }
+            }
+            if (d->comm) {
+                QSIM_NCCLCHK(ncclGroupEnd());
+                comm_settle(d, what);
+            }
+            return;
+        }
+    }
 }
 
 void exchange(qsim_dist* d, const DStep& ex) {
@@ -821,37 +957,11 @@ void exchange(qsim_dist* d, const DStep& ex) {
         QSIM_HIPCHK(hipEventRecord(d->events[p], d->stream));
     }
     for (int p = 0; p < parts; ++p) {
-        const uint64_t off = (uint64_t)p * sub;
         QSIM_HIPCHK(hipStreamWaitEvent(d->comm_stream, d->events[p], 0));
-        if (!d->virt) {
-            const Shard& sh = d->shards[0];
-            const XPlan& x = xs[0];
-            QSIM_NCCLCHK(ncclGroupStart());
-            for (int c = 0; c < (1 << ex.k); ++c) {
-                if (c == x.a.my_c) continue;
-                const size_t cnt = (size_t)sub * 2;
-                const uint64_t at = (uint64_t)c * chunk + off;
-                QSIM_NCCLCHK(ncclSend(sh.sendbuf + at, cnt, ncclDouble, x.peer_of[c], d->comm, d->comm_stream));
-                QSIM_NCCLCHK(ncclRecv(sh.recvbuf + at, cnt, ncclDouble, x.peer_of[c], d->comm, d->comm_stream));
-            }
-            QSIM_NCCLCHK(ncclGroupEnd());
-            comm_settle(d, "remap send/recv");
-        } else {  // shard r's slab c goes to shard peer(c), into that shard's slot my_c(r)
-            if (d->comm) QSIM_NCCLCHK(ncclGroupStart());
-            for (size_t i = 0; i < d->shards.size(); ++i) {
-                const XPlan& x = xs[i];
-                for (int c = 0; c < (1 << ex.k); ++c) {
-                    if (c == x.a.my_c) continue;
-                    Shard& dst = d->shards[x.peer_of[c]];
-                    virt_move(d, dst.recvbuf + (uint64_t)x.a.my_c * chunk + off,
-                              d->shards[i].sendbuf + (uint64_t)c * chunk + off, sub);
-                }
-            }
-            if (d->comm) {
-                QSIM_NCCLCHK(ncclGroupEnd());
-                comm_settle(d, "virtual remap send/recv");
-            }
-        }
+        std::vector<Post> posts;
+        for (size_t i = 0; i < d->shards.size(); ++i)
+            slab_posts(posts, d->shards[i], xs[i], ex.k, (uint64_t)p * sub, chunk, sub);
+        post_transfers(d, posts, "remap send/recv");
         QSIM_HIPCHK(hipEventRecord(d->events[parts + p], d->comm_stream));
     }
     for (int p = 0; p < parts; ++p) {
@@ -885,37 +995,10 @@ void exchange_parts(qsim_dist* d, const DStep& ex) {
         }
         QSIM_HIPCHK(hipEventRecord(d->pev[8 + h], d->copy_stream));
         QSIM_HIPCHK(hipStreamWaitEvent(d->comm_stream, d->pev[8 + h], 0));
-        if (!d->virt) {
-            const Shard& sh = d->shards[0];
-            const XPlan& x = xs[0];
-            double2* sb = sh.sendbuf + (uint64_t)h * part_amps;
-            double2* rb = sh.recvbuf + (uint64_t)h * part_amps;
-            QSIM_NCCLCHK(ncclGroupStart());
-            for (int c = 0; c < (1 << ex.k); ++c) {
-                if (c == x.a.my_c) continue;
-                QSIM_NCCLCHK(ncclSend(sb + (uint64_t)c * chunk, (size_t)chunk * 2, ncclDouble, x.peer_of[c],
-                                      d->comm, d->comm_stream));
-                QSIM_NCCLCHK(ncclRecv(rb + (uint64_t)c * chunk, (size_t)chunk * 2, ncclDouble, x.peer_of[c],
-                                      d->comm, d->comm_stream));
-            }
-            QSIM_NCCLCHK(ncclGroupEnd());
-            comm_settle(d, "overlapped remap send/recv");
-        } else {
-            if (d->comm) QSIM_NCCLCHK(ncclGroupStart());
-            for (size_t i = 0; i < d->shards.size(); ++i) {
-                const XPlan& x = xs[i];
-                for (int c = 0; c < (1 << ex.k); ++c) {
-                    if (c == x.a.my_c) continue;
-                    Shard& dst = d->shards[x.peer_of[c]];
-                    virt_move(d, dst.recvbuf + (uint64_t)h * part_amps + (uint64_t)x.a.my_c * chunk,
-                              d->shards[i].sendbuf + (uint64_t)h * part_amps + (uint64_t)c * chunk, chunk);
-                }
-            }
-            if (d->comm) {
-                QSIM_NCCLCHK(ncclGroupEnd());
-                comm_settle(d, "virtual overlapped remap send/recv");
-            }
-        }
+        std::vector<Post> posts;
+        for (size_t i = 0; i < d->shards.size(); ++i)
+            slab_posts(posts, d->shards[i], xs[i], ex.k, (uint64_t)h * part_amps, chunk, chunk);
+        post_transfers(d, posts, "overlapped remap send/recv");
         QSIM_HIPCHK(hipEventRecord(d->pev[16 + h], d->comm_stream));
         QSIM_HIPCHK(hipStreamWaitEvent(d->copy_stream, d->pev[16 + h], 0));
         for (size_t i = 0; i < d->shards.size(); ++i) {
@@ -927,9 +1010,23 @@ void exchange_parts(qsim_dist* d, const DStep& ex) {
     }
 }
 
+// Sum of one double over the ranks (virtual: `local` already sums every shard; with a world-1
+// communicator the all-reduce below runs anyway, as an identity).  Hosted: every rank sends its
+// value to every other and sums in rank order (the same order, so the same result, everywhere).
 double allreduce_sum(qsim_dist* d, double local) {
-    if (!d->comm) return local;  // virtual: `local` already sums every shard (with a world-1
-                                 // communicator the all-reduce below runs anyway, as an identity)
+    if (d->transport == qsim_dist::T_HOSTED) {
+        const int me = d->shards[0].rank;
+        std::vector<double> vals(d->world, 0.0);
+        vals[me] = local;
+        std::vector<qsim_dist_post> hp;
+        for (int r = 0; r < d->world; ++r)
+            if (r != me) hp.push_back({r, 0, sizeof(double), &local, &vals[r]});
+        host_call(d, hp, "all-reduce");
+        double s = 0.0;
+        for (double v : vals) s += v;
+        return s;
+    }
+    if (!d->comm) return local;
     QSIM_HIPCHK(hipMemcpyAsync(d->d_result, &local, sizeof(double), hipMemcpyHostToDevice, d->stream));
     QSIM_NCCLCHK(ncclAllReduce(d->d_result, d->d_result, 1, ncclDouble, ncclSum, d->comm, d->stream));
     comm_settle(d, "all-reduce");
@@ -1017,6 +1114,29 @@ qsim_dist::RunPlan& run_plan(qsim_dist* d, const qsim_gate* gates, size_t count)
     d->run_plans.push_back(std::move(rp));
     return *d->run_plans.back();
 }
+// Physical (rank-major) amplitudes -> logical index order (dst: 2 * 2^n doubles).  The map
+// i -> p(i) moves bit q to perm[q], so p is the OR of per-11-bit-chunk tables; threads split i.
+void unpermute(const qsim_dist* d, const std::vector<double2>& phys, double* dst) {
+    const int n = d->n, nch = (n + 10) / 11;
+    std::vector<uint64_t> tab((size_t)nch << 11, 0);
+    for (int c = 0; c < nch; ++c)
+        for (uint64_t v = 0; v < 2048; ++v)
+            for (int b = 0; b < 11 && c * 11 + b < n; ++b)
+                if ((v >> b) & 1ull) tab[((size_t)c << 11) + v] |= 1ull << d->perm[c * 11 + b];
+    const uint64_t N = 1ull << n;
+    const unsigned T = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(16, N >> 16));
+    std::vector<std::thread> th;
+    for (unsigned t = 0; t < T; ++t)
+        th.emplace_back([&, t] {
+            for (uint64_t i = N * t / T; i < N * (t + 1) / T; ++i) {
+                uint64_t p = 0;
+                for (int c = 0; c < nch; ++c) p |= tab[((size_t)c << 11) + ((i >> (11 * c)) & 2047)];
+                dst[2 * i] = phys[p].x;
+                dst[2 * i + 1] = phys[p].y;
+            }
+        });
+    for (auto& x : th) x.join();
+}
 }  // namespace
 
 extern "C" {
@@ -1094,6 +1214,7 @@ int qsim_dist_create_virtual(int n_qubits, int world, int device, qsim_dist** ou
         d->world = world;
         d->device = device;
         d->virt = true;
+        d->transport = qsim_dist::T_VIRTUAL;
         d->perm.resize(n_qubits);
         QSIM_HIPCHK(hipSetDevice(device));
         QSIM_HIPCHK(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
@@ -1104,6 +1225,36 @@ int qsim_dist_create_virtual(int n_qubits, int world, int device, qsim_dist** ou
         std::vector<int> ranks(world);
         for (int r = 0; r < world; ++r) ranks[r] = r;
         alloc_shards(d.get(), ranks);
+        init_zero(d.get());
+        *out = d.release();
+    });
+}
+
+int qsim_dist_create_hosted(int n_qubits, int rank, int world, int device, qsim_dist_transport_fn fn,
+                            void* ctx, qsim_dist** out) {
+    return dguard([&] {
+        if (!out || !fn) fail(QSIM_ERR_INVALID_ARGUMENT, "null argument");
+        *out = nullptr;
+        const int g = log2_exact(world);
+        if (rank < 0 || rank >= world) fail(QSIM_ERR_INVALID_ARGUMENT, "rank out of range");
+        check_sizes(n_qubits, g);
+        auto d = std::make_unique<qsim_dist>();
+        d->n = n_qubits;
+        d->g = g;
+        d->L = n_qubits - g;
+        d->world = world;
+        d->device = device;
+        d->transport = qsim_dist::T_HOSTED;
+        d->host_fn = fn;
+        d->host_ctx = ctx;
+        d->perm.resize(n_qubits);
+        QSIM_HIPCHK(hipSetDevice(device));
+        QSIM_HIPCHK(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
+        QSIM_HIPCHK(hipStreamCreateWithFlags(&d->comm_stream, hipStreamNonBlocking));
+        QSIM_HIPCHK(hipStreamCreateWithFlags(&d->copy_stream, hipStreamNonBlocking));
+        for (hipEvent_t& e : d->pev) QSIM_HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        d->timer.stream = d->stream;
+        alloc_shards(d.get(), {rank});
         init_zero(d.get());
         *out = d.release();
     });
@@ -1171,12 +1322,23 @@ int qsim_dist_run(qsim_dist* d, const qsim_gate* gates, size_t count, int flags)
                     if (d->perm[q] < d->L) d->perm[q] = pi[d->perm[q]];
         }
         d->fresh = false;
+        d->sent_bytes = 0.0;
         qsim_dist::RunPlan& rp = run_plan(d, gates, count);
         const auto& plans = rp.steps;
         const size_t S = d->shards.size();
         for (size_t i = 1; i < S; ++i)
             if (plans[i].size() != plans[0].size()) fail(QSIM_ERR_RUNTIME, "exchange skeleton mismatch");
         d->overlapped = 0;
+        static const bool dbg = std::getenv("QSIM_DIST_DEBUG") != nullptr;
+        if (dbg) {  // the exchange skeleton this run executes (kind, k, pivot mask, role)
+            std::string line = "[dist] rank " + std::to_string(d->shards[0].rank) + " perm_in";
+            for (int q = 0; q < d->n; ++q) line += " " + std::to_string(rp.perm_in[q]);
+            line += " |";
+            for (const DStep& st : plans[0])
+                line += st.kind == 1 ? " X" + std::to_string(st.k) + ":" + std::to_string(st.pmask)
+                                     : " O" + std::to_string(st.ops.size()) + "r" + std::to_string(st.role);
+            std::fprintf(stderr, "%s\n", line.c_str());
+        }
         int pending = 0;  // parts of an overlapped remap still to be waited for (0: none)
         auto wait_pending = [&]() {
             for (int h = 0; h < pending; ++h) QSIM_HIPCHK(hipStreamWaitEvent(d->stream, d->pev[24 + h], 0));
@@ -1237,6 +1399,13 @@ int qsim_dist_run(qsim_dist* d, const qsim_gate* gates, size_t count, int flags)
     });
 }
 
+int qsim_dist_remap_bytes(qsim_dist* d, double* sent) {
+    return dguard([&] {
+        need(d);
+        if (sent) *sent = d->sent_bytes;
+    });
+}
+
 int qsim_dist_overlapped(qsim_dist* d, int* remaps) {
     return dguard([&] {
         need(d);
@@ -1279,6 +1448,21 @@ int qsim_dist_gather_state(qsim_dist* d, double* dst) {
         QSIM_HIPCHK(hipSetDevice(d->device));
         const uint64_t shard = 1ull << d->L;
         const bool root = d->virt || d->shards[0].rank == 0;
+        if (d->transport == qsim_dist::T_HOSTED) {  // host-staged: rank 0 receives every shard
+            std::vector<double2> phys(root ? (1ull << d->n) : shard);
+            QSIM_HIPCHK(hipMemcpyAsync(phys.data(), d->shards[0].d,
+                                       sizeof(double2) * shard, hipMemcpyDeviceToHost, d->stream));
+            QSIM_HIPCHK(hipStreamSynchronize(d->stream));
+            std::vector<qsim_dist_post> hp;
+            if (root)
+                for (int r = 1; r < d->world; ++r)
+                    hp.push_back({r, 0, sizeof(double2) * shard, nullptr, phys.data() + r * shard});
+            else
+                hp.push_back({0, 0, sizeof(double2) * shard, phys.data(), nullptr});
+            host_call(d, hp, "gather");
+            if (root && dst) unpermute(d, phys, dst);
+            return;
+        }
         double2* all = nullptr;
         if (root) QSIM_HIPCHK(hipMalloc((void**)&all, (sizeof(double2) << d->n)));
         if (d->virt) {
@@ -1303,14 +1487,7 @@ int qsim_dist_gather_state(qsim_dist* d, double* dst) {
             std::vector<double2> phys(1ull << d->n);
             QSIM_HIPCHK(hipMemcpy(phys.data(), all, sizeof(double2) << d->n, hipMemcpyDeviceToHost));
             QSIM_HIPCHK(hipFree(all));
-            if (dst) {
-                for (uint64_t i = 0; i < (1ull << d->n); ++i) {  // logical index -> physical
-                    uint64_t p = 0;
-                    for (int q = 0; q < d->n; ++q) p |= ((i >> q) & 1ull) << d->perm[q];
-                    dst[2 * i] = phys[p].x;
-                    dst[2 * i + 1] = phys[p].y;
-                }
-            }
+            if (dst) unpermute(d, phys, dst);
         }
     });
 }
@@ -1457,6 +1634,51 @@ int qsim_dist_plan_passes(int n, int world, int rank, const qsim_gate* gates, si
         if (n_steps) *n_steps = st.size();
         if (perm_inout)
             for (int q = 0; q < n; ++q) perm_inout[q] = perm[q];
+    });
+}
+
+int qsim_dist_plan_memo_clear(void) {
+    return dguard([&] {
+        std::lock_guard<std::mutex> l(g_pivot_mu);
+        g_pivots.clear();
+    });
+}
+
+int qsim_dist_slab_map(int n, int world, int rank, const qsim_dist_step* step, int part,
+                       int32_t* my_c, int32_t* peer_of, uint64_t* index, size_t index_cap) {
+    return dguard([&] {
+        const int g = log2_exact(world);
+        check_sizes(n, g);
+        if (rank < 0 || rank >= world) fail(QSIM_ERR_INVALID_ARGUMENT, "rank out of range");
+        if (!step || step->kind != 1 || step->k < 1 || step->k > g)
+            fail(QSIM_ERR_INVALID_ARGUMENT, "not an exchange step");
+        const int L = n - g;
+        DStep ex;
+        ex.kind = 1;
+        ex.k = step->k;
+        uint64_t used = 0;
+        for (int j = 0; j < ex.k; ++j) {
+            ex.gpos[j] = step->gpos[j];
+            ex.lpos[j] = step->lpos[j];
+            if (ex.gpos[j] < L || ex.gpos[j] >= n || ex.lpos[j] < 0 || ex.lpos[j] >= L ||
+                ((used >> ex.lpos[j]) & 1ull))
+                fail(QSIM_ERR_INVALID_ARGUMENT, "bad exchange positions");
+            used |= 1ull << ex.lpos[j];
+        }
+        ex.pmask = step->pmask;
+        if (ex.pmask & (used | ~((1ull << L) - 1)))
+            fail(QSIM_ERR_INVALID_ARGUMENT, "bad pivot mask");
+        const int m = __builtin_popcountll(ex.pmask);
+        if (part >= (1 << m)) fail(QSIM_ERR_INVALID_ARGUMENT, "part out of range");
+        const XPlan x = xplan(L, rank, ex, part < 0 ? -1 : part);
+        if (my_c) *my_c = x.a.my_c;
+        if (peer_of)
+            for (int c = 0; c < (1 << ex.k); ++c) peer_of[c] = x.peer_of[c];
+        const uint64_t count = (uint64_t)x.a.chunk << ex.k;
+        if (index) {
+            if (index_cap < count) fail(QSIM_ERR_INVALID_ARGUMENT, "index buffer too small");
+            for (uint64_t e = 0; e < count; ++e) index[e] = xlocal(x.a, e);
+        }
     });
 }
 

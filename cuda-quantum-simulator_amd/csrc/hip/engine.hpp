@@ -365,6 +365,7 @@ struct Scratch {
 // packet with no extra packets; the launch site must pass them.
 struct TimedLaunch {
     Timer* tm; int slot = -1; hipEvent_t a = nullptr, b = nullptr; double bytes; bool ext = false;
+    hipStream_t stream;  // the end event goes on the stream the begin event went on
     TimedLaunch(Timer* t, const char* name, double b, hipStream_t s, bool ext = false);
     hipEvent_t start() const { return a; }  // null when profiling is off
     hipEvent_t stop() const { return b; }

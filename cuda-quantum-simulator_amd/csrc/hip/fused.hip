@@ -1303,6 +1303,9 @@ void launch_fused(double2* st, int n, uint64_t batch, const Plan& plan, const Ti
                 for (int o = plan.stages[k].op_begin; o < plan.stages[k].op_end; ++o)
                     if (plan.ops[o].step >= 0) framed = true;
         if (framed) {  // batched noisy run: non-Clifford ops under the trajectory's Pauli frame
+            // the framed kernels exist at the default stage width only (their stage descriptors
+            // must have been built for it)
+            if (p.rb != stage_rb(p.h)) fail(QSIM_ERR_RUNTIME, "framed pass with a narrowed stage width");
             a.frames = frames;
             a.nbatch = (int)batch;
             switch (p.h) {

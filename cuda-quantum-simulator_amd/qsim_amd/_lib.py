@@ -164,14 +164,27 @@ class qsim_dist_step(Structure):
                 ("pmask", c_uint64)]
 
 
+class qsim_dist_post(Structure):
+    _fields_ = [("peer", c_int32), ("_pad", c_int32), ("bytes", c_uint64), ("send", c_void_p),
+                ("recv", c_void_p)]
+
+
+qsim_dist_transport_fn = ctypes.CFUNCTYPE(c_int, c_void_p, POINTER(qsim_dist_post), c_size_t)
+
 _sig(hip, "qsim_dist_unique_id", [_P])
 _sig(hip, "qsim_dist_create", [c_int, c_int, c_int, _P, c_int, POINTER(_P)])
 _sig(hip, "qsim_dist_create_virtual", [c_int, c_int, c_int, POINTER(_P)])
+_sig(hip, "qsim_dist_create_hosted", [c_int, c_int, c_int, c_int, qsim_dist_transport_fn, _P,
+                                      POINTER(_P)])
 _sig(hip, "qsim_dist_virtual_rccl", [_P, c_char_p])
 _sig(hip, "qsim_dist_destroy", [_P])
 _sig(hip, "qsim_dist_run", [_P, POINTER(qsim_gate), c_size_t, c_int])
 _sig(hip, "qsim_dist_sync", [_P])
 _sig(hip, "qsim_dist_overlapped", [_P, POINTER(c_int)])
+_sig(hip, "qsim_dist_remap_bytes", [_P, POINTER(c_double)])
+_sig(hip, "qsim_dist_plan_memo_clear", [])
+_sig(hip, "qsim_dist_slab_map", [c_int, c_int, c_int, POINTER(qsim_dist_step), c_int, POINTER(c_int32),
+                                 POINTER(c_int32), POINTER(c_uint64), c_size_t])
 _sig(hip, "qsim_dist_reset", [_P])
 _sig(hip, "qsim_dist_perm", [_P, POINTER(c_int32)])
 _sig(hip, "qsim_dist_local_state", [_P, _P])

@@ -56,6 +56,40 @@ class DistributedSimulator:
             _lib.check(_lib.hip.qsim_dist_virtual_rccl(sim._h, buf))
         return sim
 
+    @classmethod
+    def hosted(cls, num_qubits: int, rank: int, world: int, transport, device: int = 0
+               ) -> "DistributedSimulator":
+        """One shard per process, as the RCCL path, but every transfer goes through the Python
+        callable `transport(posts)` (qsim_dist_create_hosted): `posts` is a list of
+        (peer, send, recv) with `send` / `recv` memoryviews of host staging (either may be None
+        for a one-sided post); the k-th post naming q must meet q's k-th post naming this rank.
+        An exception in `transport` fails the engine call.  Lets several rank processes share
+        one GPU (tests: the per-rank planning and exchange of the multi-rank path without RCCL)."""
+        sim = cls.__new__(cls)
+        sim._h = _c.c_void_p()
+        sim._n, sim._world, sim._rank, sim._virtual = num_qubits, world, rank, False
+        sim._transport_error = None
+
+        def cb(_ctx, posts, count):
+            try:
+                items = []
+                for i in range(count):
+                    p = posts[i]
+                    snd = (memoryview((_c.c_char * p.bytes).from_address(p.send)).cast("B")
+                           if p.send else None)
+                    rcv = (memoryview((_c.c_char * p.bytes).from_address(p.recv)).cast("B")
+                           if p.recv else None)
+                    items.append((p.peer, snd, rcv))
+                transport(items)
+                return 0
+            except BaseException as e:  # noqa: BLE001 — reported through the engine's error
+                sim._transport_error = e
+                return 1
+        sim._cb = _lib.qsim_dist_transport_fn(cb)  # kept alive with the object
+        _lib.check(_lib.hip.qsim_dist_create_hosted(num_qubits, rank, world, device, sim._cb, None,
+                                                    _c.byref(sim._h)))
+        return sim
+
     def __del__(self):
         self.close()
 
@@ -82,6 +116,12 @@ class DistributedSimulator:
         v = _c.c_int(0)
         _lib.check(_lib.hip.qsim_dist_overlapped(self._h, _c.byref(v)))
         return v.value
+    def remapBytes(self) -> float:
+        """Bytes this rank sent in the last run's remaps (it received as many)."""
+        v = _c.c_double(0)
+        _lib.check(_lib.hip.qsim_dist_remap_bytes(self._h, _c.byref(v)))
+        return v.value
+
     def reset(self) -> None: _lib.check(_lib.hip.qsim_dist_reset(self._h))
 
     def perm(self) -> List[int]:
@@ -137,7 +177,8 @@ def plan(circuit: Circuit, world: int, rank: int, perm: Optional[List[int]] = No
     arr, cnt = circuit.to_abi()
     p = (_c.c_int32 * n)(*(perm if perm is not None else range(n)))
     ns, no = _c.c_size_t(0), _c.c_size_t(0)
-    _lib.check(_lib.hip.qsim_dist_plan(n, world, rank, arr, cnt, None, None, 0, _c.byref(ns),
+    p_size = (_c.c_int32 * n)(*p)  # size the output for the SAME start map (the call updates it)
+    _lib.check(_lib.hip.qsim_dist_plan(n, world, rank, arr, cnt, p_size, None, 0, _c.byref(ns),
                                        None, 0, _c.byref(no)))
     steps = (_lib.qsim_dist_step * max(1, ns.value))()
     ops = (_lib.qsim_op * max(1, no.value))()
@@ -151,9 +192,35 @@ def plan(circuit: Circuit, world: int, rank: int, perm: Optional[List[int]] = No
     for s in steps[:ns.value]:
         if s.kind == 1:
             out_steps.append({"kind": "exchange", "k": s.k, "gpos": list(s.gpos[:s.k]),
-                              "lpos": list(s.lpos[:s.k]), "pivot": s.pivot,
+                              "lpos": list(s.lpos[:s.k]), "pivot": s.pivot, "pmask": s.pmask,
                               "pivots": [b for b in range(64) if (s.pmask >> b) & 1]})
         else:
             out_steps.append({"kind": "ops", "ops": out_ops[s.op_begin:s.op_end],
                               "role": s.role, "pivot": s.pivot})
     return out_steps, list(p)
+
+
+def plan_memo_clear() -> None:
+    """Forget the process-wide pivot memo: the next plan() decides as a fresh rank process."""
+    _lib.check(_lib.hip.qsim_dist_plan_memo_clear())
+
+
+def slab_map(n: int, world: int, rank: int, step: dict, part: int = -1):
+    """The pack / unpack layout of exchange `step` (a plan() dict) on `rank`, as the engine's
+    kernels use it (qsim_dist_slab_map): (my_c, peer_of, index) where slab c goes to and comes
+    from rank peer_of[c] and index[c * chunk + e] is the local amplitude index of its element e.
+    part >= 0: part `part` of an overlapped remap (the pivot bits hold `part`)."""
+    st = _lib.qsim_dist_step()
+    st.kind, st.k = 1, step["k"]
+    for j in range(step["k"]):
+        st.gpos[j], st.lpos[j] = step["gpos"][j], step["lpos"][j]
+    st.pmask = step.get("pmask", 0)
+    g = world.bit_length() - 1
+    m = bin(st.pmask).count("1") if part >= 0 else 0
+    count = 1 << (n - g - m)
+    my_c = _c.c_int32(0)
+    peer_of = (_c.c_int32 * (1 << st.k))()
+    index = np.empty(count, dtype=np.uint64)
+    _lib.check(_lib.hip.qsim_dist_slab_map(n, world, rank, _c.byref(st), part, _c.byref(my_c), peer_of,
+                                           index.ctypes.data_as(_c.POINTER(_c.c_uint64)), count))
+    return my_c.value, list(peer_of), index.astype(np.int64)

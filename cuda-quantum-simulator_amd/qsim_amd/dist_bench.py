@@ -112,6 +112,8 @@ def run(args, metric: str, peak_gbps: float) -> None:
     wall = grp.all_reduce_max(t1 - t0)
     stats = sim.profileStats()
     gates = circuit.getGateCount()
+    comm = comm_summary(stats, args.steps, wall, sim.remapBytes())
+    comms = [json.loads(b.decode()) for b in grp.all_gather(json.dumps(comm).encode())]
     if rank == 0:
         dom = max((s for s in stats if s["name"] != "alltoall_remap"), key=lambda s: s["ms"],
                   default=None)
@@ -135,10 +137,37 @@ def run(args, metric: str, peak_gbps: float) -> None:
                        "pass_kernels": "jit" if jit else "interpreter",
                        "parallelism": f"state sharded by high qubits over {world} GPUs (RCCL all-to-all remaps)"},
             "roofline": roof, "kernels_rank0": stats, "cpu_baseline": None,
+            "comm": dict(comms[0], per_rank_transfer_ms=[c["transfer_ms_per_step"] for c in comms],
+                         max_exposed_ms=max(c["exposed_ms_per_step"] for c in comms)),
         }
         print(json.dumps(out), flush=True)
     sim.close()
     grp.close()
+
+
+REMAP_STATS = ("alltoall_remap", "xgmi_transfer")
+
+
+def comm_summary(stats, steps: int, wall_s: float, sent_last_run: float) -> dict:
+    """This rank's remap traffic and where its time went, per step (events on the engine's
+    streams, csrc/hip/dist.hip): `xgmi_transfer` spans the grouped ncclSend / ncclRecv of every
+    remap part on the comm stream (its bytes: sent + received); the local pass kernels run on the
+    compute stream.  exposed = step time - local kernel time (what the remaps add to the step);
+    overlapped = transfer time hidden behind local work."""
+    by = {s["name"]: s for s in stats}
+    xfer = by.get("xgmi_transfer", {"ms": 0.0, "alg_bytes": 0.0, "launches": 0})
+    local_ms = sum(s["ms"] for s in stats if s["name"] not in REMAP_STATS) / max(1, steps)
+    step_ms = wall_s / max(1, steps) * 1e3
+    t_ms = xfer["ms"] / max(1, steps)
+    sent = xfer["alg_bytes"] / 2 / max(1, steps)
+    exposed = max(0.0, step_ms - local_ms)
+    return {"bytes_sent_per_step": sent, "bytes_sent_last_run": sent_last_run,
+            "transfer_ms_per_step": round(t_ms, 4),
+            "transfer_parts_per_step": xfer["launches"] / max(1, steps),
+            "sent_GBps": round(sent / (t_ms / 1e3) / 1e9, 2) if t_ms > 0 else None,
+            "local_kernel_ms_per_step": round(local_ms, 4),
+            "exposed_ms_per_step": round(exposed, 4),
+            "overlapped_ms_per_step": round(max(0.0, t_ms - exposed), 4)}
 
 
 def split_trajectories(total: int, world: int, rank: int):

@@ -6,8 +6,10 @@ libc10_hip asks for the unversioned soname, so the loader cannot reuse /opt/rocm
 process then aborts in the duplicated runtimes' static destructors at exit.  The sharded bench
 only needs three host-side operations between ranks of ONE node — broadcast the 128-byte RCCL
 unique id, barrier, max over ranks of a wall time — so they go through small files in a
-directory private to the job (key: the launcher's pid, MASTER_PORT and TORCHELASTIC_RUN_ID; every
-rank of one torchrun / bench launcher has the same parent).  All state traffic is RCCL.
+directory private to the job (key: the launcher's pid, MASTER_PORT, TORCHELASTIC_RUN_ID and
+TORCHELASTIC_RESTART_COUNT; every rank of one torchrun / bench launcher has the same parent, and a
+restarted attempt gets a fresh directory instead of reading the crashed attempt's files, e.g. an
+old RCCL unique id).  All state traffic is RCCL.
 
 Every wait is bounded (QSIM_DIST_INIT_TIMEOUT, default 300 s): a rank that never arrives makes
 the others raise instead of hanging.
@@ -28,8 +30,9 @@ class FileGroup:
         if key is None:
             key = os.environ.get("QSIM_RDZV_KEY")  # set by qsim_amd/launch.py
         if key is None:
-            key = "{}_{}_{}".format(os.getppid(), os.environ.get("MASTER_PORT", "0"),
-                                    os.environ.get("TORCHELASTIC_RUN_ID", "none"))
+            key = "{}_{}_{}_r{}".format(os.getppid(), os.environ.get("MASTER_PORT", "0"),
+                                        os.environ.get("TORCHELASTIC_RUN_ID", "none"),
+                                        os.environ.get("TORCHELASTIC_RESTART_COUNT", "0"))
         self.dir = os.path.join(root or tempfile.gettempdir(), "qsim_rdzv_" + key)
         self.timeout = float(timeout_s if timeout_s is not None
                              else os.environ.get("QSIM_DIST_INIT_TIMEOUT", "300"))

@@ -341,10 +341,26 @@ int qsim_dist_create_virtual(int n_qubits, int world, int device, qsim_dist** ou
  * its all-reduces through RCCL — the multi-rank call sequence (non-blocking init, groups,
  * settle, watchdog) on one GPU (tests). */
 int qsim_dist_virtual_rccl(qsim_dist* d, const void* unique_id);
+/* Host-staged transport (no RCCL): one shard per process like qsim_dist_create, but every
+ * point-to-point transfer is handed to `fn` as host buffers.  A post sends `bytes` from `send` to
+ * rank `peer` and receives `bytes` from `peer` into `recv` (either may be NULL for a one-sided
+ * post); posts pair up as grouped ncclSend / ncclRecv do: the k-th post of rank r naming q
+ * with the k-th post of q naming r.  `fn` returns 0 on success.  Used to run several rank
+ * processes on one GPU (tests); no counterpart in the reference (single-GPU, README.md:361-367). */
+typedef struct qsim_dist_post {
+    int32_t peer, _pad;
+    uint64_t bytes;
+    const void* send;
+    void* recv;
+} qsim_dist_post;
+typedef int (*qsim_dist_transport_fn)(void* ctx, const qsim_dist_post* posts, size_t count);
+int qsim_dist_create_hosted(int n_qubits, int rank, int world, int device, qsim_dist_transport_fn fn,
+                            void* ctx, qsim_dist** out);
 int qsim_dist_destroy(qsim_dist* d);
 int qsim_dist_run(qsim_dist* d, const qsim_gate* gates, size_t count, int flags);
 int qsim_dist_sync(qsim_dist* d);
 int qsim_dist_overlapped(qsim_dist* d, int* remaps); /* remaps of the last run that overlapped local work */
+int qsim_dist_remap_bytes(qsim_dist* d, double* sent); /* bytes this rank sent in its last run's remaps */
 int qsim_dist_reset(qsim_dist* d);                         /* |0..0>, identity qubit map */
 int qsim_dist_perm(qsim_dist* d, int32_t* perm);            /* logical -> physical, n entries */
 /* This rank's 2*2^(n-g) doubles (virtual mode: all shards in rank order, 2*2^n doubles). */
@@ -369,6 +385,17 @@ int qsim_dist_plan(int n_qubits, int world, int rank, const qsim_gate* gates, si
  * `cap` counts steps.  perm_inout updated as by qsim_dist_plan. */
 int qsim_dist_plan_passes(int n_qubits, int world, int rank, const qsim_gate* gates, size_t count,
                           int32_t* perm_inout, int32_t* passes, size_t cap, size_t* n_steps);
+
+/* Host-only: forget the process-wide memo of remap pivots (planning is then redone from scratch,
+ * as in a fresh rank process). */
+int qsim_dist_plan_memo_clear(void);
+/* Host-only: the slab layout the pack / unpack kernels use for exchange step `step` on `rank`.
+ * part < 0: the whole remap; part j: part j of an overlapped remap (its pivot bits hold j).
+ * my_c: the slab that stays; peer_of[c], c < 2^k: the rank slab c goes to and comes from;
+ * index[c * chunk + e] (e < chunk = 2^(L - k - m), m = pivots of a part, 0 for part < 0): the
+ * local amplitude index of element e of slab c.  index_cap counts entries (2^(L - m) needed). */
+int qsim_dist_slab_map(int n_qubits, int world, int rank, const qsim_dist_step* step, int part,
+                       int32_t* my_c, int32_t* peer_of, uint64_t* index, size_t index_cap);
 
 #define QSIM_MAX_QUBITS_SINGLE 30
 #define QSIM_MIN_QUBITS 1

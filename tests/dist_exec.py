@@ -2,8 +2,9 @@
 a numpy shard, with every qubit-remap exchange carried out over torch.distributed (gloo, CPU).
 
 This checks the multi-GPU logic — per-rank lowering of global controls/phases, the lookahead
-remap choice, the pack/peer/unpack index mapping and the final logical<->physical un-permutation —
-with real inter-process collectives and no GPU.  Op semantics follow engine.hpp (M1 / DIAG / SWAP).
+remap choice, the pivots of overlapped remaps (planned independently in every rank process), the
+engine's own pack/peer/unpack index maps (qsim_dist_slab_map, the C++ the kernels use) and the
+final logical<->physical un-permutation — with real inter-process transfers and no GPU.  Op semantics follow engine.hpp (M1 / DIAG / SWAP).
 """
 from __future__ import annotations
 
@@ -35,40 +36,32 @@ def apply_op(s: np.ndarray, op: dict) -> None:
         s[j] = tmp
 
 
-def chunk_index(L: int, lpos, c: int) -> np.ndarray:
-    """Local indices whose bits at lpos[j] equal bit j of c, in ascending order."""
-    k = len(lpos)
-    rest = np.arange(1 << (L - k), dtype=np.int64)
-    for p in sorted(lpos):
-        lo = rest & ((1 << p) - 1)
-        rest = ((rest ^ lo) << 1) | lo
-    for j, p in enumerate(lpos):
-        rest |= ((c >> j) & 1) << p
-    return rest
-
-
-def exchange(s: np.ndarray, L: int, rank: int, step: dict, dist) -> None:
+def exchange(s: np.ndarray, n: int, world: int, rank: int, step: dict, dist) -> None:
+    """One remap with the engine's own slab layout (qsim_dist_slab_map: the peer of every slab
+    and the local index of every slab element, as the pack / unpack kernels compute them); an
+    overlapped remap (pivots) is carried out part by part, as qsim_dist_run does."""
     import torch
-    k, gpos, lpos = step["k"], step["gpos"], step["lpos"]
+    import qsim_amd.dist as qd
+    k = step["k"]
     if k == 0:
         return
-    my_c = sum(((rank >> (gpos[j] - L)) & 1) << j for j in range(k))
-    ops, recv = [], {}
-    for c in range(1 << k):
-        if c == my_c:
-            continue
-        peer = rank
-        for j in range(k):
-            b = gpos[j] - L
-            peer = (peer & ~(1 << b)) | (((c >> j) & 1) << b)
-        send = torch.from_numpy(np.ascontiguousarray(s[chunk_index(L, lpos, c)]).view(np.float64))
-        recv[c] = torch.empty_like(send)
-        ops.append(dist.P2POp(dist.isend, send, peer))
-        ops.append(dist.P2POp(dist.irecv, recv[c], peer))
-    for w in dist.batch_isend_irecv(ops):
-        w.wait()
-    for c, buf in recv.items():
-        s[chunk_index(L, lpos, c)] = buf.numpy().view(np.complex128)
+    parts = range(1 << len(step["pivots"])) if step["pivots"] else [-1]
+    for part in parts:
+        my_c, peer_of, idx = qd.slab_map(n, world, rank, step, part)
+        chunk = idx.size >> k
+        ops, recv = [], {}
+        for c in range(1 << k):
+            if c == my_c:
+                continue
+            sl = idx[c * chunk:(c + 1) * chunk]
+            send = torch.from_numpy(np.ascontiguousarray(s[sl]).view(np.float64))
+            recv[c] = (sl, torch.empty_like(send))
+            ops.append(dist.P2POp(dist.isend, send, peer_of[c]))
+            ops.append(dist.P2POp(dist.irecv, recv[c][1], peer_of[c]))
+        for w in dist.batch_isend_irecv(ops):
+            w.wait()
+        for sl, buf in recv.values():
+            s[sl] = buf.numpy().view(np.complex128)
 
 
 def run_rank(n: int, world: int, rank: int, circuit, dist) -> tuple:
@@ -84,7 +77,7 @@ def run_rank(n: int, world: int, rank: int, circuit, dist) -> tuple:
             for op in st["ops"]:
                 apply_op(s, op)
         else:
-            exchange(s, L, rank, st, dist)
+            exchange(s, n, world, rank, st, dist)
     return s, perm
 
 

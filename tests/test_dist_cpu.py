@@ -1,9 +1,11 @@
 """CPU, multi-process (gloo): the sharded path's planner + exchange logic against the oracle.
 
-world_size 2 and 4 ranks run as separate processes (torch.multiprocessing, gloo over 127.0.0.1);
-each executes its own host plan (qsim_amd.dist.plan, the exact step list qsim_dist_run launches)
-on a numpy shard, performing every qubit remap as real isend/irecv exchanges.  Rank 0 gathers the
-shards, undoes the logical->physical map and compares with the CPUSimulator restatement at 1e-12.
+world_size 2, 4 and 8 ranks run as separate processes (torch.multiprocessing, gloo over
+127.0.0.1); each plans its own rank in its own process (qsim_amd.dist.plan, the exact step list
+qsim_dist_run launches — pivots included, decided independently per process) and executes it on a
+numpy shard, performing every qubit remap (part by part when it has pivots) as real isend/irecv
+exchanges over the engine's own slab maps (qsim_dist_slab_map).  Rank 0 gathers the shards,
+undoes the logical->physical map and compares with the CPUSimulator restatement at 1e-12.
 """
 import math
 import os
@@ -22,7 +24,8 @@ def free_port():
 
 
 def circuits(qsim, n):
-    out = [qsim.createRandomHCCircuit(n, 60, 42), qsim.createRandomCircuit(n, 80, 3)]
+    out = [qsim.createRandomHCCircuit(n, 300 if n == 16 else (100 if n >= 12 else 60), 3 if n == 16 else 42),
+           qsim.createRandomCircuit(n, 80, 3)]
     rng = np.random.default_rng(n)
     c = qsim.Circuit(n)
     for _ in range(90):
@@ -44,10 +47,15 @@ def worker(rank, world, port, n, result_q):
     import dist_exec
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import datetime
+    dist.init_process_group("gloo", rank=rank, world_size=world,
+                            timeout=datetime.timedelta(seconds=120))
     try:
         for ci, c in enumerate(circuits(qsim_amd, n)):
             shard, perm = dist_exec.run_rank(n, world, rank, c, dist)
+            if ci == 0:  # the planner must have overlapped a remap where the shard allows it
+                steps, _ = qsim_amd.dist.plan(c, world, rank)
+                result_q.put(("pivots", rank, [tuple(s["pivots"]) for s in steps if s["kind"] == "exchange"]))
             gathered = [torch.empty(2 * shard.size, dtype=torch.float64) for _ in range(world)] \
                 if rank == 0 else None
             dist.gather(torch.from_numpy(shard.view(np.float64).copy()), gathered, dst=0)
@@ -58,7 +66,7 @@ def worker(rank, world, port, n, result_q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,n", [(2, 7), (4, 8), (2, 10)])
+@pytest.mark.parametrize("world,n", [(2, 7), (4, 8), (2, 10), (2, 12), (4, 13), (8, 14), (8, 16)])
 def test_sharded_plan_matches_oracle_gloo(qsim, oracle, world, n):
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
@@ -67,11 +75,14 @@ def test_sharded_plan_matches_oracle_gloo(qsim, oracle, world, n):
     procs = [ctx.Process(target=worker, args=(r, world, port, n, q)) for r in range(world)]
     for p in procs:
         p.start()
-    got = {}
+    got, pivots = {}, {}
     try:
-        for _ in range(3):
-            ci, full = q.get(timeout=240)
-            got[ci] = full
+        while len(got) < 3 or len(pivots) < world:
+            item = q.get(timeout=240)
+            if item[0] == "pivots":
+                pivots[item[1]] = item[2]
+            else:
+                got[item[0]] = item[1]
     finally:
         for p in procs:
             p.join(timeout=60)
@@ -82,6 +93,10 @@ def test_sharded_plan_matches_oracle_gloo(qsim, oracle, world, n):
     for ci, c in enumerate(circuits(qsim, n)):
         ref = oracle.run_cpu(n, oracle.gates_of(c))
         assert np.max(np.abs(got[ci] - ref)) < 1e-12, ci
+    # every rank process chose the same pivots on its own; shards of >= 8 local qubits overlap
+    assert all(pivots[r] == pivots[0] for r in range(world))
+    if n - (world.bit_length() - 1) >= 11:
+        assert any(pivots[0]), pivots[0]
 
 
 def test_plan_structure(qsim):
@@ -118,6 +133,56 @@ def test_plan_w_hc_30q_one_remap_per_run(qsim, seed):
         steps, perm = qd.plan(c, 8, 0, perm)
         assert sum(s["kind"] == "exchange" for s in steps) <= 1
         assert all(s["k"] == 3 for s in steps if s["kind"] == "exchange")
+
+
+@pytest.mark.parametrize("n,seed", [(16, 3), (18, 8), (22, 7)])
+def test_plan_pivots_rank_independent_fresh(qsim, n, seed):
+    """Pivots are planned from rank-independent data only: each rank planned as if in its own
+    fresh process (the pivot memo cleared before every rank) gets rank 0's pivots and roles, on a
+    circuit with two or more pivoted remaps in a row (the ops step between them is the trailing
+    step of one and the leading step of the other)."""
+    import qsim_amd.dist as qd
+    world = 8
+    # (these circuits made ranks != 0 pick other pivots when the planner read the roles of
+    # rank 0's reference plan instead of its own marks — ADVICE r2, dist.hip mark_overlap)
+    c = qsim.createRandomHCCircuit(n, 300, seed)
+    ref = None
+    for r in range(world):
+        qd.plan_memo_clear()
+        steps, _ = qd.plan(c, world, r)
+        sk = [(s["kind"], tuple(s.get("pivots", ())), s.get("role", 0)) for s in steps]
+        ref = ref or sk
+        assert sk == ref, r
+    pivoted = [i for i, s in enumerate(ref) if s[0] == "exchange" and s[1]]
+    assert len(pivoted) >= 2
+    assert any(ref[i][2] == 3 for i in range(len(ref)) if ref[i][0] == "ops"), \
+        "no ops step both follows and precedes a pivoted remap"
+
+
+def test_slab_map_is_a_partition(qsim):
+    """qsim_dist_slab_map (the pack / unpack index map): for every rank, every remap of a plan and
+    every part, the slabs cover the shard exactly once; the parts of an overlapped remap cover it
+    exactly once together; peers are an involution (my slab c goes to the rank whose slab my_c
+    comes back) and differ from the rank only in the exchanged global bits."""
+    import qsim_amd.dist as qd
+    n, world = 14, 8
+    g, L = 3, 11
+    c = qsim.createRandomHCCircuit(n, 100, 42)
+    for r in range(world):
+        steps, _ = qd.plan(c, world, r)
+        for st in (s for s in steps if s["kind"] == "exchange"):
+            my_c, peer_of, idx = qd.slab_map(n, world, r, st, -1)
+            assert np.array_equal(np.sort(idx), np.arange(1 << L))
+            assert peer_of[my_c] == r
+            gmask = sum(1 << (p - L) for p in st["gpos"])
+            for cc, q in enumerate(peer_of):
+                assert (q & ~gmask) == (r & ~gmask)
+                qc, qpeer, _ = qd.slab_map(n, world, q, st, -1)
+                assert qpeer[my_c] == r and qc == cc
+            if st["pivots"]:
+                allp = np.concatenate([qd.slab_map(n, world, r, st, h)[2]
+                                       for h in range(1 << len(st["pivots"]))])
+                assert np.array_equal(np.sort(allp), np.arange(1 << L))
 
 
 def test_plan_pivots_rank_independent(qsim):
@@ -161,3 +226,32 @@ def test_plan_reorder_is_exact(qsim, oracle):
         for b in range(a + 1, len(gates)):
             if a in pos and b in pos and qs[a] & qs[b]:
                 assert pos[a] < pos[b], (a, b)
+
+
+def test_plan_sizes_output_for_the_given_map(qsim):
+    """plan() from a non-identity start map returns every step (its output was once sized by a
+    plan from the identity map, which can have fewer steps)."""
+    import qsim_amd.dist as qd
+    n, world = 14, 2
+    c = qsim.createRandomHCCircuit(n, 300, 3)
+    perm = list(range(n))
+    for _ in range(3):
+        steps, nxt = qd.plan(c, world, 0, perm)
+        ex = [s for s in steps if s["kind"] == "exchange"]
+        # the framed step list starts and ends with an ops step and alternates around remaps
+        assert steps[0]["kind"] == "ops" and steps[-1]["kind"] == "ops"
+        assert len(steps) == 2 * len(ex) + 1
+        passes = qd_passes(qd, c, world, perm)
+        assert len(passes) == len(steps)
+        perm = nxt
+
+
+def qd_passes(qd, c, world, perm):
+    import ctypes
+    from qsim_amd import _lib
+    n = c.getNumQubits()
+    arr, cnt = c.to_abi()
+    p = (ctypes.c_int32 * n)(*perm)
+    ns = ctypes.c_size_t(0)
+    _lib.check(_lib.hip.qsim_dist_plan_passes(n, world, 0, arr, cnt, p, None, 0, ctypes.byref(ns)))
+    return [0] * ns.value

@@ -153,3 +153,36 @@ def test_virtual_shards_over_rccl(qsim, oracle, gpu_ready, world, n, fused):
     assert abs(d.getTotalProbability() - 1.0) < 1e-10
     g = oracle.gates_of(c)
     np.testing.assert_allclose(got, oracle.run_cpu(n, g + g), atol=1e-12, rtol=0)
+
+
+def test_virtual_30q_8_shards_over_rccl_matches_single_gpu(qsim, gpu_ready):
+    """BASELINE config 5 at its own size on one GPU: 30 qubits in 8 virtual shards of 2 GiB
+    (16 GiB of shards + 32 GiB of send / receive slabs), every slab moved by ncclSend / ncclRecv
+    through a world-1 RCCL communicator, overlapped part-exchanges as planned for 8 ranks; W-HC run
+    twice.  Reference: the single-GPU engine on the same circuit (16 GiB).  Compared: the full
+    logical state vectors (1e-12 per component), getTotalProbability and probBitZero of every
+    qubit (collectives of the sharded object)."""
+    from qsim_amd.dist import DistributedSimulator, plan
+    n, world = 30, 8
+    c = qsim.createRandomHCCircuit(n, 100, 42)
+    steps, _ = plan(c, world, 0)
+    assert any(s["kind"] == "exchange" and s["pivots"] for s in steps)
+    d = DistributedSimulator.virtual(n, world, rccl=True)
+    for _ in range(2):
+        d.run(c)
+    d.synchronize()
+    assert d.overlappedRemaps() >= 1
+    assert abs(d.getTotalProbability() - 1.0) < 1e-10
+    p0 = [d.probBitZero(q) for q in range(n)]
+    got = d.getStateVector()
+    d.close()
+    del d
+    s = qsim.Simulator(n)
+    for _ in range(2):
+        s.run(c)
+    for q in range(n):
+        assert abs(p0[q] - s.state.probBitZero(q)) < 1e-12, q
+    ref = s.getStateVector()
+    del s
+    err = float(np.max(np.abs(got - ref)))
+    assert err < 1e-12, err

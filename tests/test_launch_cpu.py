@@ -40,6 +40,26 @@ def test_dry_run_launch_prints_one_json_line(world):
     assert out["config"]["remaps_per_step"] >= 1  # W-HC at 24q needs at least one remap per run
 
 
+def test_launcher_parent_does_not_load_the_engine():
+    """The self-launching parent of `bench.py --gpus N` never touches the GPU: after its ranks
+    have run, its own /proc/self/maps holds no libqsim_hip / RCCL / hipRTC / HIP runtime."""
+    code = ("import importlib.util, sys\n"
+            f"sys.argv = [{BENCH!r}, '--gpus', '2', '--dry-run', '--steps', '1', '--warmup', '1', "
+            "'--qubits', '20']\n"
+            f"spec = importlib.util.spec_from_file_location('bench', {BENCH!r})\n"
+            "m = importlib.util.module_from_spec(spec); spec.loader.exec_module(m)\n"
+            "try:\n    m.main()\n    rc = 0\nexcept SystemExit as e:\n    rc = e.code\n"
+            "maps = open('/proc/self/maps').read()\n"
+            "bad = [k for k in ('libqsim_hip', 'librccl', 'libhiprtc', 'libamdhip64') if k in maps]\n"
+            "print('PARENT_MAPS', bad, file=sys.stderr)\n"
+            "sys.exit(rc if not bad else 9)\n")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300,
+                       env=_env())
+    assert "PARENT_MAPS []" in r.stderr, r.stderr[-2000:]
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert len([ln for ln in r.stdout.splitlines() if ln.strip()]) == 1
+
+
 def test_failing_rank_stops_launch():
     sys.path.insert(0, os.path.join(ROOT, "cuda-quantum-simulator_amd"))
     from qsim_amd.launch import launch_ranks
