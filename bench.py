@@ -39,7 +39,7 @@ HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=5)
+    p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=2)
     p.add_argument("--qubits", type=int, default=None,
                    help="default 30 (W-HC / ref / 1q), 16 for --workload batch (W-BATCH)")
@@ -106,11 +106,26 @@ def alg_bytes_of_circuit(circuit, n):
     return total
 
 
-def cpu_baseline(circuit, n, budget):
+def cpu_baseline(circuit, n, budget, q=None, args=None):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import numpy_oracle as orc  # test infrastructure: the CPU baseline leg only
     gates = orc.gates_of(circuit)
     done, secs = orc.time_prefix(n, gates, budget)
+    full20 = None
+    if q is not None and args is not None and args.workload == "hc":
+        # BASELINE.md §3 plan: the same W-HC circuit at 20 qubits, whole runs, median of 3
+        c20 = q.createRandomHCCircuit(20, args.depth, args.seed)
+        g20 = orc.gates_of(c20)
+        runs = []
+        for _ in range(3):
+            d20, s20 = orc.time_prefix(20, g20, 120.0)
+            if d20 == len(g20):
+                runs.append(s20)
+        if runs:
+            m = sorted(runs)[len(runs) // 2]
+            full20 = {"value": round(len(g20) / m, 2), "unit": "gates/s", "cores": 1, "kind": "port",
+                      "sample": f"W-HC depth {args.depth} seed {args.seed} at 20 qubits, median of "
+                                f"{len(runs)} whole runs ({', '.join(f'{r:.3f}' for r in runs)} s)"}
     cpu_model = "unknown"
     try:
         with open("/proc/cpuinfo") as f:
@@ -121,7 +136,7 @@ def cpu_baseline(circuit, n, budget):
     except OSError:
         pass
     return {"value": done / secs if secs > 0 else None, "unit": "gates/s", "cores": 1,
-            "kind": "port",
+            "kind": "port", "w_hc_20q": full20,
             "sample": f"prefix-extrapolated: first {done} gates of the same circuit at n={n}, one "
                       f"run, single thread, {secs:.1f} s ({cpu_model}; host has {os.cpu_count()} "
                       f"logical CPUs); value = prefix gates / prefix time"}
@@ -144,18 +159,35 @@ def run_single(args):
     sim.synchronize()
     # Per-launch HIP events cost ~5 us per launch (a 20-qubit pass is ~15 us), so only the last
     # tenth of the timed steps (at least one) carries them; the kernel averages come from those.
+    # Every step is synchronised and timed on its own (the median of >= 10 steps);
+    # at 30 qubits a step is ~25 ms, the per-step synchronisation ~20 us.
     prof_from = args.steps - max(1, args.steps // 10)
+    step_s = []
     t0 = time.perf_counter()
     for i in range(args.steps):
         if i == prof_from:
             sim.state.profile(True)
+        ts = time.perf_counter()
         sim.run(circuit)
-    sim.synchronize()
+        sim.synchronize()
+        step_s.append(time.perf_counter() - ts)
     t1 = time.perf_counter()
     stats = sim.state.profileStats()
     sim.state.profile(False)
     wall = t1 - t0
+    med = sorted(step_s)[len(step_s) // 2] if len(step_s) % 2 else \
+        0.5 * sum(sorted(step_s)[len(step_s) // 2 - 1:len(step_s) // 2 + 1])
     gates = circuit.getGateCount()
+    layout = sim.state.layoutInfo()
+    # what the timed loop never pays: the first index-based readback after a relabeled run
+    # restores the identity layout with a fused SWAP network
+    restore_ms = None
+    if layout["relabeled"]:
+        tr = time.perf_counter()
+        sim.state.restoreLayout()
+        sim.synchronize()
+        restore_ms = round((time.perf_counter() - tr) * 1e3, 3)
+        restore_passes = sim.state.lastRunInfo()[0]
     dom = max(stats, key=lambda s: s["ms"]) if stats else None
     roof = None
     if dom and dom["launches"]:
@@ -178,14 +210,22 @@ def run_single(args):
                 "launches": dom["launches"]}
     eff = alg_bytes_of_circuit(circuit, n) * args.steps / wall / 1e9
     out = {
-        "metric": METRIC, "value": round(gates * args.steps / wall, 2), "unit": "gates/s",
+        "metric": METRIC, "value": round(gates / med, 2), "unit": "gates/s",
         "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
-        "ms_per_step": round(wall / args.steps * 1e3, 3), "higher_is_better": True,
+        "ms_per_step": round(med * 1e3, 3), "higher_is_better": True,
         "scaling": "strong", "vs_baseline": None, "dtype": "c128 (complex<double>)",
         "data": "synthetic",
+        "value_mean": round(gates * args.steps / wall, 2),
+        "ms_per_step_mean": round(wall / args.steps * 1e3, 3),
+        "ms_per_step_min_max": [round(min(step_s) * 1e3, 3), round(max(step_s) * 1e3, 3)],
         "config": {"workload": wl, "qubits": n, "gates": gates, "mode": mode.name,
                    "pass_kernels": "jit" if args.jit else "interpreter",
+                   "jit_mode": args.jit, "tile_qubits": layout["tile_qubits"],
+                   "calibrated": layout["calibrated"], "relabel": layout["relabeled"],
                    "state_bytes": 16 << n, "parallelism": "single GPU"},
+        "value_is": "gates / median step time (every step synchronised); value_mean = gates x steps / wall",
+        "restore_ms": restore_ms,
+        "restore_passes": restore_passes if restore_ms is not None else None,
         "roofline": roof,
         "effective_GBps": round(eff, 1),
         "kernels": stats,
@@ -194,7 +234,7 @@ def run_single(args):
     if args.workload == "hc" and not args.no_1q28:
         out["roofline_1q28"] = roofline_1q28(q)
     if args.cpu_budget > 0:
-        out["cpu_baseline"] = cpu_baseline(circuit, n, args.cpu_budget)
+        out["cpu_baseline"] = cpu_baseline(circuit, n, args.cpu_budget, q, args)
     else:
         out["cpu_baseline"] = None
     print(json.dumps(out))

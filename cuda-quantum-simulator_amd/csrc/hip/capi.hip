@@ -180,6 +180,7 @@ struct qsim_state {
     int n = 0;
     int device = 0;
     double2* d = nullptr;
+    void* base = nullptr;  // the allocation d lies in
     hipStream_t stream = nullptr;
     double* d_partials = nullptr;
     double* d_result = nullptr;
@@ -194,9 +195,13 @@ struct qsim_state {
     std::vector<int> perm;
     bool basis = true;
     uint64_t basis_idx = 0;
+    // tile height chosen for this state by the first-run calibration (-1: the size rule), and
+    // whether its layout was chosen by timing candidates on the device
+    int tile_h = -1;
+    bool calibrated = false;
     ~qsim_state() {
         if (stream) (void)hipStreamSynchronize(stream);
-        if (d) (void)hipFree(d);
+        if (base) (void)hipFree(base);
         if (d_partials) (void)hipFree(d_partials);
         if (d_result) (void)hipFree(d_result);
         if (stream) (void)hipStreamDestroy(stream);
@@ -219,10 +224,12 @@ static void check_state(const qsim_state* s) {
     if (!s) fail(QSIM_ERR_INVALID_ARGUMENT, "null state handle");
 }
 
-static void run_fused(qsim_state* s, const std::vector<Op>& ops) {
+// jit = false: the pass interpreter only (a one-off network — the layout restore — would wait
+// longer for its compile than its passes take).
+static void run_fused(qsim_state* s, const std::vector<Op>& ops, bool jit = true) {
     PlanCache::Entry& pe = s->plans.get(ops, s->n, s->stream);
     const Plan& plan = pe.plan;
-    const JitModule* jm = jit_for(pe.jit, plan, s->n);
+    const JitModule* jm = jit ? jit_for(pe.jit, plan, s->n) : nullptr;
     s->ops.upload(plan.ops.data(), plan.ops.size() * sizeof(TileOp), s->stream);
     s->stages.upload(plan.stages.data(), plan.stages.size() * sizeof(Stage), s->stream);
     launch_fused(s->d, s->n, 1, plan, (const TileOp*)s->ops.ptr, (const Stage*)s->stages.ptr,
@@ -258,29 +265,39 @@ static void canonicalize(qsim_state* s) {
         inv[q] = q;
     }
     s->perm.clear();
-    if (!swaps.empty()) run_fused(s, swaps);
+    if (!swaps.empty()) run_fused(s, swaps, false);
 }
 // Before an entry that reads amplitudes by index (touch: and writes them).
 static void prep(qsim_state* s, bool touch) {
     canonicalize(s);
     if (touch) s->basis = false;
 }
-// Time the layout choice and its alternatives with their own circuit-specialised kernels on this
-// device (each candidate's whole plan, the faster of two runs, the basis state restored after
-// each) and keep the fastest: the cost model ranks layouts from probes of other boxes, and real
-// pass times differ by a few per cent between devices.  Their plans stay cached (compiled).
-static bool calibrate_layout(qsim_state* s, LayoutChoice& lc) {
-    const size_t ncand = 1 + lc.alts.size();
+// One timed candidate of the first-run layout choice: a tile height and the labels chosen under
+// it, with the circuit lowered under those labels and its plan at that height.
+struct LayoutCandidate {
+    int h = kTileHDefault;
+    std::vector<int> perm;  // empty: identity
+    std::vector<Op> ops;
+    Plan plan;
+};
+// Time every candidate with its own circuit-specialised kernels on this device (each candidate's
+// whole plan under its own tile height, the faster of two runs, the basis state restored after
+// each) and return the fastest: the cost model ranks layouts from probes of other boxes, real
+// pass times differ by a few per cent between devices, and whether 13-qubit tiles (fewer passes,
+// slower streaming) beat 12-qubit ones depends on the circuit.  The plans stay cached
+// (compiled).
+static size_t calibrate_candidates(qsim_state* s, std::vector<LayoutCandidate>& cands) {
     hipEvent_t e0 = nullptr, e1 = nullptr;
     QSIM_HIPCHK(hipEventCreate(&e0));
     QSIM_HIPCHK(hipEventCreate(&e1));
     size_t best = 0;
     float best_ms = 3.0e38f;
     try {
-        for (size_t k = 0; k < ncand; ++k) {
-            const std::vector<Op>& ops = k ? lc.alts[k - 1].ops : lc.ops;
-            s->plans.put(ops, s->n, k ? lc.alts[k - 1].plan : lc.plan, s->stream);
-            PlanCache::Entry& pe = s->plans.get(ops, s->n, s->stream);
+        for (size_t k = 0; k < cands.size(); ++k) {
+            LayoutCandidate& c = cands[k];
+            const TileHeightScope scope(c.h, tile_rb_for(s->n, c.h));
+            s->plans.put(c.ops, s->n, c.plan, s->stream);
+            PlanCache::Entry& pe = s->plans.get(c.ops, s->n, s->stream);
             const JitModule* jm = jit_for(pe.jit, pe.plan, s->n);
             s->ops.upload(pe.plan.ops.data(), pe.plan.ops.size() * sizeof(TileOp), s->stream);
             s->stages.upload(pe.plan.stages.data(), pe.plan.stages.size() * sizeof(Stage), s->stream);
@@ -297,7 +314,9 @@ static bool calibrate_layout(qsim_state* s, LayoutChoice& lc) {
             }
             launch_init_basis(s->d, s->n, 1, s->basis_idx, s->stream);  // the state as it was
             static const bool dbg = std::getenv("QSIM_RELABEL_DEBUG") != nullptr;
-            if (dbg) std::fprintf(stderr, "[calibrate] candidate %zu: %.3f ms per run\n", k, ms);
+            if (dbg)
+                std::fprintf(stderr, "[calibrate] candidate %zu (h=%d, %zu passes): %.3f ms per run\n", k, c.h,
+                             pe.plan.passes.size(), ms);
             if (ms < best_ms) {
                 best = k;
                 best_ms = ms;
@@ -319,13 +338,95 @@ static bool calibrate_layout(qsim_state* s, LayoutChoice& lc) {
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
     QSIM_HIPCHK(hipStreamSynchronize(s->stream));
-    if (best > 0) {
-        LayoutChoice::Alt& a = lc.alts[best - 1];
-        lc.perm = std::move(a.perm);
-        lc.ops = std::move(a.ops);
-        lc.plan = std::move(a.plan);
+    return best;
+}
+
+// The labels (s->perm) and, with cross-height calibration, the tile height (s->tile_h) for the
+// first fused run of a basis state.  Candidates: the layout model's choice and its next
+// alternatives at the state's default height; with cross-height calibration also at the other
+// height (13-qubit tiles with the 13-qubit cost factor 1.25, which steers the labels toward
+// mixed plans, and with factor 1) — every candidate timed on the device, the fastest kept.
+static void choose_first_layout(qsim_state* s, const qsim_gate* gates, size_t count) {
+    const int n = s->n;
+    const size_t bytes = count * sizeof(qsim_gate);
+    auto lower_under = [&](const std::vector<int>& pi) {
+        std::vector<Op> ops;
+        ops.reserve(count);
+        for (size_t i = 0; i < count; ++i) {
+            qsim_gate m = gates[i];
+            for (int j = 0; j < m.nqubits && j < 3; ++j) m.qubits[j] = pi[m.qubits[j]];
+            ops.push_back(lower_gate(m, n));
+            ops.back().src = (int)i;
+        }
+        return ops;
+    };
+    static const size_t alts = [] {  // QSIM_RELABEL_CALIBRATE_CANDIDATES (default 3) per height
+        const char* e = std::getenv("QSIM_RELABEL_CALIBRATE_CANDIDATES");
+        return (size_t)std::max(1, e ? std::atoi(e) : 3) - 1;
+    }();
+    const bool heights = calibrate_heights(n) && s->tile_h < 0;
+    const int th = s->tile_h >= 0 ? s->tile_h : tile_height_for(n);
+    auto memo_put = [&](const std::vector<int>& perm) {
+        const TileHeightScope scope(th);  // (a single-height decision is keyed by its height)
+        layout_memo_put(n, 0, gates, bytes, perm, heights ? s->tile_h : -1);
+    };
+    {
+        std::vector<int> memo;
+        int mh = -1;
+        const TileHeightScope scope(th);
+        if (layout_memo_get(n, 0, gates, bytes, memo, heights ? &mh : nullptr)) {
+            s->perm = memo;  // decided before for this circuit (its plan: the plan cache)
+            if (heights) s->tile_h = mh;
+            return;
+        }
     }
-    return true;
+    struct Gen {
+        int h;
+        double t13;
+        size_t alts;
+    };
+    std::vector<Gen> gens{{th, layout_t13(), relabel_calibrate(n) ? alts : 0}};
+    if (heights) {
+        if (th == 7) gens.push_back({6, 1.0, alts});
+        else gens.insert(gens.end(), {{7, 1.25, alts}, {7, 1.0, 0}});
+    }
+    std::vector<LayoutCandidate> cands;
+    auto add = [&](int h, std::vector<int> perm, std::vector<Op> ops, Plan plan) {
+        for (const LayoutCandidate& c : cands)
+            if (c.h == h && c.perm == perm) return;  // the same candidate from two generators
+        cands.push_back(LayoutCandidate{h, std::move(perm), std::move(ops), std::move(plan)});
+    };
+    for (const Gen& g : gens) {
+        const TileHeightScope scope(g.h, tile_rb_for(n, g.h));
+        const LayoutT13Scope t13(g.t13);
+        LayoutChoice lc = choose_layout(n, lower_under, relabel_tries(), g.alts);
+        if (lc.perm.empty()) {  // the identity is this height's choice
+            if (!heights) {  // (nothing to time: keep the identity)
+                memo_put({});
+                return;
+            }
+            std::vector<int> id(n);
+            for (int q = 0; q < n; ++q) id[q] = q;
+            std::vector<Op> ops = lower_under(id);
+            Plan plan = plan_fused(ops, n, g.h);
+            add(g.h, {}, std::move(ops), std::move(plan));
+        } else {
+            add(g.h, std::move(lc.perm), std::move(lc.ops), std::move(lc.plan));
+        }
+        for (LayoutChoice::Alt& a : lc.alts) add(g.h, std::move(a.perm), std::move(a.ops), std::move(a.plan));
+    }
+    size_t best = 0;
+    if (cands.size() > 1) {
+        best = calibrate_candidates(s, cands);  // (their plans stay cached, compiled)
+    } else {
+        const TileHeightScope scope(cands[0].h, tile_rb_for(n, cands[0].h));
+        if (!cands[0].perm.empty()) s->plans.put(cands[0].ops, n, cands[0].plan, s->stream);
+    }
+    LayoutCandidate& w = cands[best];
+    if (heights) s->tile_h = w.h;
+    s->perm = std::move(w.perm);
+    memo_put(s->perm);
+    s->calibrated = cands.size() > 1;
 }
 
 static qsim_gate map_gate(const qsim_state* s, const qsim_gate& g) {
@@ -349,8 +450,29 @@ int qsim_state_last_run(qsim_state* s, int* passes, int* jit_passes) {
 }
 int qsim_abi_version(void) { return QSIM_ABI_VERSION; }
 
+int qsim_state_layout_info(qsim_state* s, int* tile_h, int* calibrated, int* relabeled) {
+    return guarded([&] {
+        check_state(s);
+        if (tile_h) *tile_h = s->tile_h >= 0 ? s->tile_h : tile_height_for(s->n);
+        if (calibrated) *calibrated = s->calibrated ? 1 : 0;
+        if (relabeled) *relabeled = s->perm.empty() ? 0 : 1;
+    });
+}
+
+int qsim_state_restore_layout(qsim_state* s) {
+    return guarded([&] {
+        check_state(s);
+        DeviceGuard dg(s->device);
+        canonicalize(s);
+    });
+}
+
 int qsim_set_tile_height(int h) {
     return guarded([&] { tile_height_configure(h); });
+}
+
+int qsim_set_tile_rb7(int rb) {
+    return guarded([&] { tile_rb7_configure(rb); });
 }
 
 int qsim_set_calibrate(int mode, int min_qubits) {
@@ -404,7 +526,22 @@ int qsim_state_create_on(int device, int n_qubits, qsim_state** out) {
         s->device = device;
         QSIM_HIPCHK(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
         s->timer.stream = s->stream;
-        QSIM_HIPCHK(hipMalloc((void**)&s->d, (sizeof(double2)) << n_qubits));
+        // QSIM_STATE_OFFSET_KB (experiments): the amplitudes start that far into their allocation
+        static const size_t off = [] {
+            const char* e = std::getenv("QSIM_STATE_OFFSET_KB");
+            return e ? (size_t)std::max(0ll, std::atoll(e)) * 1024 : (size_t)0;
+        }();
+        static const int contiguous = [] {  // QSIM_STATE_CONTIGUOUS (experiments)
+            const char* e = std::getenv("QSIM_STATE_CONTIGUOUS");
+            return e ? std::atoi(e) : 0;
+        }();
+        const size_t sbytes = ((sizeof(double2)) << n_qubits) + off;
+        if (!contiguous || hipExtMallocWithFlags(&s->base, sbytes, hipDeviceMallocContiguous) != hipSuccess) {
+            (void)hipGetLastError();
+            s->base = nullptr;
+            QSIM_HIPCHK(hipMalloc(&s->base, sbytes));
+        }
+        s->d = reinterpret_cast<double2*>(reinterpret_cast<char*>(s->base) + off);
         QSIM_HIPCHK(hipMalloc((void**)&s->d_partials, 4096 * sizeof(double)));
         QSIM_HIPCHK(hipMalloc((void**)&s->d_result, sizeof(double)));
         launch_init_basis(s->d, s->n, 1, 0, s->stream);
@@ -459,6 +596,8 @@ int qsim_state_init_zero(qsim_state* s) {
         s->perm.clear();
         s->basis = true;
         s->basis_idx = 0;
+        s->tile_h = -1;  // (the next first run chooses again: memo)
+        s->calibrated = false;
     });
 }
 
@@ -472,6 +611,8 @@ int qsim_state_init_basis(qsim_state* s, uint64_t idx) {
         s->perm.clear();
         s->basis = true;
         s->basis_idx = idx;
+        s->tile_h = -1;
+        s->calibrated = false;
     });
 }
 
@@ -509,45 +650,19 @@ int qsim_run(qsim_state* s, const qsim_gate* gates, size_t count, int flags) {
             }
             return ops;
         };
-        const int th = tile_height_for(s->n);
-        const TileHeightScope tile_h(th, tile_rb_for(s->n, th));  // plans of this run (and its layout choice)
+        // First run on a basis state: choose the qubit labels (and, with cross-height calibration,
+        // the tile height) for fewer passes and faster pass layouts (relabel.hip: choose_layout).
         if ((flags & QSIM_RUN_FUSED) && s->basis && s->perm.empty() && count > 0 && relabel_enabled(s->n)) {
-            // First run on a basis state: choose the qubit labels for fewer passes and faster
-            // pass layouts (relabel.hip: choose_layout).
-            auto lower_under = [&](const std::vector<int>& pi) {
-                std::vector<Op> ops;
-                ops.reserve(count);
-                for (size_t i = 0; i < count; ++i) {
-                    qsim_gate m = gates[i];
-                    for (int j = 0; j < m.nqubits && j < 3; ++j) m.qubits[j] = pi[m.qubits[j]];
-                    ops.push_back(lower_gate(m, s->n));
-                    ops.back().src = (int)i;
-                }
-                return ops;
-            };
-            std::vector<int> memo;
-            if (layout_memo_get(s->n, 0, gates, count * sizeof(qsim_gate), memo)) {
-                s->perm = memo;  // decided before for this circuit (its plan: the plan cache)
-            } else {
-                static const size_t alts = [] {  // QSIM_RELABEL_CALIBRATE_CANDIDATES (default 3)
-                    const char* e = std::getenv("QSIM_RELABEL_CALIBRATE_CANDIDATES");
-                    return (size_t)std::max(1, e ? std::atoi(e) : 3) - 1;
-                }();
-                LayoutChoice lc = choose_layout(s->n, lower_under, relabel_tries(), relabel_calibrate(s->n) ? alts : 0);
-                const bool cached = !lc.alts.empty() && calibrate_layout(s, lc);  // (plans cached)
-                layout_memo_put(s->n, 0, gates, count * sizeof(qsim_gate), lc.perm);
-                s->perm = lc.perm;
-                if (!lc.perm.empty() && !cached) s->plans.put(std::move(lc.ops), s->n, std::move(lc.plan), s->stream);
-            }
-            if (!s->perm.empty()) {
-                if (s->basis_idx) {  // relabel the basis state itself
-                    uint64_t k = 0;
-                    for (int q = 0; q < s->n; ++q)
-                        if ((s->basis_idx >> q) & 1ull) k |= 1ull << s->perm[q];
-                    launch_init_basis(s->d, s->n, 1, k, s->stream);
-                }
+            choose_first_layout(s, gates, count);
+            if (!s->perm.empty() && s->basis_idx) {  // relabel the basis state itself
+                uint64_t k = 0;
+                for (int q = 0; q < s->n; ++q)
+                    if ((s->basis_idx >> q) & 1ull) k |= 1ull << s->perm[q];
+                launch_init_basis(s->d, s->n, 1, k, s->stream);
             }
         }
+        const int th = s->tile_h >= 0 ? s->tile_h : tile_height_for(s->n);
+        const TileHeightScope tile_h(th, tile_rb_for(s->n, th));  // plans of this run
         const std::vector<Op> ops = lower_all();
         s->basis = false;
         if (flags & QSIM_RUN_FUSED) {

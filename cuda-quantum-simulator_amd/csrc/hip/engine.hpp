@@ -172,8 +172,11 @@ constexpr int kTileR0 = 6;    // contiguous run bits of a staged tile (QSIM_TILE
 Plan plan_fused(const std::vector<Op>& ops, int n, int hmax = -1, uint64_t avoid = 0);
 int tile_height_default();             // the h that hmax < 0 means (scope, setting, env, 6)
 int tile_height_for(int n);            // a single-GPU state's height (the setting, or by size)
+bool tile_height_is_set();             // qsim_set_tile_height or QSIM_TILE_HMAX in force
 void tile_height_configure(int h);     // qsim_set_tile_height: h < 0 restores the env default
 int tile_rb_default(int heff);         // register bits per stage of a staged pass of height heff
+int tile_rb7();                        // register bits per stage of 13-qubit tiles (4, or 3)
+void tile_rb7_configure(int rb);       // qsim_set_tile_rb7: 3 or 4; else back to QSIM_TILE_RB7
 int tile_rb_for(int n, int h);         // a single-GPU state's stage width (-1: stage_rb(h))
 // Plans made by this thread while the scope lives default to height h and, for 12-qubit tiles,
 // rb register bits per stage (qsim_run of a state).
@@ -221,8 +224,21 @@ bool relabel_calibrate(int n);
 void calibrate_configure(int mode, int min_qubits);  // negative: unchanged
 int relabel_tries();  // QSIM_RELABEL_TRIES (default 7): random labelings planned per choice
 // Process-wide memo of layout choices per circuit (kind: 0 state, 1 batched with its run flags).
-bool layout_memo_get(int n, int kind, const void* gates, size_t bytes, std::vector<int>& perm);
-void layout_memo_put(int n, int kind, const void* gates, size_t bytes, const std::vector<int>& perm);
+// h != null / h >= 0: a decision that also chose the tile height (cross-height calibration).
+bool layout_memo_get(int n, int kind, const void* gates, size_t bytes, std::vector<int>& perm, int* h = nullptr);
+void layout_memo_put(int n, int kind, const void* gates, size_t bytes, const std::vector<int>& perm, int h = -1);
+bool calibrate_heights(int n);  // QSIM_CALIBRATE_HEIGHTS (capi.hip: choose_first_layout)
+// Factor on the predicted cost of a 13-qubit tile (QSIM_LAYOUT_T13, default 1); a scope sets it
+// for the calling thread (and choose_layout hands it to its worker threads).
+double layout_t13();
+struct LayoutT13Scope {
+    explicit LayoutT13Scope(double f);
+    ~LayoutT13Scope();
+    LayoutT13Scope(const LayoutT13Scope&) = delete;
+    LayoutT13Scope& operator=(const LayoutT13Scope&) = delete;
+  private:
+    double prev_;
+};
 // Circuit-specialised pass kernels (jit.hip): hipRTC code object of one plan on one device.
 struct JitJob;
 struct JitModule {
@@ -257,7 +273,7 @@ struct PlanCache {
         JitState jit;
         uint64_t used = 0;
     };
-    static constexpr size_t kEntries = 4;
+    static constexpr size_t kEntries = 8;  // (first-run calibration keeps its candidates)
     std::vector<std::unique_ptr<Entry>> entries;
     uint64_t clock = 0;
     // stream: where the owner runs this cache's plans (drained before a plan is evicted)

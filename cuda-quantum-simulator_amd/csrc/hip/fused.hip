@@ -619,6 +619,7 @@ int tile_height_default() {
     const int e = env_tile_h();
     return e >= 0 ? e : kTileHDefault;
 }
+bool tile_height_is_set() { return g_tile_h.load() >= 0 || env_tile_h() >= 0; }
 // Single-GPU states without an explicit height: 13-qubit tiles from 26 to 28 qubits, where their
 // fewer passes outrun the slower streaming (W-HC 26q +23 %, 27q +15 %, 28q +5 %; 29q -3 %, 30q
 // -2 %: profiles/r02/h7s/).  QSIM_TILE_AUTO=0 keeps 12-qubit tiles everywhere.
@@ -639,7 +640,20 @@ int tile_rb_for(int n, int h) {
     if (env >= 2 && env <= 4) return env;
     return n >= 12 && n <= 20 ? 3 : -1;
 }
-int tile_rb_default(int heff) { return heff == 6 && t_tile_rb >= 2 ? t_tile_rb : stage_rb(heff); }
+// 13-qubit tiles: QSIM_TILE_RB7 = 3 gives 8 amplitudes per thread (1024-thread workgroups, 16
+// waves per CU, half the registers of the default 4) — for the tile-height calibration and tests.
+static std::atomic<int> g_tile_rb7{-1};
+int tile_rb7() {
+    const int v = g_tile_rb7.load();
+    if (v >= 0) return v;
+    static const int env = env_int("QSIM_TILE_RB7", 4);
+    return env == 3 ? 3 : 4;
+}
+void tile_rb7_configure(int rb) { g_tile_rb7.store(rb == 3 || rb == 4 ? rb : -1); }
+int tile_rb_default(int heff) {
+    if (heff == 7) return tile_rb7();
+    return heff == 6 && t_tile_rb >= 2 ? t_tile_rb : stage_rb(heff);
+}
 TileHeightScope::TileHeightScope(int h, int rb) : prev_(t_tile_h), prev_rb_(t_tile_rb) {
     t_tile_h = h;
     t_tile_rb = rb;
@@ -1305,9 +1319,14 @@ void launch_fused(double2* st, int n, uint64_t batch, const Plan& plan, const Ti
         if (framed) {  // batched noisy run: non-Clifford ops under the trajectory's Pauli frame
             // the framed kernels exist at the default stage width only (their stage descriptors
             // must have been built for it)
-            if (p.rb != stage_rb(p.h)) fail(QSIM_ERR_RUNTIME, "framed pass with a narrowed stage width");
             a.frames = frames;
             a.nbatch = (int)batch;
+            if (p.rb != stage_rb(p.h)) {
+                if (p.h != 7 || p.rb != 3) fail(QSIM_ERR_RUNTIME, "framed pass with an unsupported stage width");
+                hipExtLaunchKernelGGL((k_fused_staged<7, true, true, 3>), dim3((unsigned)blocks), dim3(1024), 0, s, ev0, ev1, 0, a);
+                QSIM_HIPCHK(hipGetLastError());
+                continue;
+            }
             switch (p.h) {
                 case 4: hipExtLaunchKernelGGL((k_fused_staged<4, true, true>), dim3((unsigned)blocks), dim3(256), 0, s, ev0, ev1, 0, a); break;
                 case 5: hipExtLaunchKernelGGL((k_fused_staged<5, true, true>), dim3((unsigned)blocks), dim3(256), 0, s, ev0, ev1, 0, a); break;
@@ -1332,6 +1351,12 @@ void launch_fused(double2* st, int n, uint64_t batch, const Plan& plan, const Ti
             continue;
         }
         if (p.h >= 4 && p.rb != stage_rb(p.h)) {  // narrower stages (small states): 512 / 1024 threads
+            if (p.h == 7 && p.rb == 3) {  // 13-qubit tiles, 8 amplitudes per thread
+                if (nt) hipExtLaunchKernelGGL((k_fused_staged<7, true, false, 3>), dim3((unsigned)blocks), dim3(1024), 0, s, ev0, ev1, 0, a);
+                else hipExtLaunchKernelGGL((k_fused_staged<7, false, false, 3>), dim3((unsigned)blocks), dim3(1024), 0, s, ev0, ev1, 0, a);
+                QSIM_HIPCHK(hipGetLastError());
+                continue;
+            }
             if (p.h != 6 || p.rb < 2 || p.rb > 3) fail(QSIM_ERR_RUNTIME, "unsupported stage width");
             if (p.rb == 3) {
                 if (nt) hipExtLaunchKernelGGL((k_fused_staged<6, true, false, 3>), dim3((unsigned)blocks), dim3(512), 0, s, ev0, ev1, 0, a);

@@ -60,6 +60,7 @@ struct MemoEntry {
     int n, kind;
     std::vector<unsigned char> key;
     std::vector<int> perm;
+    int h;  // the tile height decided with the labels (cross-height calibration), or -1
     uint64_t used;
 };
 std::mutex g_memo_mu;
@@ -68,25 +69,38 @@ uint64_t g_memo_clock = 0;
 constexpr size_t kMemo = 16;
 }  // namespace
 
-bool layout_memo_get(int n, int kind, const void* gates, size_t bytes, std::vector<int>& perm) {
+bool layout_memo_get(int n, int kind, const void* gates, size_t bytes, std::vector<int>& perm, int* h) {
     std::lock_guard<std::mutex> l(g_memo_mu);
-    kind = kind * 16 + tile_height_default();  // a choice made for one tile height only
+    // a choice made for one tile height only, unless the height was chosen with it (h != null)
+    kind = kind * 16 + (h ? 15 : tile_height_default());
     for (MemoEntry& e : g_memo)
         if (e.n == n && e.kind == kind && e.key.size() == bytes && std::memcmp(e.key.data(), gates, bytes) == 0) {
             e.used = ++g_memo_clock;
             perm = e.perm;
+            if (h) *h = e.h;
             return true;
         }
     return false;
 }
-void layout_memo_put(int n, int kind, const void* gates, size_t bytes, const std::vector<int>& perm) {
+void layout_memo_put(int n, int kind, const void* gates, size_t bytes, const std::vector<int>& perm, int h) {
     std::lock_guard<std::mutex> l(g_memo_mu);
     if (g_memo.size() >= kMemo)
         g_memo.erase(std::min_element(g_memo.begin(), g_memo.end(),
                                       [](const MemoEntry& a, const MemoEntry& b) { return a.used < b.used; }));
-    kind = kind * 16 + tile_height_default();
+    kind = kind * 16 + (h >= 0 ? 15 : tile_height_default());
     const unsigned char* p = static_cast<const unsigned char*>(gates);
-    g_memo.push_back(MemoEntry{n, kind, std::vector<unsigned char>(p, p + bytes), perm, ++g_memo_clock});
+    g_memo.push_back(MemoEntry{n, kind, std::vector<unsigned char>(p, p + bytes), perm, h, ++g_memo_clock});
+}
+
+// Cross-height calibration (QSIM_CALIBRATE_HEIGHTS, default 1; needs layout calibration, i.e.
+// inline compilation): the first run of a basis state also times 13-qubit-tile candidates
+// against 12-qubit ones (or the reverse) unless a tile height was set explicitly.
+bool calibrate_heights(int n) {
+    static const int v = [] {
+        const char* e = std::getenv("QSIM_CALIBRATE_HEIGHTS");
+        return e ? std::atoi(e) : 1;
+    }();
+    return v != 0 && relabel_calibrate(n) && !tile_height_is_set();
 }
 
 static std::atomic<int> g_calib{-1}, g_calib_min{-1};
@@ -133,13 +147,20 @@ double layout_cost_us(uint64_t tile) {
     // QSIM_LAYOUT_T13 scales its predicted cost, steering the label search toward plans whose
     // passes fit 12-qubit tiles (mixed heights): 1.25 gave W-HC 30q seed 42 at h = 7 4 224 gates/s
     // but 28q 16.2 k instead of 18.3 k (profiles/r02/mix2/), so the default stays 1.
-    static const double t13 = [] {
+    if (__builtin_popcountll(tile) >= 13) c *= layout_t13();
+    return c;
+}
+static thread_local double t_t13 = -1.0;  // LayoutT13Scope of the calling thread
+double layout_t13() {
+    if (t_t13 >= 0.0) return t_t13;
+    static const double env = [] {
         const char* e = std::getenv("QSIM_LAYOUT_T13");
         return e ? std::atof(e) : 1.0;
     }();
-    if (__builtin_popcountll(tile) >= 13) c *= t13;
-    return c;
+    return env;
 }
+LayoutT13Scope::LayoutT13Scope(double f) : prev_(t_t13) { t_t13 = f; }
+LayoutT13Scope::~LayoutT13Scope() { t_t13 = prev_; }
 
 std::vector<uint64_t> plan_tiles(const Plan& plan) {
     std::vector<uint64_t> t;
@@ -220,6 +241,7 @@ std::vector<int> choose_relabel(const std::vector<uint64_t>& tiles, int n, doubl
 LayoutChoice choose_layout(int n, const std::function<std::vector<Op>(const std::vector<int>&)>& lower,
                            int tries, size_t want_alts) {
     const int h = tile_height_default();  // the calling thread's height, for the worker threads too
+    const double t13 = layout_t13();      // and its 13-qubit tile cost factor
     struct Cand {
         std::vector<int> pi;
         size_t passes = 0;
@@ -248,7 +270,11 @@ LayoutChoice choose_layout(int n, const std::function<std::vector<Op>(const std:
     };
     {
         std::vector<std::thread> th;
-        for (size_t k = 0; k < cand.size(); ++k) th.emplace_back([&, k] { plan_cand(cand[k]); });
+        for (size_t k = 0; k < cand.size(); ++k)
+            th.emplace_back([&, k] {
+                const LayoutT13Scope sc(t13);
+                plan_cand(cand[k]);
+            });
         for (auto& t : th) t.join();
     }
     LayoutChoice out;
@@ -267,6 +293,7 @@ LayoutChoice choose_layout(int n, const std::function<std::vector<Op>(const std:
         std::vector<std::thread> th;
         for (size_t i = 0; i < pool.size(); ++i)
             th.emplace_back([&, i] {
+                const LayoutT13Scope sc(t13);
                 const Cand& c = cand[pool[i]];
                 double b = 0.0, a = 0.0;
                 std::vector<int> sigma;

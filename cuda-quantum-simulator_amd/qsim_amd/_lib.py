@@ -98,8 +98,11 @@ _sig(hip, "qsim_set_jit", [c_int, c_int])
 _sig(hip, "qsim_jit_shutdown", [])
 _sig(hip, "qsim_set_relabel", [c_int, c_int])
 _sig(hip, "qsim_state_perm", [_P, POINTER(c_int32)])
+_sig(hip, "qsim_state_layout_info", [_P, POINTER(c_int), POINTER(c_int), POINTER(c_int)])
+_sig(hip, "qsim_state_restore_layout", [_P])
 _sig(hip, "qsim_set_calibrate", [c_int, c_int])
 _sig(hip, "qsim_set_tile_height", [c_int])
+_sig(hip, "qsim_set_tile_rb7", [c_int])
 _sig(hip, "qsim_plan_relabel", [c_int, _P, c_size_t, POINTER(c_int32), POINTER(c_double), POINTER(c_double)])
 # Stop the background pass compiler before interpreter / library teardown (a hipRTC compile that
 # is still running while the compiler's statics are destroyed aborts the process).

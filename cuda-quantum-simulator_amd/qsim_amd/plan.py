@@ -67,6 +67,12 @@ def set_tile_height(h: int = -1) -> None:
     _lib.check(_lib.hip.qsim_set_tile_height(h))
 
 
+def set_tile_rb7(rb: int = -1) -> None:
+    """Register bits per stage of 13-qubit tiles (4: 512-thread workgroups, default; 3: 1024
+    threads with 8 amplitudes each); -1 restores QSIM_TILE_RB7."""
+    _lib.check(_lib.hip.qsim_set_tile_rb7(rb))
+
+
 def plan_relabel(circuit: Circuit):
     """(perm, predicted_us_before, predicted_us_after): the logical -> physical qubit map the
     engine would choose for this circuit's fused plan (identity when none pays), host only."""

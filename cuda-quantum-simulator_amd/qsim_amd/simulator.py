@@ -230,6 +230,17 @@ class StateVector:
         _lib.check(_lib.hip.qsim_state_perm(self._h, p))
         return list(p)
 
+    def layoutInfo(self) -> dict:
+        """The first-run layout decision: tile height of the fused runs, whether it was chosen by
+        timing candidates on the device, whether the qubits are relabeled now."""
+        h, c, r = _c.c_int(0), _c.c_int(0), _c.c_int(0)
+        _lib.check(_lib.hip.qsim_state_layout_info(self._h, _c.byref(h), _c.byref(c), _c.byref(r)))
+        return {"tile_qubits": 6 + h.value, "calibrated": bool(c.value), "relabeled": bool(r.value)}
+
+    def restoreLayout(self) -> None:
+        """Undo a relabeling now (the SWAP network every index-based reader runs first)."""
+        _lib.check(_lib.hip.qsim_state_restore_layout(self._h))
+
     # -- profiling
     def profile(self, enable: bool = True) -> None:
         _lib.check(_lib.hip.qsim_state_profile(self._h, 1 if enable else 0))

@@ -157,6 +157,13 @@ int qsim_jit_shutdown(void);
  * are never relabeled; negative arguments leave a setting unchanged. */
 int qsim_set_relabel(int mode, int min_qubits);
 int qsim_state_perm(qsim_state* s, int32_t* perm);  /* current logical -> physical map, n entries */
+/* First-run layout decision of a state (no reference counterpart): the tile height its fused
+ * runs plan at, whether the layout was chosen by timing candidates on the device (layout and
+ * cross-height calibration), whether the qubits are currently relabeled. */
+int qsim_state_layout_info(qsim_state* s, int* tile_h, int* calibrated, int* relabeled);
+/* Bring a relabeled state back to the identity qubit layout now (the fused SWAP network every
+ * index-based reader runs first); a no-op when it is not relabeled. */
+int qsim_state_restore_layout(qsim_state* s);
 /* Layout calibration (with QSIM_JIT = 2, from min_qubits; defaults QSIM_RELABEL_CALIBRATE = 1,
  * QSIM_RELABEL_CALIBRATE_MIN_QUBITS = 28): the first run of a basis state times the layout
  * model's choice and two alternatives with their compiled pass kernels (the basis state is
@@ -168,6 +175,9 @@ int qsim_set_calibrate(int mode, int min_qubits);
  * kernels) needs fewer passes on some circuits but streams slower.  h < 0 restores
  * the default (QSIM_TILE_HMAX); plans already cached for a circuit keep their height. */
 int qsim_set_tile_height(int h);
+/* Register bits per stage of 13-qubit tiles: 4 (16 amplitudes per thread, 512-thread workgroups,
+ * the default) or 3 (8 per thread, 1024 threads); anything else restores QSIM_TILE_RB7. */
+int qsim_set_tile_rb7(int rb);
 /* Host-only: the permutation the engine would choose for this circuit (identity when none pays)
  * and the predicted pass-layout cost (microseconds, summed over the plan's passes) before/after. */
 int qsim_plan_relabel(int n_qubits, const qsim_gate* gates, size_t count, int32_t* perm,

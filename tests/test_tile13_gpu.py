@@ -24,10 +24,22 @@ def tile7(qsim):
     set_jit(1, -1)
 
 
+@pytest.mark.parametrize("rb7", [4, 3])
 @pytest.mark.parametrize("n", [20, 22])
 @pytest.mark.parametrize("jit", [2, 0])
-def test_tile13_matches_oracle(qsim, oracle, gpu_ready, tile7, n, jit):
+def test_tile13_matches_oracle(qsim, oracle, gpu_ready, tile7, n, jit, rb7):
+    """rb7 = 3: 13-qubit tiles with 8 amplitudes per thread (1024-thread workgroups) — the
+    interpreter's k_fused_staged<7, ., ., 3> and generated kernels at that stage width."""
+    from qsim_amd.plan import set_tile_rb7
     tile7(jit, -1)
+    set_tile_rb7(rb7)
+    try:
+        _run_tile13(qsim, oracle, n, jit)
+    finally:
+        set_tile_rb7(-1)
+
+
+def _run_tile13(qsim, oracle, n, jit):
     work = [(f"W-HC seed {s}", qsim.createRandomHCCircuit(n, 100, s)) for s in (42, 5)]
     work.append(("W-REF", qsim.createScalingBenchmarkCircuit(n)))
     for name, c in work:
