@@ -418,8 +418,12 @@ static void add_fix(GArgs& a, int pos) {
 // Launch-shape knobs (defaults from MI355X sweeps, DESIGN.md §per-gate kernels); overridable by
 // QSIM_SLICE_U / QSIM_LANE_U / QSIM_DIAG_U (wave-items in flight per lane) and QSIM_NT (0/1:
 // non-temporal HBM loads/stores) for tuning runs.
+// Far-partner slice targets (QSIM_SLICE_FAR_LO..HI, default 20..25: the pair's two 1 KiB runs
+// 16-512 MiB apart) stream slower with one wave-item in flight per lane (0.68-0.72 of 8 TB/s at
+// 28 qubits vs 0.74-0.84 for the others); they get QSIM_SLICE_U_FAR items.
 struct Tune {
     int slice_u = 1, lane_u = 2, diag_u = 2;
+    int slice_u_far = 4, far_lo = 20, far_hi = 25;
     bool nt = true;
     Tune() {
         auto env = [](const char* k, int d) {
@@ -427,6 +431,9 @@ struct Tune {
             return v ? std::atoi(v) : d;
         };
         slice_u = env("QSIM_SLICE_U", slice_u);
+        slice_u_far = env("QSIM_SLICE_U_FAR", slice_u_far);
+        far_lo = env("QSIM_SLICE_FAR_LO", far_lo);
+        far_hi = env("QSIM_SLICE_FAR_HI", far_hi);
         lane_u = env("QSIM_LANE_U", lane_u);
         diag_u = env("QSIM_DIAG_U", diag_u);
         nt = env("QSIM_NT", nt ? 1 : 0) != 0;
@@ -513,7 +520,8 @@ void launch_op(double2* st, int n, uint64_t batch, const Op& op, hipStream_t s, 
                 add_fix(a, op.t0);
                 finish();
                 TimedLaunch tl(tm, "m1_slice", bytes, s, true);
-                QSIM_GO_U(k_m1_slice, T.slice_u, QSIM_U248);
+                const bool far = op.t0 >= T.far_lo && op.t0 <= T.far_hi;
+                QSIM_GO_U(k_m1_slice, far ? T.slice_u_far : T.slice_u, QSIM_U248);
             } else {
                 finish();
                 TimedLaunch tl(tm, "m1_lane", bytes, s, true);
