@@ -16,6 +16,9 @@ writes every amplitude once = 32 B x 2^n; per-gate kernels use the per-gate byte
 by its HIP-event-timed average duration inside the timed region (events on the last tenth of the
 timed steps, at least one: at 20 qubits events on every launch would add ~35 % to the step), against
 8 TB/s.
+roofline_1q28 / roofline_batch16: north_star's single-qubit target (W-1Q, 28 qubits) and BASELINE
+config 4 (W-BATCH 16q x 1024 under the reference noise process, the BatchedSimulator default, and
+under the physical process) measured in the same run.
 cpu_baseline: the oracle's single-threaded C++ restatement of the reference CPUSimulator
 (kind "port"), timed on this host on a bounded prefix of the same circuit.
 """
@@ -55,12 +58,14 @@ def parse():
                         "circuit on --trajectories noisy trajectories (depolarizing on every "
                         "qubit after every gate, SURVEY §8(d))")
     p.add_argument("--trajectories", type=int, default=1024)
-    p.add_argument("--batch-noise", choices=["physical", "reference"], default="physical",
-                   help="W-BATCH noise process: physical (one draw per trajectory, channel and "
-                        "gate; Pauli frames) or reference (per-pair draws after every gate, "
-                        "src/NoiseModel.cu:834-892)")
+    p.add_argument("--batch-noise", choices=["physical", "reference"], default="reference",
+                   help="W-BATCH noise process: reference (the BatchedSimulator default: per-pair "
+                        "draws after every gate, src/NoiseModel.cu:834-892) or physical (one draw "
+                        "per trajectory, channel and gate; Pauli frames)")
     p.add_argument("--no-1q28", action="store_true",
                    help="skip the W-1Q 28q single-qubit roofline object of the default line")
+    p.add_argument("--no-batch16", action="store_true",
+                   help="skip the W-BATCH 16q x 1024 object (BASELINE config 4) of the default line")
     p.add_argument("--noise", type=float, default=0.01)
     p.add_argument("--cpu-budget", type=float, default=12.0,
                    help="seconds of single-thread CPU oracle work for cpu_baseline (0 = skip)")
@@ -233,6 +238,8 @@ def run_single(args):
     del sim
     if args.workload == "hc" and not args.no_1q28:
         out["roofline_1q28"] = roofline_1q28(q)
+    if args.workload == "hc" and not args.no_batch16:
+        out["roofline_batch16"] = roofline_batch16(q, args)
     if args.cpu_budget > 0:
         out["cpu_baseline"] = cpu_baseline(circuit, n, args.cpu_budget, q, args)
     else:
@@ -272,28 +279,26 @@ def roofline_1q28(q, steps=3):
             "gates_per_s": round(100 * steps / wall, 1), "target_frac": 0.70}
 
 
-def run_batch(args):
+def measure_batch(q, n, B, steps, warmup, jit, seed, depth, p_noise, process, pmc_path=None):
     """W-BATCH (BASELINE config 4): BatchedSimulator, n qubits x B trajectories, depolarizing p on
-    every qubit after every gate (NoiseModel.addDepolarizingAll), the W-HC circuit.  value =
-    trajectory-gates/s.  Algorithmic bytes per gate step: the gate's own bytes x B plus the
-    realised Pauli errors; the dominant-kernel roofline uses each kernel's own
-    per-launch bytes."""
-    import qsim_amd as q
-    n, B = args.qubits, args.trajectories
-    circuit = q.createRandomHCCircuit(n, args.depth, args.seed)
+    every qubit after every gate (NoiseModel.addDepolarizingAll), the W-HC circuit, under one noise
+    process.  Returns value (trajectory-gates/s), ms per step, the kernel table and the dominant
+    kernel's roofline (its per-launch algorithmic bytes: a pass / gate its streaming bytes, a
+    reference noise step 32 B x the expected flipped pairs)."""
+    circuit = q.createRandomHCCircuit(n, depth, seed)
     nm = q.NoiseModel()
-    nm.addDepolarizingAll(n, args.noise)
+    nm.addDepolarizingAll(n, p_noise)
     from qsim_amd.plan import set_jit
-    set_jit(args.jit, -1)  # specialised pass kernels, compiled during the first warmup run
-    sem = q.BatchedNoise.Reference if args.batch_noise == "reference" else q.BatchedNoise.Physical
+    set_jit(jit, -1)  # specialised pass kernels, compiled during the first warmup run
+    sem = q.BatchedNoise.Reference if process == "reference" else q.BatchedNoise.Physical
     sim = q.BatchedSimulator(n, B, nm, noise=sem)
-    sim.setSeed(args.seed)
-    for _ in range(max(1, args.warmup) if args.jit else args.warmup):
+    sim.setSeed(seed)
+    for _ in range(max(1, warmup) if jit else warmup):
         sim.run(circuit)
     sim.synchronize()
     sim.profile(True)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for _ in range(steps):
         sim.run(circuit)
     sim.synchronize()
     wall = time.perf_counter() - t0
@@ -301,16 +306,15 @@ def run_batch(args):
     sim.profile(False)
     passes, jit_passes = sim.lastRunInfo()
     gates = circuit.getGateCount()
-    gate_stats = [s for s in stats if s["alg_bytes"] > 0]  # (noise kernels carry no byte count)
-    dom = max(gate_stats, key=lambda s: s["ms"]) if gate_stats else None
+    byte_stats = [s for s in stats if s["alg_bytes"] > 0]  # (frame builds carry no byte count)
+    dom = max(byte_stats, key=lambda s: s["ms"]) if byte_stats else None
     roof = None
     if dom and dom["launches"]:
         per = dom["alg_bytes"] / dom["launches"]
         avg_s = dom["ms"] / dom["launches"] / 1e3
         ach = per / avg_s / 1e9
         traffic, traffic_src = None, None
-        pmc_path = args.pmc_json or os.path.join(ROOT, "profiles", f"pmc_batch_{n}q.json")
-        if os.path.exists(pmc_path) and args.batch_noise == "physical":
+        if pmc_path and os.path.exists(pmc_path):
             with open(pmc_path) as f:
                 ent = json.load(f).get("kernels", {}).get(dom["name"], {})
             traffic = ent.get("hbm_bytes_per_launch")
@@ -320,22 +324,53 @@ def run_batch(args):
                 "traffic_source": traffic_src,
                 "alg_bytes_per_launch": per, "avg_launch_ms": round(avg_s * 1e3, 4),
                 "launches": dom["launches"]}
+    del sim
+    return {"value": round(gates * B * steps / wall, 1), "ms_per_step": round(wall / steps * 1e3, 3),
+            "gates": gates, "tile_passes": passes, "jit_passes": jit_passes, "roofline": roof,
+            "kernels": stats,
+            "noise_process": ("reference: per-pair draws, one pass per channel entry after every "
+                              "gate (src/NoiseModel.cu:834-892); the BatchedSimulator default"
+                              if process == "reference" else
+                              "physical: one draw per trajectory, channel and gate (Pauli frames)")}
+
+
+def batch_pmc_path(n, process):
+    return os.path.join(ROOT, "profiles", f"pmc_batch_{n}q.json" if process == "physical"
+                        else f"pmc_batch_ref_{n}q.json")
+
+
+def roofline_batch16(q, args):
+    """BASELINE config 4 in the default line: W-BATCH 16q x 1024 under both noise processes
+    (reference first: the drop-in default), 5 timed steps each."""
+    out = {}
+    for proc in ("reference", "physical"):
+        m = measure_batch(q, 16, 1024, 5, 1, args.jit, args.seed, args.depth, 0.01, proc,
+                          batch_pmc_path(16, proc))
+        out[proc] = {"value": m["value"], "unit": "trajectory-gates/s", "ms_per_step": m["ms_per_step"],
+                     "roofline": m["roofline"], "noise_process": m["noise_process"]}
+    out["workload"] = (f"W-BATCH 16q x 1024 trajectories, depolarizing 0.01 on all qubits after every "
+                       f"gate, W-HC depth {args.depth} seed {args.seed}")
+    return out
+
+
+def run_batch(args):
+    """W-BATCH line (--workload batch): value = trajectory-gates/s."""
+    import qsim_amd as q
+    n, B = args.qubits, args.trajectories
+    m = measure_batch(q, n, B, args.steps, args.warmup, args.jit, args.seed, args.depth, args.noise,
+                      args.batch_noise, args.pmc_json or batch_pmc_path(n, args.batch_noise))
     out = {
         "metric": "trajectory-gates/s, W-HC circuit on noisy trajectories (BatchedSimulator)",
-        "value": round(gates * B * args.steps / wall, 1), "unit": "trajectory-gates/s",
+        "value": m["value"], "unit": "trajectory-gates/s",
         "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
-        "ms_per_step": round(wall / args.steps * 1e3, 3), "higher_is_better": True,
+        "ms_per_step": m["ms_per_step"], "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "c128 (complex<double>)", "data": "synthetic",
         "config": {"workload": f"W-BATCH {n}q x {B} trajectories, depolarizing {args.noise} on all "
                                f"qubits after every gate, W-HC depth {args.depth} seed {args.seed}",
-                   "noise_process": ("reference: per-pair draws, one pass per channel entry "
-                                     "after every gate (src/NoiseModel.cu:834-892)"
-                                     if args.batch_noise == "reference" else
-                                     "physical: one draw per trajectory, channel and gate "
-                                     "(Pauli frames)"),
-                   "qubits": n, "trajectories": B, "gates": gates, "state_bytes": (16 << n) * B,
-                   "tile_passes": passes, "jit_passes": jit_passes},
-        "roofline": roof, "kernels": stats, "cpu_baseline": None,
+                   "noise_process": m["noise_process"],
+                   "qubits": n, "trajectories": B, "gates": m["gates"], "state_bytes": (16 << n) * B,
+                   "tile_passes": m["tile_passes"], "jit_passes": m["jit_passes"]},
+        "roofline": m["roofline"], "kernels": m["kernels"], "cpu_baseline": None,
     }
     print(json.dumps(out))
 

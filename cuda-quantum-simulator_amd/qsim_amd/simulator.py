@@ -455,9 +455,10 @@ class BatchedGateSet(enum.IntEnum):
 
 
 class BatchedNoise(enum.IntEnum):
-    """Physical: one draw per trajectory, channel and gate (the Kraus channel on a pure-state
-    trajectory).  Reference: the reference's per-amplitude-pair depolarizing process
-    (src/NoiseModel.cu:834-892; Depolarizing entries only)."""
+    """Reference (the default, as the reference behaves): the per-amplitude-pair depolarizing
+    process after every gate (src/NoiseModel.cu:834-892; Depolarizing entries only, SURVEY
+    F5/F7).  Physical (opt-in): one draw per trajectory, channel and gate (the Kraus channel on a
+    pure-state trajectory), run as Pauli frames inside fused passes."""
     Physical = 0
     Reference = _lib.QSIM_BATCH_REFERENCE_NOISE
 
@@ -467,7 +468,7 @@ class BatchedSimulator:
 
     def __init__(self, num_qubits: int, batch_size: int, noise_model: Optional[NoiseModel] = None,
                  gate_set: BatchedGateSet = BatchedGateSet.Full,
-                 noise: BatchedNoise = BatchedNoise.Physical):
+                 noise: BatchedNoise = BatchedNoise.Reference):
         self._h = _c.c_void_p()
         _lib.check(_lib.hip.qsim_batch_create(num_qubits, batch_size, _c.byref(self._h)))
         self._n, self._b = num_qubits, batch_size

@@ -103,10 +103,11 @@ private:
 // silently skipped (src/NoiseModel.cu:742-763, 808-812).  Full: every GateType.
 enum class BatchedGateSet { Full, Reference };
 
-// Noise process of the batched trajectories.  Physical (default): one draw per trajectory, channel
-// and gate — the Kraus channel on a pure-state trajectory, all four Pauli channel types.
-// Reference: the reference's per-amplitude-pair process — Depolarizing entries only, one draw
-// per pair per pass (applyBatchedDepolarizingKernel, src/NoiseModel.cu:834-892).
+// Noise process of the batched trajectories.  Reference (default, the drop-in behaviour): the
+// reference's per-amplitude-pair process — Depolarizing entries only, one draw per pair per pass
+// after every gate (applyBatchedDepolarizingKernel, src/NoiseModel.cu:834-892).
+// Physical (opt-in): one draw per trajectory, channel and gate — the Kraus channel on a
+// pure-state trajectory, all four Pauli channel types, run as Pauli frames inside fused passes.
 enum class BatchedNoise { Physical, Reference };
 
 class BatchedSimulator {
@@ -151,7 +152,7 @@ private:
     qsim_batch* h_ = nullptr;
     NoiseModel noise_model_;
     BatchedGateSet gate_set_ = BatchedGateSet::Full;
-    BatchedNoise noise_ = BatchedNoise::Physical;
+    BatchedNoise noise_ = BatchedNoise::Reference;
     std::mt19937 rng_;  // host sampling stream (reference rng_, src/NoiseModel.cu:661)
 };
 

@@ -262,7 +262,7 @@ def test_batched_depolarizing_statistics(qsim, gpu_ready):
     n, B, p = 1, 20000, 0.3
     nm = qsim.NoiseModel()
     nm.addDepolarizing([0], p)
-    b = qsim.BatchedSimulator(n, B, nm)
+    b = qsim.BatchedSimulator(n, B, nm, noise=qsim.BatchedNoise.Physical)
     b.setSeed(42)
     c = qsim.Circuit(1)
     c.x(0)                      # |1>; after noise: X flips to |0> (p/3), Y -> |0> (p/3), Z keeps |1>

@@ -50,7 +50,7 @@ def _noise(q, n):
 def test_frames_equal_per_gate(qsim, gpu_ready, n, B, seed):
     c = _mixed(qsim, n, 60, seed)
     nm = _noise(qsim, n)
-    fused, ref = qsim.BatchedSimulator(n, B, nm), qsim.BatchedSimulator(n, B, nm)
+    fused, ref = qsim.BatchedSimulator(n, B, nm, noise=qsim.BatchedNoise.Physical), qsim.BatchedSimulator(n, B, nm, noise=qsim.BatchedNoise.Physical)
     fused.setSeed(seed)
     ref.setSeed(seed)
     for _ in range(2):  # the second run continues the noise stream (step counter)
@@ -70,7 +70,7 @@ def test_carried_frames_through_mixed_runs(qsim, gpu_ready):
     n, B = 11, 6
     c1, c2 = _mixed(qsim, n, 40, 11), _mixed(qsim, n, 30, 12)
     nm, quiet = _noise(qsim, n), qsim.NoiseModel()
-    fused, ref = qsim.BatchedSimulator(n, B, nm), qsim.BatchedSimulator(n, B, nm)
+    fused, ref = qsim.BatchedSimulator(n, B, nm, noise=qsim.BatchedNoise.Physical), qsim.BatchedSimulator(n, B, nm, noise=qsim.BatchedNoise.Physical)
     for s in (fused, ref):
         s.setSeed(5)
     fused.run(c1)
@@ -101,7 +101,7 @@ def test_frames_reference_gateset(qsim, gpu_ready):
     nm = _noise(qsim, n)
     out = []
     for per_gate in (False, True):
-        s = qsim.BatchedSimulator(n, B, nm, gate_set=qsim.BatchedGateSet.Reference)
+        s = qsim.BatchedSimulator(n, B, nm, gate_set=qsim.BatchedGateSet.Reference, noise=qsim.BatchedNoise.Physical)
         s.setSeed(5)
         s.run(c, per_gate=per_gate)
         out.append([s.getStateVector(t) for t in range(B)])
@@ -126,7 +126,7 @@ def test_frames_noise_actually_applied(qsim, gpu_ready):
     c.h(3).cnot(3, 5).x(7)  # 3 gates -> 3 flips of qubit 0 -> net X on qubit 0
     nm = qsim.NoiseModel()
     nm.addBitFlip([0], 1.0)
-    s = qsim.BatchedSimulator(n, B, nm)
+    s = qsim.BatchedSimulator(n, B, nm, noise=qsim.BatchedNoise.Physical)
     s.run(c)
     ideal = qsim.Simulator(n)
     ideal.run(c)
@@ -156,7 +156,7 @@ def test_config4_noisy_frames_equal_per_gate(qsim, gpu_ready):
     c = qsim.createRandomHCCircuit(n, 100, 42)
     nm = qsim.NoiseModel()
     nm.addDepolarizingAll(n, 0.01)
-    fused, ref = qsim.BatchedSimulator(n, B, nm), qsim.BatchedSimulator(n, B, nm)
+    fused, ref = qsim.BatchedSimulator(n, B, nm, noise=qsim.BatchedNoise.Physical), qsim.BatchedSimulator(n, B, nm, noise=qsim.BatchedNoise.Physical)
     fused.setSeed(42)
     ref.setSeed(42)
     fused.run(c)
@@ -180,7 +180,7 @@ def test_config4_full_size_noisy_run(qsim, gpu_ready):
     c = qsim.createRandomHCCircuit(n, 100, 42)
     nm = qsim.NoiseModel()
     nm.addDepolarizingAll(n, 0.01)
-    s = qsim.BatchedSimulator(n, B, nm)
+    s = qsim.BatchedSimulator(n, B, nm, noise=qsim.BatchedNoise.Physical)
     s.setSeed(42)
     s.run(c)
     avg = s.getAverageProbabilities()
@@ -234,7 +234,7 @@ def test_relabeled_batch_equals_per_gate(qsim, gpu_ready, n, B):
     nm = _noise(qsim, n)
     set_relabel(1, 14)
     try:
-        fused, ref = qsim.BatchedSimulator(n, B, nm), qsim.BatchedSimulator(n, B, nm)
+        fused, ref = qsim.BatchedSimulator(n, B, nm, noise=qsim.BatchedNoise.Physical), qsim.BatchedSimulator(n, B, nm, noise=qsim.BatchedNoise.Physical)
         fused.setSeed(8)
         ref.setSeed(8)
         for _ in range(2):

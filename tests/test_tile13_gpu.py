@@ -60,7 +60,7 @@ def test_tile13_batched_frames_equal_per_gate(qsim, gpu_ready, tile7):
     n, B, seed = 14, 8, 7
     c = _mixed(qsim, n, 60, seed)
     nm = _noise(qsim, n)
-    fused, ref = qsim.BatchedSimulator(n, B, nm), qsim.BatchedSimulator(n, B, nm)
+    fused, ref = qsim.BatchedSimulator(n, B, nm, noise=qsim.BatchedNoise.Physical), qsim.BatchedSimulator(n, B, nm, noise=qsim.BatchedNoise.Physical)
     fused.setSeed(seed)
     ref.setSeed(seed)
     for _ in range(2):
