@@ -184,6 +184,7 @@ def run_single(args):
         0.5 * sum(sorted(step_s)[len(step_s) // 2 - 1:len(step_s) // 2 + 1])
     gates = circuit.getGateCount()
     layout = sim.state.layoutInfo()
+    run_passes = sim.state.lastRunInfo()[0]
     # what the timed loop never pays: the first index-based readback after a relabeled run
     # restores the identity layout with a fused SWAP network
     restore_ms = None
@@ -227,6 +228,7 @@ def run_single(args):
                    "pass_kernels": "jit" if args.jit else "interpreter",
                    "jit_mode": args.jit, "tile_qubits": layout["tile_qubits"],
                    "calibrated": layout["calibrated"], "relabel": layout["relabeled"],
+                   "relayout": layout["relayout"], "passes": run_passes,
                    "state_bytes": 16 << n, "parallelism": "single GPU"},
         "value_is": "gates / median step time (every step synchronised); value_mean = gates x steps / wall",
         "restore_ms": restore_ms,

@@ -11,6 +11,7 @@
 #include <cstring>
 #include <memory>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "engine.hpp"
@@ -199,6 +200,7 @@ struct qsim_state {
     // whether its layout was chosen by timing candidates on the device
     int tile_h = -1;
     bool calibrated = false;
+    bool relayout = false;  // the first-run choice is a relayout plan (relayout.hip)
     ~qsim_state() {
         if (stream) (void)hipStreamSynchronize(stream);
         if (base) (void)hipFree(base);
@@ -279,6 +281,7 @@ struct LayoutCandidate {
     std::vector<int> perm;  // empty: identity
     std::vector<Op> ops;
     Plan plan;
+    bool relayout = false;  // a relayout plan (relayout.hip)
 };
 // Time every candidate with its own circuit-specialised kernels on this device (each candidate's
 // whole plan under its own tile height, the faster of two runs, the basis state restored after
@@ -370,6 +373,22 @@ static void choose_first_layout(qsim_state* s, const qsim_gate* gates, size_t co
         const TileHeightScope scope(th);  // (a single-height decision is keyed by its height)
         layout_memo_put(n, 0, gates, bytes, perm, heights ? s->tile_h : -1);
     };
+    const bool relayout = relayout_enabled(n) && !tile_height_is_set();
+    {
+        std::vector<int> memo;
+        int mh = -1;
+        if (relayout && layout_memo_get(n, 2, gates, bytes, memo, &mh)) {  // a relayout choice
+            RelayoutChoice rc;
+            if (plan_relayout(n, lower_under, SIZE_MAX, rc) && rc.perm == memo) {
+                const TileHeightScope scope(6, tile_rb_for(n, 6));
+                s->plans.put(rc.ops, n, std::move(rc.plan), s->stream);
+                s->perm = memo;
+                s->tile_h = 6;
+                s->relayout = true;
+                return;
+            }
+        }
+    }
     {
         std::vector<int> memo;
         int mh = -1;
@@ -391,17 +410,55 @@ static void choose_first_layout(qsim_state* s, const qsim_gate* gates, size_t co
         else gens.insert(gens.end(), {{7, 1.25, alts}, {7, 1.0, 0}});
     }
     std::vector<LayoutCandidate> cands;
-    auto add = [&](int h, std::vector<int> perm, std::vector<Op> ops, Plan plan) {
+    auto add = [&](int h, std::vector<int> perm, std::vector<Op> ops, Plan plan, bool rl = false) {
         for (const LayoutCandidate& c : cands)
-            if (c.h == h && c.perm == perm) return;  // the same candidate from two generators
-        cands.push_back(LayoutCandidate{h, std::move(perm), std::move(ops), std::move(plan)});
+            if (c.h == h && c.perm == perm && c.relayout == rl) return;  // the same candidate twice
+        cands.push_back(LayoutCandidate{h, std::move(perm), std::move(ops), std::move(plan), rl});
+    };
+    // Relayout plan (12-qubit tiles, every pass stores under the next pass's layout): a
+    // candidate like the others when candidates are timed, else taken when it needs fewer passes
+    // than the fixed-layout choice.
+    // (planned on a worker thread while the fixed-layout candidates are chosen)
+    RelayoutChoice rc;
+    bool have_rc = false;
+    struct Joiner {
+        std::thread t;
+        void join() {
+            if (t.joinable()) t.join();
+        }
+        ~Joiner() { join(); }
+    } rc_worker;
+    if (relayout)
+        rc_worker.t = std::thread([&] {
+            try {
+                const TileHeightScope scope(6, tile_rb_for(n, 6));
+                have_rc = plan_relayout(n, lower_under, SIZE_MAX, rc);
+            } catch (...) {
+                have_rc = false;  // (no relayout candidate)
+            }
+        });
+    const bool timing = relabel_calibrate(n);
+    auto take_relayout = [&]() {
+        {
+            const TileHeightScope scope(6, tile_rb_for(n, 6));
+            s->plans.put(rc.ops, n, std::move(rc.plan), s->stream);
+        }
+        s->perm = rc.perm;
+        s->tile_h = 6;
+        s->relayout = true;
+        layout_memo_put(n, 2, gates, bytes, s->perm, 6);
     };
     for (const Gen& g : gens) {
         const TileHeightScope scope(g.h, tile_rb_for(n, g.h));
         const LayoutT13Scope t13(g.t13);
         LayoutChoice lc = choose_layout(n, lower_under, relabel_tries(), g.alts);
+        rc_worker.join();
         if (lc.perm.empty()) {  // the identity is this height's choice
-            if (!heights) {  // (nothing to time: keep the identity)
+            if (!heights && !(have_rc && timing)) {  // (nothing to time)
+                if (have_rc && rc.plan.passes.size() < lc.passes_before) {
+                    take_relayout();
+                    return;
+                }
                 memo_put({});
                 return;
             }
@@ -415,6 +472,14 @@ static void choose_first_layout(qsim_state* s, const qsim_gate* gates, size_t co
         }
         for (LayoutChoice::Alt& a : lc.alts) add(g.h, std::move(a.perm), std::move(a.ops), std::move(a.plan));
     }
+    if (have_rc) {
+        if (timing) {
+            add(6, rc.perm, rc.ops, rc.plan, true);
+        } else if (rc.plan.passes.size() < cands[0].plan.passes.size()) {
+            take_relayout();
+            return;
+        }
+    }
     size_t best = 0;
     if (cands.size() > 1) {
         best = calibrate_candidates(s, cands);  // (their plans stay cached, compiled)
@@ -423,10 +488,15 @@ static void choose_first_layout(qsim_state* s, const qsim_gate* gates, size_t co
         if (!cands[0].perm.empty()) s->plans.put(cands[0].ops, n, cands[0].plan, s->stream);
     }
     LayoutCandidate& w = cands[best];
+    s->calibrated = cands.size() > 1;
+    if (w.relayout) {
+        if (have_rc) rc.plan = w.plan;  // (re-put: the timing loop may have evicted it)
+        take_relayout();
+        return;
+    }
     if (heights) s->tile_h = w.h;
     s->perm = std::move(w.perm);
     memo_put(s->perm);
-    s->calibrated = cands.size() > 1;
 }
 
 static qsim_gate map_gate(const qsim_state* s, const qsim_gate& g) {
@@ -456,6 +526,14 @@ int qsim_state_layout_info(qsim_state* s, int* tile_h, int* calibrated, int* rel
         if (tile_h) *tile_h = s->tile_h >= 0 ? s->tile_h : tile_height_for(s->n);
         if (calibrated) *calibrated = s->calibrated ? 1 : 0;
         if (relabeled) *relabeled = s->perm.empty() ? 0 : 1;
+    });
+}
+
+int qsim_state_relayout(qsim_state* s, int* relayout) {
+    return guarded([&] {
+        check_state(s);
+        QSIM_REQUIRE(relayout, QSIM_ERR_INVALID_ARGUMENT, "null out");
+        *relayout = s->relayout ? 1 : 0;
     });
 }
 
@@ -598,6 +676,7 @@ int qsim_state_init_zero(qsim_state* s) {
         s->basis_idx = 0;
         s->tile_h = -1;  // (the next first run chooses again: memo)
         s->calibrated = false;
+        s->relayout = false;
     });
 }
 
@@ -613,6 +692,7 @@ int qsim_state_init_basis(qsim_state* s, uint64_t idx) {
         s->basis_idx = idx;
         s->tile_h = -1;
         s->calibrated = false;
+        s->relayout = false;
     });
 }
 
@@ -938,6 +1018,31 @@ int qsim_jit_build(int n_qubits, const qsim_gate* gates, size_t count, size_t* c
         std::string src(len + 1, '\0');
         qsim_jit_source(n_qubits, gates, count, &src[0], len + 1, &len);
         src.resize(len);
+        std::vector<char> code;
+        std::string log;
+        if (!src.empty() && !jit_compile(src, code, log)) fail(QSIM_ERR_RUNTIME, "hipRTC: " + log);
+        if (code_bytes) *code_bytes = code.size();
+    });
+}
+
+int qsim_jit_build_relayout(int n_qubits, const qsim_gate* gates, size_t count, size_t* code_bytes) {
+    return guarded([&] {
+        QSIM_REQUIRE(gates || count == 0, QSIM_ERR_INVALID_ARGUMENT, "null gate list");
+        if (n_qubits < QSIM_MIN_QUBITS || n_qubits > 40) fail(QSIM_ERR_INVALID_ARGUMENT, "bad qubit count");
+        for (size_t i = 0; i < count; ++i) validate_gate(gates[i], n_qubits);
+        auto lower = [&](const std::vector<int>& pi) {
+            std::vector<Op> ops;
+            for (size_t i = 0; i < count; ++i) {
+                qsim_gate m = gates[i];
+                for (int j = 0; j < m.nqubits && j < 3; ++j) m.qubits[j] = pi[m.qubits[j]];
+                ops.push_back(lower_gate(m, n_qubits));
+                ops.back().src = (int)i;
+            }
+            return ops;
+        };
+        RelayoutChoice rc;
+        if (!plan_relayout(n_qubits, lower, SIZE_MAX, rc)) fail(QSIM_ERR_RUNTIME, "no relayout plan");
+        const std::string src = jit_source(rc.plan);
         std::vector<char> code;
         std::string log;
         if (!src.empty() && !jit_compile(src, code, log)) fail(QSIM_ERR_RUNTIME, "hipRTC: " + log);

@@ -107,6 +107,15 @@ struct FusedPass {
     // Algorithmic HBM bytes per amplitude of the pass: min(32, sum of its gates' SURVEY §8(d)
     // bytes) — a pass of one CNOT is charged 16, not the 32 a full read+write would move.
     double alg_bpa = 32.0;
+    // Relayout pass (plan_relayout, relayout.hip): the tile is loaded under this pass's layout
+    // (r0 / hpos above) but stored under the next pass's: tile bit x goes to physical position
+    // st_pos[x], tile-id bit i (the i-th non-tile position of the load layout, ascending) to
+    // st_tid[i].  The last stage's lanes are the tile bits with the lowest store positions
+    // (Stage::tmap), so the store still moves whole runs.
+    int relayout = 0;
+    int st_pos[13] = {0};
+    int st_tid[32] = {0};
+    int n_tid = 0;
 };
 struct TileOp {            // an Op re-expressed in tile-index bits
     int kind, sub, b0, b1;
@@ -141,7 +150,12 @@ struct Stage {
     uint32_t trow_in[4], trow_out[4];  // the two layouts' sigma rows (see above)
     int fix[4];            // ascending stage tile bits
     int op_begin, op_end;
-    int _pad[2];
+    // Thread bit i of the stage's element index jb sits at tile bit tmap[i] (the non-register
+    // tile bits, ascending — the zero insertion at fix[] — except in the last stage of a
+    // relayout pass, where they are ordered by store position).  tscatter != 0: use tmap.
+    int tmap[10];
+    int tscatter;
+    int _pad;
 };
 // sigma of a layout (host and device)
 __host__ __device__ __forceinline__ uint32_t lds_sigma(uint32_t j, const uint32_t* trow) {
@@ -170,6 +184,24 @@ constexpr int kTileR0 = 6;    // contiguous run bits of a staged tile (QSIM_TILE
 // hmax < 0: the process default (kTileHDefault, or QSIM_TILE_HMAX up to kTileHMax).
 // avoid: qubits no tile may contain (ops never act on them; only tile padding is affected).
 Plan plan_fused(const std::vector<Op>& ops, int n, int hmax = -1, uint64_t avoid = 0);
+// One tile pass appended to a plan (fused.hip; plan_fused and the relayout planner use it).
+void append_tile_pass(Plan& plan, const std::vector<Op>& ops, int n, int h, int r0, const int* hpos,
+                      const int* bit_of, const int* st_pos, const int* st_tid);
+// Relayout plans (relayout.hip): every pass stores its tile under the next pass's layout, so
+// each pass may choose all of its tile qubits except the four of the contiguous run, which come
+// from the pass before (the last pass restores the first layout, so re-runs need no restore).
+// `lower` maps the circuit through a logical -> physical permutation exactly as the caller will.
+// Returns false when no relayout plan beats `max_passes` passes.
+struct RelayoutChoice {
+    std::vector<int> perm;  // the first (and last) layout, logical -> physical
+    std::vector<Op> ops;    // the circuit lowered under perm
+    Plan plan;
+    double cost_us = 0.0;   // predicted (layout model)
+};
+bool plan_relayout(int n, const std::function<std::vector<Op>(const std::vector<int>&)>& lower,
+                   size_t max_passes, RelayoutChoice& out);
+bool relayout_enabled(int n);  // QSIM_RELAYOUT (default 1), QSIM_RELAYOUT_MIN_QUBITS (default 22)
+void relayout_configure(int mode, int min_qubits);  // qsim_set_relayout; < 0 leaves a setting
 int tile_height_default();             // the h that hmax < 0 means (scope, setting, env, 6)
 int tile_height_for(int n);            // a single-GPU state's height (the setting, or by size)
 bool tile_height_is_set();             // qsim_set_tile_height or QSIM_TILE_HMAX in force

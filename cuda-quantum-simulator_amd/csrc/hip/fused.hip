@@ -64,7 +64,9 @@ static constexpr int kMaxUnnormH = 512;
 // `sbits` (lanes = the stage's thread bits: tid spread over the other tile bits) under layout
 // `trow`: ds_write_b128 banks by slot mod 8 in 8 groups of 8 contiguous lanes, ds_read_b128 by
 // slot mod 16 in 4 groups of 16 lanes (MI355X_MICROARCH.md §LDS).
-static int lds_conflicts(uint32_t sbits, const uint32_t* trow, bool write, int tile_bits) {
+// tmap (null: ascending) orders the lanes over the non-register tile bits (Stage::tmap).
+static int lds_conflicts(uint32_t sbits, const uint32_t* trow, bool write, int tile_bits,
+                         const int* tmap = nullptr) {
     static const int kReadGroups[4][16] = {
         {0, 1, 2, 3, 12, 13, 14, 15, 20, 21, 22, 23, 24, 25, 26, 27},
         {4, 5, 6, 7, 8, 9, 10, 11, 16, 17, 18, 19, 28, 29, 30, 31},
@@ -76,7 +78,12 @@ static int lds_conflicts(uint32_t sbits, const uint32_t* trow, bool write, int t
     uint32_t lane_j[64];
     for (int l = 0; l < 64; ++l) {
         uint32_t j = (uint32_t)l;
-        for (int i = 0; i < nf; ++i) j = ins0_host(j, fix[i]);
+        if (tmap) {
+            j = 0;
+            for (int i = 0; i < 6; ++i) j |= (uint32_t)((l >> i) & 1) << tmap[i];
+        } else {
+            for (int i = 0; i < nf; ++i) j = ins0_host(j, fix[i]);
+        }
         lane_j[l] = j;
     }
     int extra = 0;
@@ -107,12 +114,13 @@ static int lds_conflicts(uint32_t sbits, const uint32_t* trow, bool write, int t
 // A layout for the LDS round trip between a stage with register bits `wbits` (writes) and one
 // with `rbits` (reads): the fixed j ^ ((j >> 4) & 15) when it is conflict-free, else the best
 // triangular swizzle found by a deterministic random search with local moves.
-static std::array<uint32_t, 4> choose_swizzle(uint32_t wbits, uint32_t rbits, int tile_bits) {
+static std::array<uint32_t, 4> choose_swizzle(uint32_t wbits, uint32_t rbits, int tile_bits,
+                                              const int* rtmap = nullptr) {
     std::array<uint32_t, 4> best = {0x10u, 0x20u, 0x40u, 0x80u};
     const uint32_t all = (1u << tile_bits) - 1u;
     auto cost = [&](const std::array<uint32_t, 4>& t) {
         return lds_conflicts(wbits, t.data(), true, tile_bits) +
-               lds_conflicts(rbits, t.data(), false, tile_bits);
+               lds_conflicts(rbits, t.data(), false, tile_bits, rtmap);
     };
     int bc = cost(best);
     uint64_t rng = 0x9e3779b97f4a7c15ull ^ ((uint64_t)wbits << 20) ^ rbits;
@@ -141,8 +149,11 @@ static std::array<uint32_t, 4> choose_swizzle(uint32_t wbits, uint32_t rbits, in
 }
 
 // Group one pass's ops (tile bits) into register stages of at most `rb` target bits.
+// st_pos (relayout passes, else null): store position of every tile bit; the last stage's lanes
+// are then the six tile bits with the lowest store positions (its register bits avoid them) and
+// its HBM offsets are store positions — a relayout pass always has an LDS round trip before it.
 static void plan_stages(std::vector<TileOp>& pass_ops, std::vector<int>& pass_src, int tile_bits,
-                        int rb, Plan& plan, FusedPass& p) {
+                        int rb, Plan& plan, FusedPass& p, const int* st_pos = nullptr) {
     // SWAP -> three controlled-X on the register bits (exact data movement).
     std::vector<TileOp> ops;
     std::vector<int> src;
@@ -232,18 +243,42 @@ static void plan_stages(std::vector<TileOp>& pass_ops, std::vector<int>& pass_sr
         seq.push_back({t.sbits, t.in});
         rem.swap(t.deferred);
     }
-    if (seq.size() > 1) {  // the last stage must be storable straight from registers
-        if ((seq.back().first & ~high_bits) == 0)
-            seq.back().first = pad(seq.back().first, high_bits, seq.back().second);
+    // tile bits by store position (relayout): the first six are the store's lanes
+    int st_order[32];
+    uint32_t st_high = high_bits;
+    if (st_pos) {
+        for (int b = 0; b < tile_bits; ++b) st_order[b] = b;
+        std::sort(st_order, st_order + tile_bits, [&](int a, int b) { return st_pos[a] < st_pos[b]; });
+        st_high = all_bits;
+        for (int i = 0; i < 6; ++i) st_high &= ~(1u << st_order[i]);
+    }
+    if (st_pos && seq.size() == 1) {
+        seq.push_back({pad(0u, st_high, {}), {}});
+    } else if (seq.size() > 1) {  // the last stage must be storable straight from registers
+        if ((seq.back().first & ~st_high) == 0)
+            seq.back().first = pad(seq.back().first, st_high, seq.back().second);
         else
-            seq.push_back({pad(0u, high_bits, {}), {}});
+            seq.push_back({pad(0u, st_high, {}), {}});
+    }
+    // thread-bit -> tile-bit map of every stage (ascending non-register bits; the relayout
+    // pass's last stage in store-position order)
+    std::vector<std::array<int, 10>> tmaps(seq.size());
+    for (size_t si = 0; si < seq.size(); ++si) {
+        int k = 0;
+        const bool sorted = st_pos && si + 1 == seq.size();
+        for (int i = 0; i < tile_bits; ++i) {
+            const int b = sorted ? st_order[i] : i;
+            if (!((seq[si].first >> b) & 1u) && k < 10) tmaps[si][k++] = b;
+        }
+        for (; k < 10; ++k) tmaps[si][k] = 0;
     }
     for (size_t k = 1; k + 1 < seq.size(); ++k) seq[k].first = pad(seq[k].first, all_bits, seq[k].second);
     // LDS layouts of the transitions: transition k sits between stage k's writes and stage k+1's
     // reads; each gets a conflict-free swizzle (choose_swizzle)
     std::vector<std::array<uint32_t, 4>> layout(seq.size());
     for (size_t k = 0; k + 1 < seq.size(); ++k)
-        layout[k] = choose_swizzle(seq[k].first, seq[k + 1].first, tile_bits);
+        layout[k] = choose_swizzle(seq[k].first, seq[k + 1].first, tile_bits,
+                                   st_pos && k + 2 == seq.size() ? tmaps[k + 1].data() : nullptr);
     for (size_t si = 0; si < seq.size(); ++si) {
         auto& sq = seq[si];
         const uint32_t sbits = sq.first;
@@ -264,13 +299,16 @@ static void plan_stages(std::vector<TileOp>& pass_ops, std::vector<int>& pass_sr
                 pos_of[b] = k;
                 ++k;
             }
+        const bool store_map = st_pos && si + 1 == seq.size();
+        for (int i = 0; i < 10; ++i) st.tmap[i] = tmaps[si][i];
+        st.tscatter = store_map ? 1 : 0;
         for (int r = 0; r < (1 << rb); ++r) {
             uint32_t o = 0;
             for (int i = 0; i < rb; ++i)
                 if ((r >> i) & 1) o |= 1u << st.fix[i];
             uint64_t g = 0;
             for (int b = 0; b < tile_bits; ++b)
-                if ((o >> b) & 1u) g |= 1ull << (b < p.r0 ? b : p.hpos[b - p.r0]);
+                if ((o >> b) & 1u) g |= 1ull << (store_map ? st_pos[b] : b < p.r0 ? b : p.hpos[b - p.r0]);
             st.goff[r] = g;
             st.lds[r] = 16u * lds_sigma(o, st.trow_in);
             st.lds_w[r] = 16u * lds_sigma(o, st.trow_out);
@@ -667,6 +705,55 @@ void tile_height_configure(int h) {
     g_tile_h.store(h < 0 ? -1 : h);
 }
 
+// One staged (h >= 4) or unstaged tile pass appended to `plan`: tile bits 0..r0-1 are physical
+// positions 0..r0-1, tile bits r0.. are hpos[] (ascending); bit_of[q] is the tile bit of qubit q
+// as the ops name it.  st_pos / st_tid (relayout passes, relayout.hip; null otherwise): store
+// positions of the tile bits and of the tile-id bits.
+void append_tile_pass(Plan& plan, const std::vector<Op>& ops, int n, int h, int r0, const int* hpos,
+                      const int* bit_of, const int* st_pos, const int* st_tid) {
+    FusedPass p;
+    p.h = h;
+    p.r0 = r0;
+    double bpa = 0.0;
+    for (const Op& op : ops) bpa += op_alg_bytes(op, 1.0);
+    p.alg_bpa = std::min(32.0, bpa);
+    for (int i = 0; i < 6 + h - r0; ++i) p.hpos[i] = hpos[i];
+    if (st_pos) {
+        p.relayout = 1;
+        p.n_tid = n - 6 - h;
+        if (p.n_tid > 32 || h < 4) fail(QSIM_ERR_RUNTIME, "relayout pass out of range");
+        for (int x = 0; x < 6 + h; ++x) p.st_pos[x] = st_pos[x];
+        for (int i = 0; i < p.n_tid; ++i) p.st_tid[i] = st_tid[i];
+    }
+    std::vector<TileOp> tops;
+    std::vector<int> tsrc;
+    for (const Op& op : ops) {
+        uint32_t cm = 0;
+        for (int q = 0; q < n; ++q)
+            if ((op.cmask >> q) & 1ull) cm |= 1u << bit_of[q];
+        int b0 = bit_of[op.t0], b1 = op.kind == K_SWAP ? bit_of[op.t1] : -1;
+        if (op.kind == K_SWAP && b0 > b1) std::swap(b0, b1);
+        tops.push_back(make_tile_op(op.kind, op.sub, b0, b1, cm, op.d0_one ? 1 : 0, op.m));
+        tops.back().step = op.src;
+        tsrc.push_back(op.src);
+    }
+    if (h >= 4) {
+        p.rb = tile_rb_default(h);
+        plan_stages(tops, tsrc, 6 + h, p.rb, plan, p, st_pos);
+    } else {
+        if (st_pos) fail(QSIM_ERR_RUNTIME, "relayout pass needs staged tiles");
+        p.op_begin = (int)plan.ops.size();
+        for (size_t i = 0; i < tops.size(); ++i) {
+            plan.ops.push_back(tops[i]);
+            plan.order.push_back(tsrc[i]);
+        }
+        p.op_end = (int)plan.ops.size();
+    }
+    plan.fused_gate_count += ops.size();
+    plan.tile_passes += 1;
+    plan.passes.push_back(p);
+}
+
 Plan plan_fused(const std::vector<Op>& ops, int n, int hmax, uint64_t avoid) {
     if (hmax < 0) hmax = tile_height_default();
     Plan plan;
@@ -741,47 +828,16 @@ Plan plan_fused(const std::vector<Op>& ops, int n, int hmax, uint64_t avoid) {
         // the avoided qubit, which the caller detects (the sharded engine then runs the step on
         // the whole shard)
         for (int q = r0; q < n && __builtin_popcountll(hi) < nfree; ++q) hi |= 1ull << q;
-        FusedPass p;
-        p.h = hp;
-        p.r0 = r0;
-        double bpa = 0.0;
-        for (const Op& op : ch.ops) bpa += op_alg_bytes(op, 1.0);
-        p.alg_bpa = std::min(32.0, bpa);
+        int hpos[kHposMax] = {0}, bit_of[64];
         int k = 0;
-        int bit_of[64];
         for (int q = 0; q < r0; ++q) bit_of[q] = q;
         for (int q = r0; q < n; ++q)
             if ((hi >> q) & 1ull) {
-                p.hpos[k] = q;
+                hpos[k] = q;
                 bit_of[q] = r0 + k;
                 ++k;
             }
-        std::vector<TileOp> tops;
-        std::vector<int> tsrc;
-        for (const Op& op : ch.ops) {
-            uint32_t cm = 0;
-            for (int q = 0; q < n; ++q)
-                if ((op.cmask >> q) & 1ull) cm |= 1u << bit_of[q];
-            int b0 = bit_of[op.t0], b1 = op.kind == K_SWAP ? bit_of[op.t1] : -1;
-            if (op.kind == K_SWAP && b0 > b1) std::swap(b0, b1);
-            tops.push_back(make_tile_op(op.kind, op.sub, b0, b1, cm, op.d0_one ? 1 : 0, op.m));
-            tops.back().step = op.src;
-            tsrc.push_back(op.src);
-        }
-        if (hp >= 4) {
-            p.rb = tile_rb_default(hp);
-            plan_stages(tops, tsrc, 6 + hp, p.rb, plan, p);
-        } else {
-            p.op_begin = (int)plan.ops.size();
-            for (size_t i = 0; i < tops.size(); ++i) {
-                plan.ops.push_back(tops[i]);
-                plan.order.push_back(tsrc[i]);
-            }
-            p.op_end = (int)plan.ops.size();
-        }
-        plan.fused_gate_count += ch.ops.size();
-        plan.tile_passes += 1;
-        plan.passes.push_back(p);
+        append_tile_pass(plan, ch.ops, n, hp, r0, hpos, bit_of, nullptr, nullptr);
     }
     return plan;
 }
@@ -808,6 +864,10 @@ struct FArgs {
     // Sub-space launch (sharded engine's overlapped remaps): tiles skip the fix_mask positions,
     // which read fix_val; zmask = fix_mask | the tile's own positions above the run.
     uint64_t fix_mask, fix_val, zmask;
+    // Relayout pass (FusedPass::relayout): store positions of tile bits and tile-id bits.
+    int relayout, n_tid;
+    int st_pos[13];
+    int st_tid[32];
 };
 
 // Runtime-count forms for the staged kernel (count = tile bits above the run, < kHposMax).
@@ -1203,13 +1263,26 @@ __global__ __launch_bounds__((64 << H) >> RBT, H >= 7 ? 1 : 2) void k_fused_stag
         kt = deposit_n(kt, a.hpos, nh);
     }
     const uint64_t base = (tile_id >> a.log_tpt) * a.stride + kt;
+    uint64_t base_st = 0;  // relayout: the tile's base under the next pass's layout
+    if (a.relayout) {
+        const uint64_t kl = tile_id & a.tpt_mask;
+        for (int i = 0; i < a.n_tid; ++i) base_st |= ((kl >> i) & 1ull) << a.st_tid[i];
+        base_st += (tile_id >> a.log_tpt) * a.stride;
+    }
     const uint32_t run_mask = (1u << r0) - 1u;
     const int sb = a.stage_begin, se = a.stage_end;
     double2 v[R];
     char* const lds = reinterpret_cast<char*>(tile);
     for (int s = sb; s < se; ++s) {  // one copy of the op interpreter; phase branches are uniform
         const Stage sg = ldc(a.stages, s);
-        const uint32_t jb = stage_jb<RB>(sg);
+        uint32_t jb;
+        if (sg.tscatter) {  // relayout pass, last stage: lanes over the store's run bits
+            jb = 0;
+#pragma unroll
+            for (int i = 0; i < 6 + H - RB; ++i) jb |= ((threadIdx.x >> i) & 1u) << sg.tmap[i];
+        } else {
+            jb = stage_jb<RB>(sg);
+        }
         const uint32_t lb = 16u * lds_sigma(jb, sg.trow_in);    // thread part: LDS reads
         const uint32_t lbw = 16u * lds_sigma(jb, sg.trow_out);  // and writes
         if (s == sb) {
@@ -1231,7 +1304,14 @@ __global__ __launch_bounds__((64 << H) >> RBT, H >= 7 ? 1 : 2) void k_fused_stag
             for (int o = sg.op_begin; o < sg.op_end; ++o) stage_op<RB>(v, jb, ldc(a.ops, o));
         }
         if (s == se - 1) {
-            const uint64_t gb = base | (jb & run_mask) | spread_n(jb >> r0, a.hpos, nh);
+            uint64_t gb;
+            if (a.relayout) {
+                gb = base_st;
+#pragma unroll
+                for (int x = 0; x < 6 + H; ++x) gb |= (uint64_t)((jb >> x) & 1u) << a.st_pos[x];
+            } else {
+                gb = base | (jb & run_mask) | spread_n(jb >> r0, a.hpos, nh);
+            }
             const double sc = a.scale;
 #pragma unroll
             for (int r = 0; r < R; ++r)
@@ -1305,6 +1385,15 @@ void launch_fused(double2* st, int n, uint64_t batch, const Plan& plan, const Ti
         a.fix_mask = range.fix_mask;
         a.fix_val = range.fix_val;
         a.zmask = hmask | range.fix_mask;
+        if (p.relayout) {
+            if (range.fix_mask || frames || p.h < 4 || p.stage_end - p.stage_begin < 2)
+                fail(QSIM_ERR_RUNTIME, "relayout pass outside a whole-state staged run");
+            if (n - 6 - p.h != p.n_tid || p.n_tid > 32) fail(QSIM_ERR_RUNTIME, "relayout pass planned for another size");
+            a.relayout = 1;
+            a.n_tid = p.n_tid;
+            for (int i = 0; i < 13; ++i) a.st_pos[i] = p.st_pos[i];
+            for (int i = 0; i < 32; ++i) a.st_tid[i] = p.st_tid[i];
+        }
         const int lt = n - 6 - p.h - nfix;
         a.log_tpt = lt;
         a.tpt_mask = (1ull << lt) - 1ull;

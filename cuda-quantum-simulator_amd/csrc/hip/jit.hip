@@ -222,8 +222,29 @@ bool jit_pass_pipelined(const FusedPass& p) {
     return v >= 2 || (v == 1 && p.h >= 7);
 }
 namespace {
+// sum_i ((src >> i) & 1) << dst[i] over i < cnt, consecutive bit runs moved by one mask + shift
+std::string scatter_expr(const std::string& src, const int* dst, int cnt, bool wide) {
+    const std::string ty = wide ? "(unsigned long long)" : "";
+    const std::string one = wide ? "1ull" : "1u";
+    std::string e;
+    for (int i = 0; i < cnt;) {
+        int k = 1;
+        while (i + k < cnt && dst[i + k] == dst[i] + k) ++k;
+        const uint64_t m = ((1ull << k) - 1ull) << i;
+        std::string t = "(" + ty + "(" + src + " & " + (wide ? hexu(m) : std::to_string((uint32_t)m) + "u") + ")";
+        const int sh = dst[i] - i;
+        if (sh > 0) t += " << " + std::to_string(sh);
+        else if (sh < 0) t += " >> " + std::to_string(-sh);
+        t += ")";
+        e += e.empty() ? t : " | " + t;
+        i += k;
+    }
+    (void)one;
+    return e.empty() ? (wide ? std::string("0ull") : std::string("0u")) : e;
+}
 // Thread index spread over the tile bits that are not register bits of stage `st`.
-std::string jb_expr(const Stage& st, int rb) {
+std::string jb_expr(const Stage& st, int rb, int tile_bits) {
+    if (st.tscatter) return scatter_expr("tid", st.tmap, tile_bits - rb, false);
     std::string e = "tid";
     for (int i = 0; i < rb; ++i) e = "qins0(" + e + ", " + std::to_string(st.fix[i]) + ")";
     return e;
@@ -260,6 +281,7 @@ void gen_pass(std::ostringstream& out, const Plan& plan, const FusedPass& p, int
     const int H = p.h, RB = p.rb, R = 1 << RB, T = 64 << H;
     const int r0 = p.r0, nh = 6 + H - r0;
     const bool pipe = jit_pass_pipelined(p);
+    if (pipe && p.relayout) fail(QSIM_ERR_RUNTIME, "relayout passes are not pipelined");
     Gen g;
     g.R = R;
     g.RB = RB;
@@ -324,7 +346,7 @@ void gen_pass(std::ostringstream& out, const Plan& plan, const FusedPass& p, int
         o << "  }\n";
         {
             const Stage& st0 = plan.stages[sb];
-            o << "  const unsigned long long gth0 = [&] { const unsigned jb = " << jb_expr(st0, RB) << "; return "
+            o << "  const unsigned long long gth0 = [&] { const unsigned jb = " << jb_expr(st0, RB, 6 + H) << "; return "
               << gthread(st0) << "; }();\n";
             for (int r = 0; r < R; ++r) o << "  v" << r << " = qld(st + (base | gth0 | " << hexu(st0.goff[r]) << "));\n";
         }
@@ -334,15 +356,22 @@ void gen_pass(std::ostringstream& out, const Plan& plan, const FusedPass& p, int
     } else {
         o << tile_id_expr() << "  unsigned long long base;\n";
         tile_base("tile_id", "base");
+        if (p.relayout)  // the tile's base under the next pass's layout
+            o << "  const unsigned long long base_st = (tile_id >> log_tpt) * stride | ("
+              << scatter_expr("(tile_id & tpt_mask)", p.st_tid, p.n_tid, true) << ");\n";
     }
     auto body = [&]() {
         for (int r = 0; r < R; ++r) g.nm[r] = r;
         if (pipe) o << "  const bool more = tile_ok(it + 1);\n";
         for (int s = sb; s < se; ++s) {
             const Stage& st = plan.stages[s];
-            o << "  {\n  const unsigned jb = " << jb_expr(st, RB) << ";\n";
+            o << "  {\n  const unsigned jb = " << jb_expr(st, RB, 6 + H) << ";\n";
             if (s == sb && pipe) o << "  const unsigned long long gb = base | gth0;\n";
-            else if (s == sb || s == se - 1) o << "  const unsigned long long gb = base | " << gthread(st) << ";\n";
+            else if (s == se - 1 && p.relayout) {
+                int dst[16];
+                for (int i = 0; i < 6 + H - RB; ++i) dst[i] = p.st_pos[st.tmap[i]];
+                o << "  const unsigned long long gb = base_st | " << scatter_expr("(unsigned long long)tid", dst, 6 + H - RB, true) << ";\n";
+            } else if (s == sb || s == se - 1) o << "  const unsigned long long gb = base | " << gthread(st) << ";\n";
             auto sigma_expr = [](const uint32_t* trow) {
                 std::string e = "jb";
                 for (int i = 0; i < 4; ++i)

@@ -100,6 +100,13 @@ _sig(hip, "qsim_set_relabel", [c_int, c_int])
 _sig(hip, "qsim_state_perm", [_P, POINTER(c_int32)])
 _sig(hip, "qsim_state_layout_info", [_P, POINTER(c_int), POINTER(c_int), POINTER(c_int)])
 _sig(hip, "qsim_state_restore_layout", [_P])
+_sig(hip, "qsim_state_relayout", [_P, POINTER(c_int)])
+_sig(hip, "qsim_set_relayout", [c_int, c_int])
+_sig(hip, "qsim_jit_build_relayout", [c_int, POINTER(qsim_gate), c_size_t, POINTER(c_size_t)])
+_sig(hip, "qsim_plan_relayout", [c_int, POINTER(qsim_gate), c_size_t, POINTER(c_int32), POINTER(c_int),
+                                 POINTER(c_double)])
+_sig(hip, "qsim_plan_exec_host", [c_int, POINTER(qsim_gate), c_size_t, c_int, _P, POINTER(c_int32),
+                                  POINTER(c_int)])
 _sig(hip, "qsim_set_calibrate", [c_int, c_int])
 _sig(hip, "qsim_set_tile_height", [c_int])
 _sig(hip, "qsim_set_tile_rb7", [c_int])

@@ -55,6 +55,13 @@ def set_relabel(mode: int = -1, min_qubits: int = -1) -> None:
     _lib.check(_lib.hip.qsim_set_relabel(mode, min_qubits))
 
 
+def set_relayout(mode: int = -1, min_qubits: int = -1) -> None:
+    """Relayout plans (every pass stores its tile under the next pass's qubit layout) for first
+    runs of states from `min_qubits` on (qsim_set_relayout): mode 0 off, 1 on; negative
+    arguments leave a setting unchanged."""
+    _lib.check(_lib.hip.qsim_set_relayout(mode, min_qubits))
+
+
 def set_calibrate(mode: int = -1, min_qubits: int = -1) -> None:
     """Time the layout model's top candidates on the device at a basis state's first run and
     keep the fastest (qsim_set_calibrate; needs set_jit(2)): mode 0 off, 1 on."""
@@ -82,3 +89,44 @@ def plan_relabel(circuit: Circuit):
     b, a = ctypes.c_double(), ctypes.c_double()
     _lib.check(_lib.hip.qsim_plan_relabel(n, arr, cnt, perm, ctypes.byref(b), ctypes.byref(a)))
     return list(perm), b.value, a.value
+
+
+def plan_exec_host(circuit: Circuit, mode: int = 1, state=None):
+    """Plan the circuit (mode 0: fixed-layout planner under the identity labels, 1: relayout
+    planner) and execute the plan on the host exactly as the staged pass kernels address the
+    state (qsim_plan_exec_host; tests of the planners' index math, no GPU).  Returns
+    (state in logical order, start/end layout, pass count)."""
+    n = circuit.getNumQubits()
+    arr, cnt = circuit.to_abi()
+    if state is None:
+        st = np.zeros(1 << n, np.complex128)
+        st[0] = 1.0
+    else:
+        st = np.array(state, dtype=np.complex128)
+    st = np.ascontiguousarray(st)
+    perm = (ctypes.c_int32 * n)()
+    passes = ctypes.c_int(0)
+    _lib.check(_lib.hip.qsim_plan_exec_host(n, arr, cnt, mode, st.ctypes.data_as(ctypes.c_void_p),
+                                            perm, ctypes.byref(passes)))
+    return st, list(perm), passes.value
+
+
+def plan_relayout(circuit: Circuit):
+    """(perm, passes, predicted_us) of the circuit's relayout plan (qsim_plan_relayout, host
+    only); passes = 0 when no relayout plan exists."""
+    n = circuit.getNumQubits()
+    arr, cnt = circuit.to_abi()
+    perm = (ctypes.c_int32 * n)()
+    passes = ctypes.c_int(0)
+    pred = ctypes.c_double(0.0)
+    _lib.check(_lib.hip.qsim_plan_relayout(n, arr, cnt, perm, ctypes.byref(passes), ctypes.byref(pred)))
+    return list(perm), passes.value, pred.value
+
+
+def jit_build_relayout(circuit: Circuit) -> int:
+    """Compile the circuit's relayout plan (qsim_jit_build_relayout, hipRTC for gfx950, no GPU
+    needed); returns the code-object size in bytes."""
+    arr, cnt = circuit.to_abi()
+    n = ctypes.c_size_t(0)
+    _lib.check(_lib.hip.qsim_jit_build_relayout(circuit.getNumQubits(), arr, cnt, ctypes.byref(n)))
+    return n.value

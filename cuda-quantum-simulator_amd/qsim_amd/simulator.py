@@ -235,7 +235,10 @@ class StateVector:
         timing candidates on the device, whether the qubits are relabeled now."""
         h, c, r = _c.c_int(0), _c.c_int(0), _c.c_int(0)
         _lib.check(_lib.hip.qsim_state_layout_info(self._h, _c.byref(h), _c.byref(c), _c.byref(r)))
-        return {"tile_qubits": 6 + h.value, "calibrated": bool(c.value), "relabeled": bool(r.value)}
+        rl = _c.c_int(0)
+        _lib.check(_lib.hip.qsim_state_relayout(self._h, _c.byref(rl)))
+        return {"tile_qubits": 6 + h.value, "calibrated": bool(c.value), "relabeled": bool(r.value),
+                "relayout": bool(rl.value)}
 
     def restoreLayout(self) -> None:
         """Undo a relabeling now (the SWAP network every index-based reader runs first)."""

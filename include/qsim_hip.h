@@ -164,6 +164,30 @@ int qsim_state_layout_info(qsim_state* s, int* tile_h, int* calibrated, int* rel
 /* Bring a relabeled state back to the identity qubit layout now (the fused SWAP network every
  * index-based reader runs first); a no-op when it is not relabeled. */
 int qsim_state_restore_layout(qsim_state* s);
+/* Whether the state's first fused run chose a relayout plan (no reference counterpart): every
+ * 12-qubit tile pass stores its tile under the next pass's qubit layout, so each pass picks all
+ * of its tile qubits except the four of the contiguous run (fewer passes); the last pass restores
+ * the first layout.  QSIM_RELAYOUT=0 disables them (QSIM_RELAYOUT_MIN_QUBITS, default 22). */
+int qsim_state_relayout(qsim_state* s, int* relayout);
+/* Relayout plans on (mode 1) / off (0) for first runs from now on, for states of at least
+ * min_qubits qubits (relabeling must be enabled too); negative arguments leave a setting. */
+int qsim_set_relayout(int mode, int min_qubits);
+/* Host-only: compile the relayout plan's pass kernels with hipRTC for gfx950 (no GPU needed);
+ * code_bytes: the code object's size.  QSIM_ERR_RUNTIME when there is no relayout plan. */
+int qsim_jit_build_relayout(int n_qubits, const qsim_gate* gates, size_t count, size_t* code_bytes);
+/* Host-only check of the planners' index math (tests; no GPU): plan the circuit (mode 0: the
+ * fixed-layout planner under the identity labels; 1: the relayout planner) and execute the plan
+ * on the host exactly as the staged pass kernels address the state (register stages, LDS slots,
+ * store layouts).  amps: 2^n interleaved re/im in logical qubit order, updated in place.
+ * perm (n entries, may be null): the layout the plan starts and ends in (logical -> physical);
+ * passes: the plan's pass count.  QSIM_ERR_RUNTIME when mode 1 finds no relayout plan. */
+int qsim_plan_exec_host(int n_qubits, const qsim_gate* gates, size_t count, int mode, double* amps,
+                        int32_t* perm, int* passes);
+/* Host-only: the relayout plan of a circuit (what qsim_run would consider): its first/last layout
+ * (perm, n entries, may be null), pass count and predicted time in microseconds (layout model);
+ * *passes = 0 when none exists. */
+int qsim_plan_relayout(int n_qubits, const qsim_gate* gates, size_t count, int32_t* perm, int* passes,
+                       double* predicted_us);
 /* Layout calibration (with QSIM_JIT = 2, from min_qubits; defaults QSIM_RELABEL_CALIBRATE = 1,
  * QSIM_RELABEL_CALIBRATE_MIN_QUBITS = 28): the first run of a basis state times the layout
  * model's choice and two alternatives with their compiled pass kernels (the basis state is
