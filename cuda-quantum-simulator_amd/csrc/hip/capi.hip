@@ -201,9 +201,16 @@ struct qsim_state {
     int tile_h = -1;
     bool calibrated = false;
     bool relayout = false;  // the first-run choice is a relayout plan (relayout.hip)
+    // Relayout passes write out of place: the state alternates between two buffers (d is the
+    // current one; alt_base is allocated on the first relayout run).  pinned: a raw device
+    // pointer was handed out, so the amplitudes are copied back to it after such a run.
+    void* alt_base = nullptr;
+    double2* alt = nullptr;
+    bool pinned = false;
     ~qsim_state() {
         if (stream) (void)hipStreamSynchronize(stream);
         if (base) (void)hipFree(base);
+        if (alt_base) (void)hipFree(alt_base);
         if (d_partials) (void)hipFree(d_partials);
         if (d_result) (void)hipFree(d_result);
         if (stream) (void)hipStreamDestroy(stream);
@@ -226,6 +233,30 @@ static void check_state(const qsim_state* s) {
     if (!s) fail(QSIM_ERR_INVALID_ARGUMENT, "null state handle");
 }
 
+// One fused plan on the state: relayout passes alternate between the state's two buffers.
+static void launch_plan(qsim_state* s, const Plan& plan, Timer* tm, const JitModule* jm) {
+    FusedRange range;
+    bool relayout = false;
+    for (const FusedPass& p : plan.passes) relayout = relayout || p.relayout;
+    if (relayout) {
+        if (!s->alt) {
+            QSIM_HIPCHK(hipStreamSynchronize(s->stream));
+            QSIM_HIPCHK(hipMalloc(&s->alt_base, sizeof(double2) << s->n));
+            s->alt = reinterpret_cast<double2*>(s->alt_base);
+        }
+        range.alt = s->alt;
+    }
+    double2* r = launch_fused(s->d, s->n, 1, plan, (const TileOp*)s->ops.ptr, (const Stage*)s->stages.ptr,
+                              s->stream, tm, jm, nullptr, range);
+    if (r == s->d) return;
+    if (s->pinned) {  // keep the amplitudes where the handed-out pointer points
+        QSIM_HIPCHK(hipMemcpyAsync(s->d, r, sizeof(double2) << s->n, hipMemcpyDeviceToDevice, s->stream));
+        return;
+    }
+    s->alt = s->d;
+    s->d = r;
+}
+
 // jit = false: the pass interpreter only (a one-off network — the layout restore — would wait
 // longer for its compile than its passes take).
 static void run_fused(qsim_state* s, const std::vector<Op>& ops, bool jit = true) {
@@ -234,8 +265,7 @@ static void run_fused(qsim_state* s, const std::vector<Op>& ops, bool jit = true
     const JitModule* jm = jit ? jit_for(pe.jit, plan, s->n) : nullptr;
     s->ops.upload(plan.ops.data(), plan.ops.size() * sizeof(TileOp), s->stream);
     s->stages.upload(plan.stages.data(), plan.stages.size() * sizeof(Stage), s->stream);
-    launch_fused(s->d, s->n, 1, plan, (const TileOp*)s->ops.ptr, (const Stage*)s->stages.ptr,
-                 s->stream, &s->timer, jm);
+    launch_plan(s, plan, &s->timer, jm);
     s->last_passes = (int)plan.passes.size();
     s->last_jit_passes = 0;
     if (jm)
@@ -307,8 +337,7 @@ static size_t calibrate_candidates(qsim_state* s, std::vector<LayoutCandidate>& 
             float ms = 3.0e38f;
             for (int rep = 0; rep < 2; ++rep) {
                 QSIM_HIPCHK(hipEventRecord(e0, s->stream));
-                launch_fused(s->d, s->n, 1, pe.plan, (const TileOp*)s->ops.ptr, (const Stage*)s->stages.ptr,
-                             s->stream, nullptr, jm);
+                launch_plan(s, pe.plan, nullptr, jm);
                 QSIM_HIPCHK(hipEventRecord(e1, s->stream));
                 QSIM_HIPCHK(hipEventSynchronize(e1));
                 float t = 0.0f;
@@ -438,6 +467,7 @@ static void choose_first_layout(qsim_state* s, const qsim_gate* gates, size_t co
             }
         });
     const bool timing = relabel_calibrate(n);
+    const bool force_rc = relayout_forced();  // (tests: QSIM_RELAYOUT=2 / qsim_set_relayout(2))
     auto take_relayout = [&]() {
         {
             const TileHeightScope scope(6, tile_rb_for(n, 6));
@@ -451,8 +481,12 @@ static void choose_first_layout(qsim_state* s, const qsim_gate* gates, size_t co
     for (const Gen& g : gens) {
         const TileHeightScope scope(g.h, tile_rb_for(n, g.h));
         const LayoutT13Scope t13(g.t13);
-        LayoutChoice lc = choose_layout(n, lower_under, relabel_tries(), g.alts);
         rc_worker.join();
+        if (have_rc && force_rc) {
+            take_relayout();
+            return;
+        }
+        LayoutChoice lc = choose_layout(n, lower_under, relabel_tries(), g.alts);
         if (lc.perm.empty()) {  // the identity is this height's choice
             if (!heights && !(have_rc && timing)) {  // (nothing to time)
                 if (have_rc && rc.plan.passes.size() < lc.passes_before) {
@@ -654,6 +688,7 @@ int qsim_state_device_ptr(qsim_state* s, void** dptr) {
         check_state(s);
         DeviceGuard dg(s->device);
         prep(s, true);  // the caller may read or write through the pointer
+        s->pinned = true;  // (relayout runs copy their result back to this buffer)
         *dptr = s->d;
     });
 }

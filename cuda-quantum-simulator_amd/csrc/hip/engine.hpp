@@ -202,6 +202,7 @@ bool plan_relayout(int n, const std::function<std::vector<Op>(const std::vector<
                    size_t max_passes, RelayoutChoice& out);
 bool relayout_enabled(int n);  // QSIM_RELAYOUT (default 1), QSIM_RELAYOUT_MIN_QUBITS (default 22)
 void relayout_configure(int mode, int min_qubits);  // qsim_set_relayout; < 0 leaves a setting
+bool relayout_forced();  // mode 2: a relayout plan whenever one exists (tests)
 int tile_height_default();             // the h that hmax < 0 means (scope, setting, env, 6)
 int tile_height_for(int n);            // a single-GPU state's height (the setting, or by size)
 bool tile_height_is_set();             // qsim_set_tile_height or QSIM_TILE_HMAX in force
@@ -318,9 +319,14 @@ struct PlanCache {
 struct FusedRange {
     size_t first = 0, last = SIZE_MAX;
     uint64_t fix_mask = 0, fix_val = 0;
+    // relayout passes write out of place (a tile's store addresses are other tiles' load
+    // addresses): they alternate between the state and `alt` (same size)
+    double2* alt = nullptr;
 };
 // frames != null: batched noisy run under per-trajectory Pauli frames (FArgs::frames).
-void launch_fused(double2* st, int n, uint64_t batch, const Plan& plan, const TileOp* d_ops,
+// Returns the buffer that holds the result (st, or range.alt after an odd number of relayout
+// passes).
+double2* launch_fused(double2* st, int n, uint64_t batch, const Plan& plan, const TileOp* d_ops,
                   const Stage* d_stages, hipStream_t s, Timer* tm, const JitModule* jm = nullptr,
                   const uint64_t* frames = nullptr, const FusedRange& range = FusedRange());
 

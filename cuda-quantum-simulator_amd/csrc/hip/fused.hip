@@ -864,7 +864,9 @@ struct FArgs {
     // Sub-space launch (sharded engine's overlapped remaps): tiles skip the fix_mask positions,
     // which read fix_val; zmask = fix_mask | the tile's own positions above the run.
     uint64_t fix_mask, fix_val, zmask;
-    // Relayout pass (FusedPass::relayout): store positions of tile bits and tile-id bits.
+    // Relayout pass (FusedPass::relayout): the tile is stored to dst (out of place) at the store
+    // positions of its tile bits and tile-id bits.
+    double2* dst;
     int relayout, n_tid;
     int st_pos[13];
     int st_tid[32];
@@ -1313,9 +1315,10 @@ __global__ __launch_bounds__((64 << H) >> RBT, H >= 7 ? 1 : 2) void k_fused_stag
                 gb = base | (jb & run_mask) | spread_n(jb >> r0, a.hpos, nh);
             }
             const double sc = a.scale;
+            double2* const out = a.relayout ? a.dst : a.st;
 #pragma unroll
             for (int r = 0; r < R; ++r)
-                st<NT>(a.st + (gb | sg.goff[r]), make_double2(v[r].x * sc, v[r].y * sc));
+                st<NT>(out + (gb | sg.goff[r]), make_double2(v[r].x * sc, v[r].y * sc));
         } else {
 #pragma unroll
             for (int r = 0; r < R; ++r) *reinterpret_cast<double2*>(lds + (lbw ^ sg.lds_w[r])) = v[r];
@@ -1349,14 +1352,17 @@ static uint64_t pipe_workgroups(int h) {
     return (uint64_t)cus * (uint64_t)(per > 0 ? per : (h >= 7 ? 1 : 2));
 }
 
-void launch_fused(double2* st, int n, uint64_t batch, const Plan& plan, const TileOp* d_ops,
-                  const Stage* d_stages, hipStream_t s, Timer* tm, const JitModule* jm,
-                  const uint64_t* frames, const FusedRange& range) {
+double2* launch_fused(double2* st, int n, uint64_t batch, const Plan& plan, const TileOp* d_ops,
+                      const Stage* d_stages, hipStream_t s, Timer* tm, const JitModule* jm,
+                      const uint64_t* frames, const FusedRange& range) {
+    double2* const home = st;
     const int nfix = __builtin_popcountll(range.fix_mask);
     const double pass_bytes = 32.0 * std::ldexp((double)(1ull << n), -nfix) * (double)batch;
     const bool nt = fused_nt();
     const size_t last = std::min(range.last, plan.passes.size());
+    double2* next_st = st;  // where the next pass reads (a relayout pass's dst)
     for (size_t pidx = range.first; pidx < last; ++pidx) {
+        st = next_st;
         const FusedPass& p = plan.passes[pidx];
         if (range.fix_mask && (p.single >= 0 || p.h < 4 || frames))
             fail(QSIM_ERR_RUNTIME, "sub-space launch needs staged tile passes");
@@ -1389,7 +1395,10 @@ void launch_fused(double2* st, int n, uint64_t batch, const Plan& plan, const Ti
             if (range.fix_mask || frames || p.h < 4 || p.stage_end - p.stage_begin < 2)
                 fail(QSIM_ERR_RUNTIME, "relayout pass outside a whole-state staged run");
             if (n - 6 - p.h != p.n_tid || p.n_tid > 32) fail(QSIM_ERR_RUNTIME, "relayout pass planned for another size");
+            if (!range.alt || batch != 1) fail(QSIM_ERR_RUNTIME, "relayout pass without a second buffer");
             a.relayout = 1;
+            a.dst = st == home ? range.alt : home;
+            next_st = a.dst;
             a.n_tid = p.n_tid;
             for (int i = 0; i < 13; ++i) a.st_pos[i] = p.st_pos[i];
             for (int i = 0; i < 32; ++i) a.st_tid[i] = p.st_tid[i];
@@ -1429,7 +1438,7 @@ void launch_fused(double2* st, int n, uint64_t batch, const Plan& plan, const Ti
         if (jm && pi < jm->fn.size() && jm->fn[pi]) {  // circuit-specialised kernel (jit.hip)
             unsigned long long stride = a.stride, tpt = a.tpt_mask, zm = a.zmask, fv = a.fix_val, ntiles = blocks;
             int lt_arg = lt;
-            void* args[] = {&a.st, &stride, &tpt, &lt_arg, &zm, &fv, &ntiles};
+            void* args[] = {&a.st, &stride, &tpt, &lt_arg, &zm, &fv, &ntiles, &a.dst};  // (dst: relayout kernels)
             const unsigned nthr = (unsigned)((64 << p.h) >> p.rb);
             // a pipelined (persistent) kernel gets the resident workgroups only and walks its tiles
             const uint64_t grid = jit_pass_pipelined(p) ? std::min<uint64_t>(blocks, pipe_workgroups(p.h)) : blocks;
@@ -1479,6 +1488,7 @@ void launch_fused(double2* st, int n, uint64_t batch, const Plan& plan, const Ti
         }
         QSIM_HIPCHK(hipGetLastError());
     }
+    return next_st;
 }
 
 }  // namespace qsim_hip

@@ -309,7 +309,8 @@ void gen_pass(std::ostringstream& out, const Plan& plan, const FusedPass& p, int
     o << "extern \"C\" __global__ void __launch_bounds__(" << (T >> RB) << ", " << (H >= 7 ? 1 : 2)
       << ")\nqk" << idx
       << "(double2* __restrict__ st, unsigned long long stride, unsigned long long tpt_mask, int log_tpt,"
-         " unsigned long long zmask, unsigned long long fix_val, unsigned long long ntiles) {\n"
+         " unsigned long long zmask, unsigned long long fix_val, unsigned long long ntiles"
+      << (p.relayout ? ", double2* __restrict__ dst" : "") << ") {\n"
       << "  __shared__ double2 tile[" << T << "];\n"
       << "  char* const lds = reinterpret_cast<char*>(tile);\n"
       << "  const unsigned tid = threadIdx.x;\n";
@@ -394,7 +395,7 @@ void gen_pass(std::ostringstream& out, const Plan& plan, const FusedPass& p, int
                 for (int r = 0; r < R; ++r) {
                     std::string val = g.v(r);
                     if (sc != 1.0) val = "make_double2(" + val + ".x * " + lit(sc) + ", " + val + ".y * " + lit(sc) + ")";
-                    o << "  qst(st + (gb | " << hexu(st.goff[r]) << "), " << val << ");\n";
+                    o << "  qst(" << (p.relayout ? "dst" : "st") << " + (gb | " << hexu(st.goff[r]) << "), " << val << ");\n";
                 }
             } else {
                 for (int r = 0; r < R; ++r)

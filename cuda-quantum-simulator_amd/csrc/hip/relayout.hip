@@ -290,6 +290,7 @@ bool relayout_enabled(int n) {
     if (g_relayout_min.load() < 0) g_relayout_min.store(env_int("QSIM_RELAYOUT_MIN_QUBITS", 22));
     return g_relayout.load() != 0 && n >= g_relayout_min.load() && n - kTile <= 32;
 }
+bool relayout_forced() { return g_relayout.load() == 2; }
 void relayout_configure(int mode, int min_qubits) {
     relayout_enabled(0);  // defaults first
     if (mode >= 0) g_relayout.store(mode);

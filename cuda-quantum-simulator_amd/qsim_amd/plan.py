@@ -57,8 +57,9 @@ def set_relabel(mode: int = -1, min_qubits: int = -1) -> None:
 
 def set_relayout(mode: int = -1, min_qubits: int = -1) -> None:
     """Relayout plans (every pass stores its tile under the next pass's qubit layout) for first
-    runs of states from `min_qubits` on (qsim_set_relayout): mode 0 off, 1 on; negative
-    arguments leave a setting unchanged."""
+    runs of states from `min_qubits` on (qsim_set_relayout): mode 0 off, 1 on (when they need
+    fewer passes or win the device timing), 2 forced (tests); negative arguments leave a setting
+    unchanged."""
     _lib.check(_lib.hip.qsim_set_relayout(mode, min_qubits))
 
 

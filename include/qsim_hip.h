@@ -169,8 +169,10 @@ int qsim_state_restore_layout(qsim_state* s);
  * of its tile qubits except the four of the contiguous run (fewer passes); the last pass restores
  * the first layout.  QSIM_RELAYOUT=0 disables them (QSIM_RELAYOUT_MIN_QUBITS, default 22). */
 int qsim_state_relayout(qsim_state* s, int* relayout);
-/* Relayout plans on (mode 1) / off (0) for first runs from now on, for states of at least
- * min_qubits qubits (relabeling must be enabled too); negative arguments leave a setting. */
+/* Relayout plans on (mode 1: when they need fewer passes, or win the device timing with
+ * calibration) / off (0) / forced (2: whenever one exists — tests) for first runs from now on, for
+ * states of at least min_qubits qubits (relabeling must be enabled too); negative arguments leave
+ * a setting unchanged. */
 int qsim_set_relayout(int mode, int min_qubits);
 /* Host-only: compile the relayout plan's pass kernels with hipRTC for gfx950 (no GPU needed);
  * code_bytes: the code object's size.  QSIM_ERR_RUNTIME when there is no relayout plan. */

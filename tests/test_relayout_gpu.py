@@ -20,7 +20,7 @@ def _err(a, b):
 def relayout_low():
     from qsim_amd.plan import set_calibrate, set_jit, set_relabel, set_relayout
     set_relabel(1, 14)
-    set_relayout(1, 22)
+    set_relayout(2, 22)  # forced: a relayout plan whenever one exists
     set_calibrate(0, -1)
     yield
     set_relabel(1, 26)
@@ -58,16 +58,16 @@ def test_relayout_all_gate_types(qsim, oracle, gpu_ready, relayout_low):
         relayout = sim.state.layoutInfo()["relayout"]
         np.testing.assert_allclose(sim.getProbabilities(), np.abs(ref) ** 2, atol=1e-12, rtol=0)
         assert _err(sim.getStateVector(), ref) < 1e-12
-        if jit == 0:
-            assert relayout  # (fewer passes than the fixed-layout plan for this circuit)
+        assert relayout
 
 
 def test_relayout_calibrated_choice_matches_oracle(qsim, oracle, gpu_ready, relayout_low):
     """With inline compilation and calibration on (the bench's mode) the relayout plan is timed
     against the fixed-layout candidates; whichever wins, forward + inverse returns to |0>."""
-    from qsim_amd.plan import set_calibrate, set_jit
+    from qsim_amd.plan import set_calibrate, set_jit, set_relayout
     set_jit(2, 20)
     set_calibrate(1, 22)
+    set_relayout(1, 22)  # a candidate among the timed ones
     n = 24
     c = qsim.createRandomHCCircuit(n, 100, 42)
     inv = qsim.Circuit(n)
