@@ -403,10 +403,13 @@ static void choose_first_layout(qsim_state* s, const qsim_gate* gates, size_t co
         layout_memo_put(n, 0, gates, bytes, perm, heights ? s->tile_h : -1);
     };
     const bool relayout = relayout_enabled(n) && !tile_height_is_set();
+    const bool timing = relabel_calibrate(n);
     {
+        // a relayout choice made before for this circuit (by timing, or by pass count when
+        // candidates are not timed: memoised apart)
         std::vector<int> memo;
         int mh = -1;
-        if (relayout && layout_memo_get(n, 2, gates, bytes, memo, &mh)) {  // a relayout choice
+        if (relayout && layout_memo_get(n, 2, gates, bytes, memo, timing ? &mh : nullptr)) {
             RelayoutChoice rc;
             if (plan_relayout(n, lower_under, SIZE_MAX, rc) && rc.perm == memo) {
                 const TileHeightScope scope(6, tile_rb_for(n, 6));
@@ -414,6 +417,7 @@ static void choose_first_layout(qsim_state* s, const qsim_gate* gates, size_t co
                 s->perm = memo;
                 s->tile_h = 6;
                 s->relayout = true;
+                s->calibrated = timing;
                 return;
             }
         }
@@ -425,6 +429,7 @@ static void choose_first_layout(qsim_state* s, const qsim_gate* gates, size_t co
         if (layout_memo_get(n, 0, gates, bytes, memo, heights ? &mh : nullptr)) {
             s->perm = memo;  // decided before for this circuit (its plan: the plan cache)
             if (heights) s->tile_h = mh;
+            s->calibrated = heights;  // (a cross-height decision is always a timed one)
             return;
         }
     }
@@ -466,7 +471,6 @@ static void choose_first_layout(qsim_state* s, const qsim_gate* gates, size_t co
                 have_rc = false;  // (no relayout candidate)
             }
         });
-    const bool timing = relabel_calibrate(n);
     const bool force_rc = relayout_forced();  // (tests: QSIM_RELAYOUT=2 / qsim_set_relayout(2))
     auto take_relayout = [&]() {
         {
@@ -476,7 +480,7 @@ static void choose_first_layout(qsim_state* s, const qsim_gate* gates, size_t co
         s->perm = rc.perm;
         s->tile_h = 6;
         s->relayout = true;
-        layout_memo_put(n, 2, gates, bytes, s->perm, 6);
+        layout_memo_put(n, 2, gates, bytes, s->perm, timing ? 6 : -1);
     };
     for (const Gen& g : gens) {
         const TileHeightScope scope(g.h, tile_rb_for(n, g.h));
