@@ -278,6 +278,22 @@ static void run_fused(qsim_state* s, const std::vector<Op>& ops, bool jit = true
 static void canonicalize(qsim_state* s) {
     if (s->perm.empty()) return;
     const int n = s->n;
+    // One gate-free relayout pass (relayout.hip) from 16 qubits: every amplitude stored at its
+    // identity-layout position in a single HBM round trip (QSIM_RESTORE_ONE_PASS=0: the SWAP
+    // network below, a few passes).
+    static const bool one_pass = [] {
+        const char* e = std::getenv("QSIM_RESTORE_ONE_PASS");
+        return e == nullptr || std::atoi(e) != 0;
+    }();
+    if (one_pass && n >= 16 && n - 12 <= 32) {
+        const Plan plan = plan_permutation_pass(n, s->perm);
+        s->stages.upload(plan.stages.data(), plan.stages.size() * sizeof(Stage), s->stream);
+        launch_plan(s, plan, &s->timer, nullptr);
+        s->last_passes = 1;
+        s->last_jit_passes = 0;
+        s->perm.clear();
+        return;
+    }
     std::vector<int> p = s->perm, inv(n);
     for (int q = 0; q < n; ++q) inv[p[q]] = q;
     std::vector<Op> swaps;

@@ -202,6 +202,8 @@ bool plan_relayout(int n, const std::function<std::vector<Op>(const std::vector<
                    size_t max_passes, RelayoutChoice& out);
 bool relayout_enabled(int n);  // QSIM_RELAYOUT (default 1), QSIM_RELAYOUT_MIN_QUBITS (default 22)
 void relayout_configure(int mode, int min_qubits);  // qsim_set_relayout; < 0 leaves a setting
+// A single gate-free relayout pass taking logical qubit q from physical perm[q] to q (n >= 12).
+Plan plan_permutation_pass(int n, const std::vector<int>& perm);
 bool relayout_forced();  // mode 2: a relayout plan whenever one exists (tests)
 int tile_height_default();             // the h that hmax < 0 means (scope, setting, env, 6)
 int tile_height_for(int n);            // a single-GPU state's height (the setting, or by size)

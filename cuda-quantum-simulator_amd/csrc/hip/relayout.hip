@@ -385,6 +385,35 @@ bool plan_relayout(int n, const std::function<std::vector<Op>(const std::vector<
     return true;
 }
 
+// One gate-free relayout pass that moves logical qubit q from physical position perm[q] to q
+// (the identity-layout restore before index-based readers: one pass instead of a SWAP network of
+// several).  Tile: physical 0..5 (the load runs) and the positions of logical 0..5 (the store
+// runs), padded; every tile bit and tile-id bit is stored at its logical position.
+Plan plan_permutation_pass(int n, const std::vector<int>& perm) {
+    if (n < kTile || n - kTile > 32 || (int)perm.size() != n) fail(QSIM_ERR_RUNTIME, "permutation pass out of range");
+    std::vector<int> inv(n);
+    for (int q = 0; q < n; ++q) inv[perm[q]] = q;
+    uint64_t tile = 0;  // physical positions
+    for (int q = 0; q < 6; ++q) tile |= (1ull << q) | (1ull << perm[q]);
+    for (int p = 6; p < n && __builtin_popcountll(tile) < kTile; ++p) tile |= 1ull << p;
+    const int r0 = 6;  // (physical 0..5 are tile positions)
+    int hpos[kHposMax] = {0}, bit_of[64] = {0}, st_pos[13] = {0}, st_tid[32] = {0};
+    int x = 0, i = 0;
+    for (int p = 0; p < n; ++p) {
+        if ((tile >> p) & 1ull) {
+            if (x >= r0) hpos[x - r0] = p;
+            bit_of[p] = x;
+            st_pos[x++] = inv[p];
+        } else {
+            st_tid[i++] = inv[p];
+        }
+    }
+    Plan plan;
+    const TileHeightScope scope(6);
+    append_tile_pass(plan, {}, n, 6, r0, hpos, bit_of, st_pos, st_tid);
+    return plan;
+}
+
 // ---------------------------------------------------------------------------------------
 // Host execution of a plan (tests: qsim_plan_exec_host).  Every staged pass is run tile by
 // tile exactly as k_fused_staged / the generated kernels address it — first-stage HBM offsets,
@@ -531,6 +560,24 @@ extern "C" int qsim_plan_exec_host(int n_qubits, const qsim_gate* gates, size_t 
         std::vector<int> pi(n);
         for (int q = 0; q < n; ++q) pi[q] = q;
         Plan plan;
+        if (mode == 2) {  // the one-pass identity restore from layout `perm` (amps: physical order)
+            if (!perm) fail(QSIM_ERR_INVALID_ARGUMENT, "null perm");
+            std::vector<int> from(perm, perm + n), chk(from);
+            std::sort(chk.begin(), chk.end());
+            for (int q = 0; q < n; ++q)
+                if (chk[q] != q) fail(QSIM_ERR_INVALID_ARGUMENT, "perm is not a permutation");
+            plan = plan_permutation_pass(n, from);
+            const uint64_t N = 1ull << n;
+            std::vector<std::complex<double>> st(N);
+            for (uint64_t i = 0; i < N; ++i) st[i] = std::complex<double>(amps[2 * i], amps[2 * i + 1]);
+            exec_plan_host(plan, n, st);
+            for (uint64_t i = 0; i < N; ++i) {
+                amps[2 * i] = st[i].real();
+                amps[2 * i + 1] = st[i].imag();
+            }
+            if (passes) *passes = (int)plan.passes.size();
+            return QSIM_OK;
+        }
         if (mode == 1) {
             RelayoutChoice rc;
             if (!plan_relayout(n, lower, SIZE_MAX, rc)) fail(QSIM_ERR_RUNTIME, "no relayout plan");

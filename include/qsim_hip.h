@@ -182,7 +182,9 @@ int qsim_jit_build_relayout(int n_qubits, const qsim_gate* gates, size_t count, 
  * on the host exactly as the staged pass kernels address the state (register stages, LDS slots,
  * store layouts).  amps: 2^n interleaved re/im in logical qubit order, updated in place.
  * perm (n entries, may be null): the layout the plan starts and ends in (logical -> physical);
- * passes: the plan's pass count.  QSIM_ERR_RUNTIME when mode 1 finds no relayout plan. */
+ * passes: the plan's pass count.  QSIM_ERR_RUNTIME when mode 1 finds no relayout plan.
+ * mode 2: the one-pass identity-layout restore instead (gates unused): amps holds the state in
+ * the physical order of layout perm (input), and is returned in logical order. */
 int qsim_plan_exec_host(int n_qubits, const qsim_gate* gates, size_t count, int mode, double* amps,
                         int32_t* perm, int* passes);
 /* Host-only: the relayout plan of a circuit (what qsim_run would consider): its first/last layout

@@ -61,3 +61,27 @@ def test_relayout_needs_fewer_passes_at_30_qubits(qsim, seed):
 def test_relayout_kernels_compile_for_gfx950(qsim):
     from qsim_amd.plan import jit_build_relayout
     assert jit_build_relayout(qsim.createRandomHCCircuit(30, 100, 42)) > 0
+
+
+@pytest.mark.parametrize("n,seed", [(16, 1), (20, 2)])
+def test_one_pass_identity_restore(qsim, n, seed):
+    """The identity-layout restore before index-based readers is one gate-free relayout pass
+    (capi.hip canonicalize): every amplitude lands at its logical index."""
+    import ctypes
+    from qsim_amd import _lib
+    rng = np.random.default_rng(seed)
+    perm = rng.permutation(n).astype(np.int32)
+    psi = rng.normal(size=1 << n) + 1j * rng.normal(size=1 << n)
+    idx = np.arange(1 << n, dtype=np.int64)
+    phys = np.zeros_like(idx)
+    for q in range(n):
+        phys |= ((idx >> q) & 1) << int(perm[q])
+    st = np.zeros(1 << n, np.complex128)
+    st[phys] = psi
+    p = (ctypes.c_int32 * n)(*perm.tolist())
+    passes = ctypes.c_int(0)
+    arr, cnt = qsim.Circuit(n).to_abi()
+    _lib.check(_lib.hip.qsim_plan_exec_host(n, arr, 0, 2, st.ctypes.data_as(ctypes.c_void_p), p,
+                                            ctypes.byref(passes)))
+    assert passes.value == 1
+    assert np.array_equal(st, psi)
