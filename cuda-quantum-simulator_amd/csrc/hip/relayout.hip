@@ -25,6 +25,7 @@
 #include <atomic>
 #include <cmath>
 #include <complex>
+#include <cstdio>
 #include <cstdint>
 #include <cstdlib>
 #include <random>
@@ -208,33 +209,59 @@ std::vector<int> assign_layout(int n, uint64_t run, uint64_t x, uint64_t y) {
     std::vector<int> L(n, -1);
     int k = 0;
     for (uint64_t m = run; m; m &= m - 1) L[__builtin_ctzll(m)] = k++;
-    const uint64_t s = (x | y) & ~run;
     std::vector<int> sq;
-    for (uint64_t m = s; m; m &= m - 1) sq.push_back(__builtin_ctzll(m));
-    const int npos = n - kRun;  // positions kRun..n-1
-    std::vector<int> at(npos, -1);  // qubit at position kRun + i (-1: another qubit)
+    // QSIM_RELAYOUT_RUN6=1: positions 4 and 5 go to tile qubits first (shared ones, then the
+    // loading tile's), so loads and stores move whole 1 KiB runs where the tiles allow
+    // (2: the storing tile's qubits instead, so the stores move whole runs)
+    static const int run6 = env_int("QSIM_RELAYOUT_RUN6", 0);
+    int first = kRun;
+    if (run6) {
+        const uint64_t pref[2] = {x & y & ~run, (run6 == 2 ? x : y) & ~run};
+        for (int p = kRun; p < 6; ++p)
+            for (uint64_t c : pref) {
+                uint64_t m = c;
+                for (int q = 0; q < n; ++q)
+                    if (L[q] >= 0) m &= ~(1ull << q);
+                if (!m) continue;
+                L[__builtin_ctzll(m)] = p;
+                first = p + 1;
+                break;
+            }
+    }
+    uint64_t placed = run;
+    for (int q = 0; q < n; ++q)
+        if (L[q] >= 0) placed |= 1ull << q;
+    (void)placed;
+    const int npos = n - first;  // positions first..n-1
+    for (uint64_t m = (x | y) & ~placed; m; m &= m - 1) sq.push_back(__builtin_ctzll(m));
+    uint64_t fixed_x = 0, fixed_y = 0;  // positions already taken by x / y qubits
+    for (int q = 0; q < n; ++q)
+        if (L[q] >= 0) {
+            if ((x >> q) & 1ull) fixed_x |= 1ull << L[q];
+            if ((y >> q) & 1ull) fixed_y |= 1ull << L[q];
+        }
     auto cost = [&](const std::vector<int>& pos_of) {
-        uint64_t mx = 0, my = 0;
+        uint64_t mx = fixed_x, my = fixed_y;
         for (size_t i = 0; i < sq.size(); ++i) {
             const uint64_t b = 1ull << sq[i];
             if (x & b) mx |= 1ull << pos_of[i];
             if (y & b) my |= 1ull << pos_of[i];
         }
-        return layout_cost_us(mx | ((1ull << kRun) - 1ull)) + layout_cost_us(my | ((1ull << kRun) - 1ull));
+        return layout_cost_us(mx) + layout_cost_us(my);
     };
     std::vector<int> best_pos;
     double best = 1e300;
     for (int restart = 0; restart < 4; ++restart) {
         std::mt19937 rng(0x7e1a0u + (unsigned)restart);
         std::vector<int> slots(npos);
-        for (int i = 0; i < npos; ++i) slots[i] = kRun + i;
+        for (int i = 0; i < npos; ++i) slots[i] = first + i;
         if (restart > 0) std::shuffle(slots.begin(), slots.end(), rng);
         // sq[i] at slots[i]; slots beyond sq.size() are free
         std::vector<int> pos_of(slots.begin(), slots.begin() + sq.size());
         double cur = cost(pos_of);
         std::uniform_int_distribution<int> pick_q(0, (int)sq.size() - 1), pick_p(0, npos - 1);
         for (int it = 0; it < 3000; ++it) {
-            const int a = pick_q(rng), pb = kRun + pick_p(rng);
+            const int a = pick_q(rng), pb = first + pick_p(rng);
             int b = -1;  // the qubit of sq at position pb, if any
             for (size_t i = 0; i < sq.size(); ++i)
                 if (pos_of[i] == pb) b = (int)i;
@@ -256,7 +283,8 @@ std::vector<int> assign_layout(int n, uint64_t run, uint64_t x, uint64_t y) {
         }
     }
     std::vector<char> used(n, 0);
-    for (int p = 0; p < kRun; ++p) used[p] = 1;
+    for (int q = 0; q < n; ++q)
+        if (L[q] >= 0) used[L[q]] = 1;
     for (size_t i = 0; i < sq.size(); ++i) {
         L[sq[i]] = best_pos[i];
         used[best_pos[i]] = 1;
@@ -287,7 +315,7 @@ uint64_t choose_run(uint64_t pool, const int* uses) {
 static std::atomic<int> g_relayout{-1}, g_relayout_min{-1};
 bool relayout_enabled(int n) {
     if (g_relayout.load() < 0) g_relayout.store(env_int("QSIM_RELAYOUT", 1));
-    if (g_relayout_min.load() < 0) g_relayout_min.store(env_int("QSIM_RELAYOUT_MIN_QUBITS", 22));
+    if (g_relayout_min.load() < 0) g_relayout_min.store(env_int("QSIM_RELAYOUT_MIN_QUBITS", 20));
     return g_relayout.load() != 0 && n >= g_relayout_min.load() && n - kTile <= 32;
 }
 bool relayout_forced() { return g_relayout.load() == 2; }
@@ -379,6 +407,16 @@ bool plan_relayout(int n, const std::function<std::vector<Op>(const std::vector<
             mst |= 1ull << sl[q];
         }
         cost += 0.5 * (layout_cost_us(mld) + layout_cost_us(mst));
+        static const bool dbg = std::getenv("QSIM_RELAYOUT_DEBUG") != nullptr;
+        if (dbg) {
+            std::fprintf(stderr, "[relayout] pass %zu: %zu gates, r0 %d, load", k, ran[k].size(), r0);
+            for (int b = 0; b < n; ++b)
+                if ((mld >> b) & 1ull) std::fprintf(stderr, " %d", b);
+            std::fprintf(stderr, " | store");
+            for (int b = 0; b < n; ++b)
+                if ((mst >> b) & 1ull) std::fprintf(stderr, " %d", b);
+            std::fprintf(stderr, " | model %.0f / %.0f us\n", layout_cost_us(mld), layout_cost_us(mst));
+        }
     }
     out.plan = std::move(plan);
     out.cost_us = cost;

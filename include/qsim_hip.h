@@ -167,7 +167,7 @@ int qsim_state_restore_layout(qsim_state* s);
 /* Whether the state's first fused run chose a relayout plan (no reference counterpart): every
  * 12-qubit tile pass stores its tile under the next pass's qubit layout, so each pass picks all
  * of its tile qubits except the four of the contiguous run (fewer passes); the last pass restores
- * the first layout.  QSIM_RELAYOUT=0 disables them (QSIM_RELAYOUT_MIN_QUBITS, default 22). */
+ * the first layout.  QSIM_RELAYOUT=0 disables them (QSIM_RELAYOUT_MIN_QUBITS, default 20). */
 int qsim_state_relayout(qsim_state* s, int* relayout);
 /* Relayout plans on (mode 1: when they need fewer passes, or win the device timing with
  * calibration) / off (0) / forced (2: whenever one exists — tests) for first runs from now on, for
