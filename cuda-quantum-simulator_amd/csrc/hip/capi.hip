@@ -425,8 +425,10 @@ static void choose_first_layout(qsim_state* s, const qsim_gate* gates, size_t co
         int mh = -1;
         if (relayout && layout_memo_get(n, 2, gates, bytes, memo, timing ? &mh : nullptr)) {
             if (memo.empty()) return;  // (decided: no relayout plan, and no relabeling below)
-            RelayoutChoice rc;
-            if (plan_relayout(n, lower_under, SIZE_MAX, rc) && rc.perm == memo) {
+            std::vector<RelayoutChoice> vs;
+            plan_relayout_variants(n, lower_under, SIZE_MAX, vs);
+            for (RelayoutChoice& rc : vs) {
+                if (rc.perm != memo) continue;
                 const TileHeightScope scope(6, tile_rb_for(n, 6));
                 s->plans.put(rc.ops, n, std::move(rc.plan), s->stream);
                 s->perm = memo;
@@ -468,7 +470,8 @@ static void choose_first_layout(qsim_state* s, const qsim_gate* gates, size_t co
     // candidate like the others when candidates are timed, else taken when it needs fewer passes
     // than the fixed-layout choice.
     // (planned on a worker thread while the fixed-layout candidates are chosen)
-    RelayoutChoice rc;
+    RelayoutChoice rc;  // the best predicted variant (timing compares all of rcs)
+    std::vector<RelayoutChoice> rcs;
     bool have_rc = false;
     struct Joiner {
         std::thread t;
@@ -481,7 +484,8 @@ static void choose_first_layout(qsim_state* s, const qsim_gate* gates, size_t co
         rc_worker.t = std::thread([&] {
             try {
                 const TileHeightScope scope(6, tile_rb_for(n, 6));
-                have_rc = plan_relayout(n, lower_under, SIZE_MAX, rc);
+                have_rc = plan_relayout_variants(n, lower_under, SIZE_MAX, rcs) > 0;
+                if (have_rc) rc = rcs.front();
             } catch (...) {
                 have_rc = false;  // (no relayout candidate)
             }
@@ -540,7 +544,7 @@ static void choose_first_layout(qsim_state* s, const qsim_gate* gates, size_t co
     }
     if (have_rc) {
         if (timing) {
-            add(6, rc.perm, rc.ops, rc.plan, true);
+            for (const RelayoutChoice& v : rcs) add(6, v.perm, v.ops, v.plan, true);
         } else if (rc.plan.passes.size() < cands[0].plan.passes.size()) {
             take_relayout();
             return;
@@ -555,8 +559,10 @@ static void choose_first_layout(qsim_state* s, const qsim_gate* gates, size_t co
     }
     LayoutCandidate& w = cands[best];
     s->calibrated = cands.size() > 1;
-    if (w.relayout) {
-        if (have_rc) rc.plan = w.plan;  // (re-put: the timing loop may have evicted it)
+    if (w.relayout) {  // (re-put: the timing loop may have evicted it)
+        rc.perm = w.perm;
+        rc.ops = w.ops;
+        rc.plan = w.plan;
         take_relayout();
         return;
     }

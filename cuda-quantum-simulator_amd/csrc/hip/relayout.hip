@@ -28,6 +28,7 @@
 #include <cstdio>
 #include <cstdint>
 #include <cstdlib>
+#include <mutex>
 #include <random>
 #include <unordered_set>
 
@@ -130,7 +131,8 @@ bool close_cycle(std::vector<uint64_t>& T, const std::vector<uint64_t>& U) {
     return true;
 }
 
-std::vector<uint64_t> search_tiles(const Search& S, size_t nops, int width, size_t max_passes) {
+std::vector<std::vector<uint64_t>> search_tiles(const Search& S, size_t nops, int width, size_t max_passes,
+                                               int nvar) {
     const int n = S.n;
     std::vector<St> states(1);
     states[0].rem.resize(nops);
@@ -171,7 +173,8 @@ std::vector<uint64_t> search_tiles(const Search& S, size_t nops, int width, size
             for (const auto& pp : part) {
                 St t;
                 t.rem = S.apply(s.rem, pp.second);
-                if (t.rem.size() == s.rem.size() || !seen.insert(t.rem).second) continue;
+                // (finished sequences are all kept: they are the variants a timed first run compares)
+                if (t.rem.size() == s.rem.size() || (!t.rem.empty() && !seen.insert(t.rem).second)) continue;
                 t.tiles = s.tiles;
                 t.tiles.push_back(pp.second);
                 next.push_back(std::move(t));
@@ -179,6 +182,7 @@ std::vector<uint64_t> search_tiles(const Search& S, size_t nops, int width, size
         }
         if (next.empty()) return {};
         std::stable_sort(next.begin(), next.end(), [](const St& a, const St& b) { return a.rem.size() < b.rem.size(); });
+        std::vector<std::vector<uint64_t>> done;  // closed sequences of this (the fewest-pass) step
         for (St& s : next) {
             if (!s.rem.empty()) break;
             // a finished sequence: close the cycle (its gates per pass first)
@@ -192,8 +196,12 @@ std::vector<uint64_t> search_tiles(const Search& S, size_t nops, int width, size
                 for (int i : ran) u |= S.qm[i];
                 U.push_back(u);
             }
-            if (close_cycle(s.tiles, U)) return s.tiles;
+            if (close_cycle(s.tiles, U)) {
+                done.push_back(s.tiles);
+                if ((int)done.size() >= nvar) break;
+            }
         }
+        if (!done.empty()) return done;
         next.erase(std::remove_if(next.begin(), next.end(), [](const St& s) { return s.rem.empty(); }), next.end());
         if (next.empty()) return {};
         if ((int)next.size() > width) next.resize(width);
@@ -325,22 +333,11 @@ void relayout_configure(int mode, int min_qubits) {
     if (min_qubits >= 0) g_relayout_min.store(min_qubits);
 }
 
-bool plan_relayout(int n, const std::function<std::vector<Op>(const std::vector<int>&)>& lower,
-                   size_t max_passes, RelayoutChoice& out) {
-    if (n < kTile + kRun || n - kTile > 32) return false;
-    std::vector<int> id(n);
-    for (int q = 0; q < n; ++q) id[q] = q;
-    const std::vector<Op> logical = lower(id);
-    if (logical.empty()) return false;
-    std::vector<uint64_t> qm(logical.size());
-    for (size_t i = 0; i < logical.size(); ++i) {
-        qm[i] = op_mask(logical[i]);
-        if (__builtin_popcountll(qm[i]) > kTile - kRun) return false;
-    }
-    const Search S{qm, n};
-    static const int width = env_int("QSIM_RELAYOUT_BEAM", 96);
-    const int w = std::max(2, (int)(width * 256.0 / std::max<size_t>(256, logical.size())));
-    std::vector<uint64_t> T = search_tiles(S, logical.size(), w, std::min<size_t>(max_passes, 64));
+namespace {
+// One relayout choice from a closed tile sequence T: runs, layouts, the plan.
+bool build_choice(int n, const std::function<std::vector<Op>(const std::vector<int>&)>& lower,
+                  const std::vector<Op>& logical, const Search& S, const std::vector<uint64_t>& T,
+                  size_t max_passes, RelayoutChoice& out) {
     const size_t K = T.size();
     if (K < 2 || K >= max_passes) return false;
     // gates of every pass
@@ -420,6 +417,85 @@ bool plan_relayout(int n, const std::function<std::vector<Op>(const std::vector<
     }
     out.plan = std::move(plan);
     out.cost_us = cost;
+    return true;
+}
+
+// Process-wide memo of relayout choices by circuit (its identity-lowered ops): a state reset and
+// re-run, or another state running the same circuit, does not search again.
+struct RelayoutMemo {
+    int n;
+    size_t max_passes;
+    std::vector<unsigned char> key;
+    std::vector<RelayoutChoice> v;
+    uint64_t used;
+};
+std::mutex g_rl_mu;
+std::vector<RelayoutMemo> g_rl_memo;
+uint64_t g_rl_clock = 0;
+std::vector<unsigned char> ops_key(const std::vector<Op>& ops) {
+    std::vector<unsigned char> k;
+    for (const Op& o : ops) {
+        const int64_t ints[7] = {o.kind, o.sub, o.t0, o.t1, (int64_t)o.cmask, o.d0_one ? 1 : 0, o.src};
+        const unsigned char* a = reinterpret_cast<const unsigned char*>(ints);
+        k.insert(k.end(), a, a + sizeof ints);
+        const unsigned char* m = reinterpret_cast<const unsigned char*>(o.m);
+        k.insert(k.end(), m, m + sizeof o.m);
+    }
+    return k;
+}
+}  // namespace
+
+size_t plan_relayout_variants(int n, const std::function<std::vector<Op>(const std::vector<int>&)>& lower,
+                              size_t max_passes, std::vector<RelayoutChoice>& out) {
+    out.clear();
+    if (n < kTile + kRun || n - kTile > 32) return 0;
+    std::vector<int> id(n);
+    for (int q = 0; q < n; ++q) id[q] = q;
+    const std::vector<Op> logical = lower(id);
+    if (logical.empty()) return 0;
+    const std::vector<unsigned char> key = ops_key(logical);
+    {
+        std::lock_guard<std::mutex> l(g_rl_mu);
+        for (RelayoutMemo& m : g_rl_memo)
+            if (m.n == n && m.max_passes == max_passes && m.key == key) {
+                m.used = ++g_rl_clock;
+                out = m.v;
+                return out.size();
+            }
+    }
+    std::vector<uint64_t> qm(logical.size());
+    bool fits = true;
+    for (size_t i = 0; i < logical.size(); ++i) {
+        qm[i] = op_mask(logical[i]);
+        fits = fits && __builtin_popcountll(qm[i]) <= kTile - kRun;
+    }
+    if (fits) {
+        const Search S{qm, n};
+        static const int width = env_int("QSIM_RELAYOUT_BEAM", 96);
+        static const int nvar = std::max(1, env_int("QSIM_RELAYOUT_VARIANTS", 3));
+        const int w = std::max(2, (int)(width * 256.0 / std::max<size_t>(256, logical.size())));
+        for (const std::vector<uint64_t>& T : search_tiles(S, logical.size(), w, std::min<size_t>(max_passes, 64), nvar)) {
+            RelayoutChoice rc;
+            if (build_choice(n, lower, logical, S, T, max_passes, rc)) out.push_back(std::move(rc));
+        }
+        std::stable_sort(out.begin(), out.end(), [](const RelayoutChoice& x, const RelayoutChoice& y) {
+            return x.plan.passes.size() != y.plan.passes.size() ? x.plan.passes.size() < y.plan.passes.size()
+                                                                : x.cost_us < y.cost_us;
+        });
+    }
+    std::lock_guard<std::mutex> l(g_rl_mu);
+    if (g_rl_memo.size() >= 8)
+        g_rl_memo.erase(std::min_element(g_rl_memo.begin(), g_rl_memo.end(),
+                                         [](const RelayoutMemo& x, const RelayoutMemo& y) { return x.used < y.used; }));
+    g_rl_memo.push_back(RelayoutMemo{n, max_passes, key, out, ++g_rl_clock});
+    return out.size();
+}
+
+bool plan_relayout(int n, const std::function<std::vector<Op>(const std::vector<int>&)>& lower,
+                   size_t max_passes, RelayoutChoice& out) {
+    std::vector<RelayoutChoice> v;
+    if (!plan_relayout_variants(n, lower, max_passes, v)) return false;
+    out = std::move(v.front());
     return true;
 }
 
