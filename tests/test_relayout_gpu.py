@@ -79,3 +79,31 @@ def test_relayout_calibrated_choice_matches_oracle(qsim, oracle, gpu_ready, rela
     sim.run(inv)
     sv = sim.getStateVector()
     assert abs(sv[0] - 1.0) < 1e-10 and float(np.sum(np.abs(sv[1:]) ** 2)) < 1e-20
+
+
+def test_relayout_from_basis_state_then_readers_and_gates(qsim, oracle, gpu_ready, relayout_low):
+    """A relayout run from a non-zero basis state, then per-gate entries under the layout, then
+    the readers (each restores the identity layout with one gate-free relayout pass first)."""
+    from qsim_amd.plan import set_jit
+    set_jit(0, 20)
+    n = 22
+    c = qsim.createRandomCircuit(n, 120, 9)
+    g = oracle.gates_of(c)
+    k = (1 << 21) | (1 << 13) | 5
+    start = np.zeros(1 << n, complex)
+    start[k] = 1.0
+    sv = qsim.StateVector(n)
+    sv.initializeBasis(k)
+    sv.run(c, qsim.RunMode.Fused)
+    assert sv.perm() != list(range(n))
+    extra = qsim.Circuit(n)
+    extra.h(n - 1).cnot(3, 17).t(9)
+    for gt in extra.getGates():
+        sv.applyGate(gt)  # mapped through the layout (no restore needed)
+    assert sv.perm() != list(range(n))
+    ref = oracle.run_cpu(n, oracle.gates_of(extra), state=oracle.run_cpu(n, g, state=start))
+    probs = np.abs(ref) ** 2
+    idx = np.arange(1 << n)
+    assert abs(sv.probBitZero(11) - probs[((idx >> 11) & 1) == 0].sum()) < 1e-12
+    assert sv.perm() == list(range(n))
+    assert _err(sv.toHost(), ref) < 1e-12
