@@ -200,8 +200,8 @@ struct RelayoutChoice {
 };
 bool plan_relayout(int n, const std::function<std::vector<Op>(const std::vector<int>&)>& lower,
                    size_t max_passes, RelayoutChoice& out);
-// Up to QSIM_RELAYOUT_VARIANTS (default 3) relayout choices of the fewest passes (different tile
-// sequences), best predicted first — the candidates a timed first run compares; memoised.
+// Up to QSIM_RELAYOUT_VARIANTS (default 3) closed tile sequences of the fewest passes, each with
+// QSIM_RELAYOUT_LAYOUT_VARIANTS (default 2) position choices: relayout choices, best predicted first — the candidates a timed first run compares; memoised.
 size_t plan_relayout_variants(int n, const std::function<std::vector<Op>(const std::vector<int>&)>& lower,
                               size_t max_passes, std::vector<RelayoutChoice>& out);
 bool relayout_enabled(int n);  // QSIM_RELAYOUT (default 1), QSIM_RELAYOUT_MIN_QUBITS (default 20)
@@ -312,7 +312,7 @@ struct PlanCache {
         JitState jit;
         uint64_t used = 0;
     };
-    static constexpr size_t kEntries = 12;  // (first-run calibration keeps its candidates)
+    static constexpr size_t kEntries = 16;  // (first-run calibration keeps its candidates)
     std::vector<std::unique_ptr<Entry>> entries;
     uint64_t clock = 0;
     // stream: where the owner runs this cache's plans (drained before a plan is evicted)

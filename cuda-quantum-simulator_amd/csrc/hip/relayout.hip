@@ -213,7 +213,8 @@ std::vector<std::vector<uint64_t>> search_tiles(const Search& S, size_t nops, in
 // A layout (logical -> physical) with `run` at positions 0..3 and the other qubits of x (the
 // tile stored into this layout) and y (the tile loaded from it) where the layout model prices
 // store + load lowest; the remaining qubits fill the remaining positions in order.
-std::vector<int> assign_layout(int n, uint64_t run, uint64_t x, uint64_t y) {
+// seed: the hill climbing's restarts (layout variants of one tile sequence differ by it)
+std::vector<int> assign_layout(int n, uint64_t run, uint64_t x, uint64_t y, unsigned seed = 0) {
     std::vector<int> L(n, -1);
     int k = 0;
     for (uint64_t m = run; m; m &= m - 1) L[__builtin_ctzll(m)] = k++;
@@ -260,7 +261,7 @@ std::vector<int> assign_layout(int n, uint64_t run, uint64_t x, uint64_t y) {
     std::vector<int> best_pos;
     double best = 1e300;
     for (int restart = 0; restart < 4; ++restart) {
-        std::mt19937 rng(0x7e1a0u + (unsigned)restart);
+        std::mt19937 rng(0x7e1a0u + (unsigned)restart + 0x1000u * seed);
         std::vector<int> slots(npos);
         for (int i = 0; i < npos; ++i) slots[i] = first + i;
         if (restart > 0) std::shuffle(slots.begin(), slots.end(), rng);
@@ -337,7 +338,7 @@ namespace {
 // One relayout choice from a closed tile sequence T: runs, layouts, the plan.
 bool build_choice(int n, const std::function<std::vector<Op>(const std::vector<int>&)>& lower,
                   const std::vector<Op>& logical, const Search& S, const std::vector<uint64_t>& T,
-                  size_t max_passes, RelayoutChoice& out) {
+                  size_t max_passes, RelayoutChoice& out, unsigned seed = 0) {
     const size_t K = T.size();
     if (K < 2 || K >= max_passes) return false;
     // gates of every pass
@@ -360,7 +361,7 @@ bool build_choice(int n, const std::function<std::vector<Op>(const std::vector<i
     }
     // layouts: L[k] is loaded by pass k and stored by pass k-1 (L[0] also by the last pass)
     std::vector<std::vector<int>> L(K + 1);
-    for (size_t k = 0; k < K; ++k) L[k] = assign_layout(n, R[k], T[(k + K - 1) % K], T[k]);
+    for (size_t k = 0; k < K; ++k) L[k] = assign_layout(n, R[k], T[(k + K - 1) % K], T[k], seed);
     L[K] = L[0];
     out.perm = L[0];
     out.ops = lower(out.perm);
@@ -473,10 +474,17 @@ size_t plan_relayout_variants(int n, const std::function<std::vector<Op>(const s
         const Search S{qm, n};
         static const int width = env_int("QSIM_RELAYOUT_BEAM", 96);
         static const int nvar = std::max(1, env_int("QSIM_RELAYOUT_VARIANTS", 3));
+        static const int nlay = std::max(1, env_int("QSIM_RELAYOUT_LAYOUT_VARIANTS", 2));
         const int w = std::max(2, (int)(width * 256.0 / std::max<size_t>(256, logical.size())));
         for (const std::vector<uint64_t>& T : search_tiles(S, logical.size(), w, std::min<size_t>(max_passes, 64), nvar)) {
-            RelayoutChoice rc;
-            if (build_choice(n, lower, logical, S, T, max_passes, rc)) out.push_back(std::move(rc));
+            for (int ls = 0; ls < nlay; ++ls) {  // layout variants of the sequence (unique first layouts:
+                                                 // a memoised choice is found again by it)
+                RelayoutChoice rc;
+                if (!build_choice(n, lower, logical, S, T, max_passes, rc, (unsigned)ls)) continue;
+                bool dup = false;
+                for (const RelayoutChoice& o : out) dup = dup || o.perm == rc.perm;
+                if (!dup) out.push_back(std::move(rc));
+            }
         }
         std::stable_sort(out.begin(), out.end(), [](const RelayoutChoice& x, const RelayoutChoice& y) {
             return x.plan.passes.size() != y.plan.passes.size() ? x.plan.passes.size() < y.plan.passes.size()
