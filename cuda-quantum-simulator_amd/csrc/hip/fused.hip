@@ -1438,7 +1438,8 @@ double2* launch_fused(double2* st, int n, uint64_t batch, const Plan& plan, cons
         if (jm && pi < jm->fn.size() && jm->fn[pi]) {  // circuit-specialised kernel (jit.hip)
             unsigned long long stride = a.stride, tpt = a.tpt_mask, zm = a.zmask, fv = a.fix_val, ntiles = blocks;
             int lt_arg = lt;
-            void* args[] = {&a.st, &stride, &tpt, &lt_arg, &zm, &fv, &ntiles, &a.dst};  // (dst: relayout kernels)
+            // (dst: the eighth parameter of relayout kernels only; other kernels take seven)
+            void* args[] = {&a.st, &stride, &tpt, &lt_arg, &zm, &fv, &ntiles, &a.dst};
             const unsigned nthr = (unsigned)((64 << p.h) >> p.rb);
             // a pipelined (persistent) kernel gets the resident workgroups only and walks its tiles
             const uint64_t grid = jit_pass_pipelined(p) ? std::min<uint64_t>(blocks, pipe_workgroups(p.h)) : blocks;

@@ -225,7 +225,6 @@ namespace {
 // sum_i ((src >> i) & 1) << dst[i] over i < cnt, consecutive bit runs moved by one mask + shift
 std::string scatter_expr(const std::string& src, const int* dst, int cnt, bool wide) {
     const std::string ty = wide ? "(unsigned long long)" : "";
-    const std::string one = wide ? "1ull" : "1u";
     std::string e;
     for (int i = 0; i < cnt;) {
         int k = 1;
@@ -239,7 +238,6 @@ std::string scatter_expr(const std::string& src, const int* dst, int cnt, bool w
         e += e.empty() ? t : " | " + t;
         i += k;
     }
-    (void)one;
     return e.empty() ? (wide ? std::string("0ull") : std::string("0u")) : e;
 }
 // Thread index spread over the tile bits that are not register bits of stage `st`.

@@ -237,10 +237,9 @@ std::vector<int> assign_layout(int n, uint64_t run, uint64_t x, uint64_t y, unsi
                 break;
             }
     }
-    uint64_t placed = run;
+    uint64_t placed = run;  // qubits with a position already
     for (int q = 0; q < n; ++q)
         if (L[q] >= 0) placed |= 1ull << q;
-    (void)placed;
     const int npos = n - first;  // positions first..n-1
     for (uint64_t m = (x | y) & ~placed; m; m &= m - 1) sq.push_back(__builtin_ctzll(m));
     uint64_t fixed_x = 0, fixed_y = 0;  // positions already taken by x / y qubits
