@@ -256,7 +256,7 @@ struct LayoutChoice {
 };
 LayoutChoice choose_layout(int n, const std::function<std::vector<Op>(const std::vector<int>&)>& lower,
                            int tries, size_t want_alts = 0);
-// QSIM_RELABEL_CALIBRATE (default 1) / QSIM_RELABEL_CALIBRATE_MIN_QUBITS (default 28): with
+// QSIM_RELABEL_CALIBRATE (default 1) / QSIM_RELABEL_CALIBRATE_MIN_QUBITS (default 26): with
 // inline compilation (QSIM_JIT=2) the first run of a basis state times the model's choice and
 // its alternatives with their circuit-specialised kernels and keeps the fastest (capi.hip).
 bool relabel_calibrate(int n);

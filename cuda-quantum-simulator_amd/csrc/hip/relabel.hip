@@ -111,7 +111,7 @@ bool relabel_calibrate(int n) {
     }
     if (g_calib_min.load() < 0) {
         const char* e = std::getenv("QSIM_RELABEL_CALIBRATE_MIN_QUBITS");
-        g_calib_min.store(e ? std::atoi(e) : 28);
+        g_calib_min.store(e ? std::atoi(e) : 26);
     }
     return g_calib.load() != 0 && n >= g_calib_min.load() && jit_mode() == 2;
 }

@@ -193,7 +193,7 @@ int qsim_plan_exec_host(int n_qubits, const qsim_gate* gates, size_t count, int 
 int qsim_plan_relayout(int n_qubits, const qsim_gate* gates, size_t count, int32_t* perm, int* passes,
                        double* predicted_us);
 /* Layout calibration (with QSIM_JIT = 2, from min_qubits; defaults QSIM_RELABEL_CALIBRATE = 1,
- * QSIM_RELABEL_CALIBRATE_MIN_QUBITS = 28): the first run of a basis state times the layout
+ * QSIM_RELABEL_CALIBRATE_MIN_QUBITS = 26): the first run of a basis state times the layout
  * model's choice and two alternatives with their compiled pass kernels (the basis state is
  * restored after each) and keeps the fastest.  Negative arguments leave a setting unchanged. */
 int qsim_set_calibrate(int mode, int min_qubits);
