@@ -52,11 +52,13 @@ def parse():
     p.add_argument("--jit", type=int, choices=[0, 1, 2], default=2,
                    help="circuit-specialised pass kernels: 0 interpreter only, 1 background "
                         "compile, 2 compile during the first warmup run (default)")
-    p.add_argument("--workload", choices=["hc", "ref", "1q", "batch"], default="hc",
+    p.add_argument("--workload", choices=["hc", "ref", "1q", "batch", "dm", "noisy"], default="hc",
                    help="hc: W-HC random H+CNOT; ref: reference benchmark_scaling circuit; "
                         "1q: 100 unfused H gates on targets i %% n; batch: W-BATCH, the W-HC "
                         "circuit on --trajectories noisy trajectories (depolarizing on every "
-                        "qubit after every gate, SURVEY §8(d))")
+                        "qubit after every gate, SURVEY §8(d)); dm: DensityMatrixSimulator (default 14 "
+                        "qubits); noisy: NoisySimulator (default 26 qubits), both W-HC with "
+                        "depolarizing --noise on all qubits")
     p.add_argument("--trajectories", type=int, default=1024)
     p.add_argument("--batch-noise", choices=["physical", "reference"], default="reference",
                    help="W-BATCH noise process: reference (the BatchedSimulator default: per-pair "
@@ -66,6 +68,9 @@ def parse():
                    help="skip the W-1Q 28q single-qubit roofline object of the default line")
     p.add_argument("--no-batch16", action="store_true",
                    help="skip the W-BATCH 16q x 1024 object (BASELINE config 4) of the default line")
+    p.add_argument("--no-extras", action="store_true",
+                   help="skip the default line's extra objects (seeds, default_mode, w_ref, "
+                        "gate_table_20q, dm_14q, noisy_26q)")
     p.add_argument("--noise", type=float, default=0.01)
     p.add_argument("--cpu-budget", type=float, default=12.0,
                    help="seconds of single-thread CPU oracle work for cpu_baseline (0 = skip)")
@@ -79,7 +84,7 @@ def parse():
                    help="per-launch HBM traffic measured by rocprofv3 --pmc (see profiles/)")
     a = p.parse_args()
     if a.qubits is None:
-        a.qubits = 16 if a.workload == "batch" else 30
+        a.qubits = {"batch": 16, "dm": 14, "noisy": 26}.get(a.workload, 30)
     return a
 
 
@@ -157,8 +162,15 @@ def run_single(args):
     from qsim_amd.plan import set_jit
     set_jit(args.jit, -1)
     sim = q.Simulator(n, mode=mode)
-    for _ in range(max(1, args.warmup) if args.jit else args.warmup):
+    # the first run() on |0..0> alone: what a one-shot sim.run(c) user pays (layout choice,
+    # calibration candidates timed on the device, pass-kernel compiles, the run itself)
+    first_run_ms = None
+    for i in range(max(1, args.warmup) if args.jit else args.warmup):
+        tf = time.perf_counter()
         sim.run(circuit)
+        if i == 0:
+            sim.synchronize()
+            first_run_ms = round((time.perf_counter() - tf) * 1e3, 1)
     sim.synchronize()
     sim.state.profileReset()
     sim.synchronize()
@@ -231,6 +243,7 @@ def run_single(args):
                    "relayout": layout["relayout"], "passes": run_passes,
                    "state_bytes": 16 << n, "parallelism": "single GPU"},
         "value_is": "gates / median step time (every step synchronised); value_mean = gates x steps / wall",
+        "first_run_ms": first_run_ms,
         "restore_ms": restore_ms,
         "restore_passes": restore_passes if restore_ms is not None else None,
         "roofline": roof,
@@ -238,6 +251,13 @@ def run_single(args):
         "kernels": stats,
     }
     del sim
+    if args.workload == "hc" and not args.no_extras:
+        out["seeds"] = hc_seeds(q, args)
+        out["default_mode"] = default_mode(q, args, circuit)
+        out["w_ref"] = w_ref(q, args)
+        out["gate_table_20q"] = gate_table_20q(q)
+        out["dm_14q"] = measure_dm(q, 14, 3, 1, args.jit, args.seed, args.depth, 0.01)
+        out["noisy_26q"] = measure_noisy(q, 26, 3, 1, args.seed, args.depth, 0.01)
     if args.workload == "hc" and not args.no_1q28:
         out["roofline_1q28"] = roofline_1q28(q)
     if args.workload == "hc" and not args.no_batch16:
@@ -247,6 +267,252 @@ def run_single(args):
     else:
         out["cpu_baseline"] = None
     print(json.dumps(out))
+
+
+def _median(xs):
+    xs = sorted(xs)
+    m = len(xs) // 2
+    return xs[m] if len(xs) % 2 else 0.5 * (xs[m - 1] + xs[m])
+
+
+def _timed_runs(sim, circuit, steps):
+    """Median wall time of `steps` synchronised runs (seconds)."""
+    ts = []
+    for _ in range(steps):
+        t0 = time.perf_counter()
+        sim.run(circuit)
+        sim.synchronize()
+        ts.append(time.perf_counter() - t0)
+    return _median(ts)
+
+
+def hc_seeds(q, args, seeds=(1, 2, 3, 4), steps=5):
+    """W-HC at the line's size for seeds 1-4 beside the headline seed: each seed's
+    calibrated first run on |0..0> (its first_run_ms), one warm-up run, then the median of
+    `steps` synchronised runs; passes / relayout / tile height of the plan it keeps."""
+    n = args.qubits
+    from qsim_amd.plan import set_jit
+    set_jit(args.jit, -1)
+    sim = q.Simulator(n)
+    out = {"workload": f"W-HC depth {args.depth} at {n} qubits, seeds {list(seeds)}, same mode as the line",
+           "runs": []}
+    for sd in seeds:
+        sim.reset()
+        c = q.createRandomHCCircuit(n, args.depth, sd)
+        t0 = time.perf_counter()
+        sim.run(c)
+        sim.synchronize()
+        first = time.perf_counter() - t0
+        sim.run(c)
+        med = _timed_runs(sim, c, steps)
+        info = sim.state.layoutInfo()
+        out["runs"].append({"seed": sd, "value": round(c.getGateCount() / med, 1), "unit": "gates/s",
+                            "ms_per_step": round(med * 1e3, 3), "passes": sim.state.lastRunInfo()[0],
+                            "relayout": info["relayout"], "tile_qubits": info["tile_qubits"],
+                            "first_run_ms": round(first * 1e3, 1)})
+    del sim
+    vals = [r["value"] for r in out["runs"]]
+    out["min"], out["max"] = min(vals), max(vals)
+    return out
+
+
+def default_mode(q, args, circuit, steps=10, compile_wait_s=60.0):
+    """The same circuit at the library defaults (jit = 1: pass kernels compiled in the background
+    while the interpreter runs; no device calibration: the layout model's untimed choice).  The
+    first run is timed alone (what a one-shot user pays); then runs continue until every pass
+    runs its compiled kernel, and `steps` synchronised runs are timed."""
+    from qsim_amd.plan import DEFAULTS, set_jit
+    set_jit(*DEFAULTS["jit"])
+    try:
+        n = circuit.getNumQubits()
+        sim = q.Simulator(n)
+        t0 = time.perf_counter()
+        sim.run(circuit)
+        sim.synchronize()
+        first = time.perf_counter() - t0
+        runs_before_compiled = 1
+        tw = time.perf_counter()
+        while True:
+            passes, jit_passes = sim.state.lastRunInfo()
+            if jit_passes >= passes or time.perf_counter() - tw > compile_wait_s:
+                break
+            sim.run(circuit)
+            sim.synchronize()
+            runs_before_compiled += 1
+        med = _timed_runs(sim, circuit, steps)
+        info = sim.state.layoutInfo()
+        passes, jit_passes = sim.state.lastRunInfo()
+        out = {"value": round(circuit.getGateCount() / med, 1), "unit": "gates/s",
+               "ms_per_step": round(med * 1e3, 3), "first_run_ms": round(first * 1e3, 1),
+               "runs_before_compiled": runs_before_compiled, "passes": passes,
+               "jit_passes": jit_passes, "relayout": info["relayout"], "relabel": info["relabeled"],
+               "tile_qubits": info["tile_qubits"], "calibrated": info["calibrated"],
+               "mode": "library default: jit 1 (background compile), no calibration"}
+        del sim
+        return out
+    finally:
+        set_jit(args.jit, -1)
+
+
+# README.md:30-38 (RTX 4070 laptop, GPU times taken without a device synchronisation) and :58-63
+REF_W_REF_MS = {20: {"gpu_ms": 0.28, "cpu_ms": 143.50}, 22: {"gpu_ms": 0.28, "cpu_ms": 720.39}}
+REF_GATE_TABLE_20Q = {"CNOT": 53200, "X": 34300, "H": 24600, "Rz": 5940}
+
+
+def w_ref(q, args, sizes=(20, 22), steps=20):
+    """The reference's own GPU-vs-CPU workload (benchmarks/benchmark_scaling.cu:69-76: 100 H on
+    i % n plus a CNOT(i % n, (i+1) % n) every 5th, 120 gates) at 20 and 22 qubits: the engine in
+    the line's mode (median of `steps` synchronised runs after warm-up) beside the oracle's
+    single-thread CPUSimulator restatement on this host (one whole run) and the README numbers."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import numpy_oracle as orc  # test infrastructure: the CPU column only
+    from qsim_amd.plan import set_jit
+    set_jit(args.jit, -1)
+    rows = []
+    for n in sizes:
+        c = q.createScalingBenchmarkCircuit(n)
+        sim = q.Simulator(n)
+        for _ in range(3):
+            sim.run(c)
+        sim.synchronize()
+        med = _timed_runs(sim, c, steps)
+        del sim
+        g = orc.gates_of(c)
+        done, secs = orc.time_prefix(n, g, 60.0)
+        rows.append({"qubits": n, "gates": c.getGateCount(), "gpu_ms": round(med * 1e3, 4),
+                     "gates_per_s": round(c.getGateCount() / med, 1),
+                     "cpu_ms": round(secs * 1e3, 2) if done == len(g) else None, "cpu_cores": 1,
+                     "speedup_vs_cpu": round(secs / med, 1) if done == len(g) else None,
+                     "reference_readme": REF_W_REF_MS.get(n)})
+    return {"workload": "W-REF benchmark_scaling.cu:69-76 (100 H + 20 CNOT)", "rows": rows,
+            "note": "reference README GPU times are taken without a device synchronisation (launch "
+                    "time); ours are synchronised"}
+
+
+def gate_table_20q(q, n=20, count=1000, reps=3):
+    """The reference's gate-throughput table (benchmarks/benchmark_gates.cu:36-88, README.md:58-63):
+    1000 gates of one type on targets i % n (CNOT: control i % (n-1), target control + 1) at 20
+    qubits, one run after a warm-up run and reset; here synchronised, median of `reps`, in the
+    reference's one-kernel-per-gate mode and in the default fused mode."""
+    def circ(kind):
+        c = q.Circuit(n)
+        for i in range(count):
+            if kind == "H":
+                c.h(i % n)
+            elif kind == "X":
+                c.x(i % n)
+            elif kind == "Rz":
+                c.rz(i % n, 0.5)
+            else:
+                c.cnot(i % (n - 1), i % (n - 1) + 1)
+        return c
+    rows = {}
+    for kind in ("H", "X", "Rz", "CNOT"):
+        c = circ(kind)
+        row = {"reference_readme_gates_per_s": REF_GATE_TABLE_20Q[kind]}
+        for mode in (q.RunMode.PerGate, q.RunMode.Fused):
+            sim = q.Simulator(n, mode=mode)
+            sim.run(c)
+            sim.synchronize()
+            ts = []
+            for _ in range(reps):
+                sim.reset()
+                t0 = time.perf_counter()
+                sim.run(c)
+                sim.synchronize()
+                ts.append(time.perf_counter() - t0)
+            del sim
+            row["per_gate" if mode == q.RunMode.PerGate else "fused"] = round(count / _median(ts), 1)
+        rows[kind] = row
+    return {"workload": f"{count} gates per type at {n} qubits (benchmark_gates.cu)", "unit": "gates/s",
+            "rows": rows}
+
+
+def _dominant_roofline(stats):
+    byte_stats = [s for s in stats if s["alg_bytes"] > 0 and s["launches"]]
+    if not byte_stats:
+        return None
+    dom = max(byte_stats, key=lambda s: s["ms"])
+    per = dom["alg_bytes"] / dom["launches"]
+    avg_s = dom["ms"] / dom["launches"] / 1e3
+    ach = per / avg_s / 1e9
+    return {"bound": "hbm", "kernel": dom["name"], "achieved": round(ach, 1), "peak": HBM_PEAK_GBPS,
+            "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBPS, 4), "alg_bytes_per_launch": per,
+            "avg_launch_ms": round(avg_s * 1e3, 4), "launches": dom["launches"]}
+
+
+def measure_dm(q, n, steps, warmup, jit, seed, depth, p_noise):
+    """DensityMatrixSimulator (src/DensityMatrix.cu:978-1122): rho of n qubits as a 2n-index-bit
+    engine state (4^n x 16 B), the W-HC circuit with depolarizing p on all qubits (the reference
+    applies each channel after a gate that touches its qubit).  gates/s = circuit gates / median
+    synchronised run; roofline of the dominant kernel from per-launch HIP events."""
+    from qsim_amd.density import DensityMatrixSimulator
+    from qsim_amd.plan import set_jit
+    set_jit(jit, -1)
+    c = q.createRandomHCCircuit(n, depth, seed)
+    nm = q.NoiseModel()
+    nm.addDepolarizingAll(n, p_noise)
+    sim = DensityMatrixSimulator(n, nm)
+    sv = sim.density.state
+    for _ in range(max(1, warmup)):
+        sim.run(c)
+        sv.synchronize()
+    sv.profile(True)
+    sv.profileReset()
+    ts = []
+    for _ in range(steps):
+        sim.reset()
+        sv.synchronize()
+        t0 = time.perf_counter()
+        sim.run(c)
+        sv.synchronize()
+        ts.append(time.perf_counter() - t0)
+    stats = sv.profileStats()
+    sv.profile(False)
+    passes, jit_passes = sv.lastRunInfo()
+    tr = sim.getTrace()
+    del sim
+    med = _median(ts)
+    return {"workload": f"DensityMatrixSimulator {n} qubits (rho: {2 * n} index bits, {16 << (2 * n)} B), "
+                        f"W-HC depth {depth} seed {seed}, depolarizing {p_noise} on all qubits",
+            "value": round(c.getGateCount() / med, 1), "unit": "gates/s", "ms_per_step": round(med * 1e3, 3),
+            "passes": passes, "jit_passes": jit_passes, "trace": tr, "roofline": _dominant_roofline(stats),
+            "kernels": stats}
+
+
+def measure_noisy(q, n, steps, warmup, seed, depth, p_noise):
+    """NoisySimulator (src/NoiseModel.cu:117-314): the W-HC circuit with depolarizing p on all n
+    qubits, every channel entry a per-pair Monte-Carlo pass after every gate (the reference's
+    structure; flips walked geometrically, noise.hip).  gates/s = circuit gates / median run."""
+    c = q.createRandomHCCircuit(n, depth, seed)
+    nm = q.NoiseModel()
+    nm.addDepolarizingAll(n, p_noise)
+    sim = q.NoisySimulator(n, nm)
+    sim.setSeed(seed)
+    for _ in range(max(1, warmup)):
+        sim.run(c)
+    sim.synchronize()
+    sv = sim.state
+    sv.profile(True)
+    sv.profileReset()
+    ts = []
+    for _ in range(steps):
+        sim.reset()
+        sim.synchronize()
+        t0 = time.perf_counter()
+        sim.run(c)
+        sim.synchronize()
+        ts.append(time.perf_counter() - t0)
+    stats = sv.profileStats()
+    sv.profile(False)
+    del sim
+    med = _median(ts)
+    noise = [s for s in stats if s["name"] == "noise"]
+    return {"workload": f"NoisySimulator {n} qubits, W-HC depth {depth} seed {seed}, depolarizing "
+                        f"{p_noise} on all qubits after every gate ({n} channel passes per gate)",
+            "value": round(c.getGateCount() / med, 1), "unit": "gates/s", "ms_per_step": round(med * 1e3, 3),
+            "roofline": _dominant_roofline(stats),
+            "noise_roofline": _dominant_roofline(noise) if noise else None, "kernels": stats}
 
 
 def roofline_1q28(q, steps=3):
@@ -273,7 +539,20 @@ def roofline_1q28(q, steps=3):
     ms = sum(s["ms"] for s in stats)
     by = sum(s["alg_bytes"] for s in stats)
     achieved = by / (ms / 1e3) / 1e9
+    # PMC traffic per launch (profiles/pmc_1q_28q.json, the same W-1Q command under rocprofv3
+    # --pmc), launch-weighted over the kernels this workload ran
+    traffic, traffic_src = None, None
+    pmc_path = os.path.join(ROOT, "profiles", "pmc_1q_28q.json")
+    if os.path.exists(pmc_path):
+        with open(pmc_path) as f:
+            kern = json.load(f).get("kernels", {})
+        ents = [kern[s["name"]] for s in stats if s["name"] in kern]
+        tl = sum(e["launches"] for e in ents)
+        if ents and tl:
+            traffic = sum(e["hbm_bytes_per_launch"] * e["launches"] for e in ents) / tl
+            traffic_src = os.path.relpath(pmc_path, ROOT)
     return {"workload": "W-1Q 100 unfused H gates on targets i % 28, 28 qubits",
+            "traffic": traffic, "traffic_source": traffic_src,
             "kernels": sorted({s["name"] for s in stats}), "launches": launches,
             "avg_launch_ms": round(ms / launches, 4), "alg_bytes_per_launch": by / launches,
             "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
@@ -377,6 +656,24 @@ def run_batch(args):
     print(json.dumps(out))
 
 
+def run_model_line(args):
+    """--workload dm / noisy: one line for the §8(f) simulators (value = circuit gates/s)."""
+    import qsim_amd as q
+    if args.workload == "dm":
+        m = measure_dm(q, args.qubits, args.steps, args.warmup, args.jit, args.seed, args.depth, args.noise)
+        metric = "gates/s, W-HC circuit with depolarizing noise (DensityMatrixSimulator)"
+    else:
+        m = measure_noisy(q, args.qubits, args.steps, args.warmup, args.seed, args.depth, args.noise)
+        metric = "gates/s, W-HC circuit with depolarizing noise (NoisySimulator)"
+    out = {"metric": metric, "value": m["value"], "unit": "gates/s", "n_gpus": 1, "steps": args.steps,
+           "warmup": args.warmup, "ms_per_step": m["ms_per_step"], "higher_is_better": True,
+           "scaling": "weak", "vs_baseline": None, "dtype": "c128 (complex<double>)", "data": "synthetic",
+           "config": {"workload": m["workload"], "qubits": args.qubits},
+           "roofline": m["roofline"], "cpu_baseline": None}
+    out.update({k: v for k, v in m.items() if k not in out and k not in ("value", "workload")})
+    print(json.dumps(out))
+
+
 def main():
     args = parse()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -392,6 +689,11 @@ def main():
         sys.exit(launch.launch_ranks(os.path.abspath(__file__), sys.argv[1:], args.gpus,
                                      timeout_s=args.launch_timeout))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.workload in ("dm", "noisy"):
+        if world > 1 or args.gpus > 1:
+            sys.exit("--workload dm / noisy run on one GPU")
+        run_model_line(args)
+        return
     if args.workload == "batch":
         if world > 1 or args.dry_run:
             from qsim_amd import dist_bench  # trajectory-sharded replicas

@@ -261,9 +261,22 @@ struct qsim_batch {
     // its frame build from them (frames compose: no Pauli pass per run); everything that reads
     // or writes amplitudes otherwise materialises them first (materialize), and so does sync.
     bool frame_pending = false;
+    // Pulled reference noise (noise.hip: launch_pull_noise_step) writes out of place: the
+    // ensemble alternates between d0 (allocated at create) and d1 (allocated on the first pulled
+    // run when the device has room; otherwise the push kernels run).  d is the current one.
+    // pinned: a raw pointer to d0 was handed out, so a run that ends in d1 copies back.
+    double2* d0 = nullptr;
+    double2* d1 = nullptr;
+    uint32_t* d_codes = nullptr;  // per-step flip codes, 2 bits per pair per channel
+    size_t codes_cap = 0;
+    uint32_t* d_touched = nullptr;  // per-step touched bits, one per amplitude
+    bool pinned = false;
     ~qsim_batch() {
         if (stream) (void)hipStreamSynchronize(stream);
-        if (d) (void)hipFree(d);
+        if (d0) (void)hipFree(d0);
+        if (d1) (void)hipFree(d1);
+        if (d_codes) (void)hipFree(d_codes);
+        if (d_touched) (void)hipFree(d_touched);
         if (d_xz) (void)hipFree(d_xz);
         if (d_e) (void)hipFree(d_e);
         if (d_ch) (void)hipFree(d_ch);
@@ -296,6 +309,50 @@ qsim_gate map_gate(const qsim_batch* b, const qsim_gate& g) {
         for (int j = 0; j < g.nqubits && j < 3; ++j)
             if (g.qubits[j] >= 0 && g.qubits[j] < b->n) m.qubits[j] = b->perm[g.qubits[j]];
     return m;
+}
+// The ensemble back in its first buffer (after a pulled run that ended in the second one).
+void settle_in_d0(qsim_batch* b) {
+    if (b->d == b->d0) return;
+    QSIM_HIPCHK(hipMemcpyAsync(b->d0, b->d, ((uint64_t)b->batch * sizeof(double2)) << b->n,
+                               hipMemcpyDeviceToDevice, b->stream));
+    b->d = b->d0;
+}
+// Buffers of the pulled noise path (second ensemble buffer, flip codes, touched bits), allocated
+// when the device has room for them beside a margin; false: run the push kernels instead.
+bool ensure_pull_buffers(qsim_batch* b, size_t nch) {
+    const uint64_t amps = (uint64_t)b->batch << b->n;
+    const size_t state_b = amps * sizeof(double2);
+    const size_t codes_b = pull_noise_codes_bytes(b->n, (uint64_t)b->batch, nch);
+    const size_t touched_b = amps / 8;
+    size_t need_b = (b->d1 ? 0 : state_b) + (codes_b > b->codes_cap ? codes_b : 0) + (b->d_touched ? 0 : touched_b);
+    if (need_b == 0) return true;
+    size_t free_b = 0, total_b = 0;
+    if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    if (free_b < need_b + (256ull << 20)) return false;
+    auto grab = [&](void** p, size_t bytes) {
+        if (hipMalloc(p, bytes) != hipSuccess) {
+            (void)hipGetLastError();
+            *p = nullptr;
+            return false;
+        }
+        return true;
+    };
+    if (!b->d1 && !grab((void**)&b->d1, state_b)) return false;
+    if (codes_b > b->codes_cap) {
+        if (b->d_codes) {
+            QSIM_HIPCHK(hipStreamSynchronize(b->stream));
+            (void)hipFree(b->d_codes);
+            b->d_codes = nullptr;
+            b->codes_cap = 0;
+        }
+        if (!grab((void**)&b->d_codes, codes_b)) return false;
+        b->codes_cap = codes_b;
+    }
+    if (!b->d_touched && !grab((void**)&b->d_touched, touched_b)) return false;
+    return true;
 }
 // Apply the carried Pauli frames to the stored vectors (one pass), frames back to 1.
 void materialize(qsim_batch* b) {
@@ -358,7 +415,8 @@ int qsim_batch_create(int n_qubits, int batch_size, qsim_batch** out) {
         QSIM_HIPCHK(hipGetDevice(&b->device));
         QSIM_HIPCHK(hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking));
         b->timer.stream = b->stream;
-        QSIM_HIPCHK(hipMalloc((void**)&b->d, ((uint64_t)batch_size * sizeof(double2)) << n_qubits));
+        QSIM_HIPCHK(hipMalloc((void**)&b->d0, ((uint64_t)batch_size * sizeof(double2)) << n_qubits));
+        b->d = b->d0;
         QSIM_HIPCHK(hipMalloc((void**)&b->d_xz, 2 * sizeof(uint64_t) * batch_size));
         QSIM_HIPCHK(hipMalloc((void**)&b->d_e, sizeof(int) * batch_size));
         b->seed = std::random_device{}();  // reference seeds from random_device (NoiseModel.cu:663)
@@ -486,6 +544,34 @@ int qsim_batch_run(qsim_batch* b, const qsim_gate* gates, size_t count,
             std::vector<NoiseChan> dep;
             for (size_t i = 0; i < n_channels; ++i)
                 if (channels[i].type == 0) dep.push_back(NoiseChan{0, channels[i].qubit, channels[i].probability});
+            if (pull_noise_supported(b->n, dep) && ensure_pull_buffers(b, dep.size())) {
+                // Pulled: the noise after gate i is applied by gate i+1's pass (out of place),
+                // the noise after the last gate by one identity pass; same draws, same states.
+                bool pending = false;
+                uint64_t c_pending = 0;
+                for (const Op& op : ops) {
+                    if (!pending) {
+                        if (op.kind >= 0) launch_op(b->d, b->n, (uint64_t)b->batch, op, b->stream, &b->timer);
+                    } else {
+                        double2* dst = b->d == b->d0 ? b->d1 : b->d0;
+                        launch_pull_noise_step(b->d, dst, b->n, (uint64_t)b->batch, b->traj0, dep, b->seed, c_pending,
+                                               op.kind >= 0 ? &op : nullptr, b->d_codes, b->d_touched, b->stream,
+                                               &b->timer);
+                        b->d = dst;
+                    }
+                    pending = true;
+                    c_pending = b->ncounter;
+                    b->ncounter += dep.size();  // (one pass counter per channel entry, as the push path)
+                }
+                if (pending) {
+                    double2* dst = b->d == b->d0 ? b->d1 : b->d0;
+                    launch_pull_noise_step(b->d, dst, b->n, (uint64_t)b->batch, b->traj0, dep, b->seed, c_pending,
+                                           nullptr, b->d_codes, b->d_touched, b->stream, &b->timer);
+                    b->d = dst;
+                }
+                if (b->pinned) settle_in_d0(b);
+                return;
+            }
             for (const Op& op : ops) {
                 if (op.kind >= 0) launch_op(b->d, b->n, (uint64_t)b->batch, op, b->stream, &b->timer);
                 launch_noise_after_gate(b->d, b->n, dep, b->seed, b->ncounter, b->stream, &b->timer,
@@ -659,6 +745,8 @@ int qsim_batch_device_ptr(qsim_batch* b, void** dptr) {
         need(b);
         canonicalize(b);
         b->basis = false;  // the caller may write through the pointer
+        settle_in_d0(b);   // (pulled runs copy their result back to this buffer from now on)
+        b->pinned = true;
         *dptr = b->d;
     });
 }

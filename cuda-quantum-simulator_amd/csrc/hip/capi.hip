@@ -206,11 +206,18 @@ struct qsim_state {
     // pointer was handed out, so the amplitudes are copied back to it after such a run.
     void* alt_base = nullptr;
     double2* alt = nullptr;
+    double2* base_d = nullptr;  // the amplitudes' address inside `base` (d == base_d or alt_base)
     bool pinned = false;
+    // pulled noise (NoisySimulator flip channels, noise.hip): per-step flip codes and touched bits
+    uint32_t* noise_codes = nullptr;
+    size_t noise_codes_cap = 0;
+    uint32_t* noise_touched = nullptr;
     ~qsim_state() {
         if (stream) (void)hipStreamSynchronize(stream);
         if (base) (void)hipFree(base);
         if (alt_base) (void)hipFree(alt_base);
+        if (noise_codes) (void)hipFree(noise_codes);
+        if (noise_touched) (void)hipFree(noise_touched);
         if (d_partials) (void)hipFree(d_partials);
         if (d_result) (void)hipFree(d_result);
         if (stream) (void)hipStreamDestroy(stream);
@@ -233,17 +240,83 @@ static void check_state(const qsim_state* s) {
     if (!s) fail(QSIM_ERR_INVALID_ARGUMENT, "null state handle");
 }
 
+// The second 2^n buffer relayout passes write into (they run out of place).  Allocated only
+// when the device has room for it beside a margin; a refused or failed allocation is cleared and
+// reported as false, so the caller keeps the in-place fixed-layout plan (the reference's
+// StateVector owns exactly one buffer, and coexisting states must not fail where it would not).
+static constexpr size_t kAltMarginBytes = 256ull << 20;
+static bool ensure_alt(qsim_state* s) {
+    if (s->alt) return true;
+    static const bool off = [] {  // QSIM_RELAYOUT_NO_ALT=1: behave as if it never fits (tests)
+        const char* e = std::getenv("QSIM_RELAYOUT_NO_ALT");
+        return e != nullptr && std::atoi(e) != 0;
+    }();
+    if (off) return false;
+    const size_t bytes = sizeof(double2) << s->n;
+    size_t free_b = 0, total_b = 0;
+    if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    if (free_b < bytes + kAltMarginBytes) return false;
+    void* p = nullptr;
+    if (hipMalloc(&p, bytes) != hipSuccess) {
+        (void)hipGetLastError();  // (clear the sticky error: the state itself is intact)
+        return false;
+    }
+    s->alt_base = p;
+    s->alt = reinterpret_cast<double2*>(p);
+    return true;
+}
+// Free the buffer the amplitudes are not in (the state goes back to one 2^n buffer).
+static void release_alt(qsim_state* s) {
+    if (!s->alt_base) return;
+    QSIM_HIPCHK(hipStreamSynchronize(s->stream));
+    if (s->d != s->base_d) {  // the amplitudes live in alt_base: it becomes the state's buffer
+        (void)hipFree(s->base);
+        s->base = s->alt_base;
+        s->base_d = s->d;
+    } else {
+        (void)hipFree(s->alt_base);
+    }
+    s->alt_base = nullptr;
+    s->alt = nullptr;
+}
+
+// Buffers of the pulled noise path: the second state buffer, per-step flip codes, touched bits.
+static bool ensure_noise_buffers(qsim_state* s, size_t nch) {
+    const size_t codes_b = pull_noise_codes_bytes(s->n, 1, nch), touched_b = (sizeof(double2) << s->n) / 128;
+    if (!ensure_alt(s)) return false;
+    auto grab = [&](uint32_t** p, size_t bytes) {
+        if (hipMalloc((void**)p, bytes) != hipSuccess) {
+            (void)hipGetLastError();
+            *p = nullptr;
+            return false;
+        }
+        return true;
+    };
+    if (codes_b > s->noise_codes_cap) {
+        if (s->noise_codes) {
+            QSIM_HIPCHK(hipStreamSynchronize(s->stream));
+            (void)hipFree(s->noise_codes);
+            s->noise_codes = nullptr;
+            s->noise_codes_cap = 0;
+        }
+        if (!grab(&s->noise_codes, codes_b)) return false;
+        s->noise_codes_cap = codes_b;
+    }
+    if (!s->noise_touched && !grab(&s->noise_touched, touched_b)) return false;
+    return true;
+}
+
 // One fused plan on the state: relayout passes alternate between the state's two buffers.
 static void launch_plan(qsim_state* s, const Plan& plan, Timer* tm, const JitModule* jm) {
     FusedRange range;
     bool relayout = false;
     for (const FusedPass& p : plan.passes) relayout = relayout || p.relayout;
     if (relayout) {
-        if (!s->alt) {
-            QSIM_HIPCHK(hipStreamSynchronize(s->stream));
-            QSIM_HIPCHK(hipMalloc(&s->alt_base, sizeof(double2) << s->n));
-            s->alt = reinterpret_cast<double2*>(s->alt_base);
-        }
+        // (choose_first_layout only takes relayout plans once the buffer exists)
+        if (!ensure_alt(s)) fail(QSIM_ERR_DEVICE, "out of device memory for the relayout buffer");
         range.alt = s->alt;
     }
     double2* r = launch_fused(s->d, s->n, 1, plan, (const TileOp*)s->ops.ptr, (const Stage*)s->stages.ptr,
@@ -285,11 +358,13 @@ static void canonicalize(qsim_state* s) {
         const char* e = std::getenv("QSIM_RESTORE_ONE_PASS");
         return e == nullptr || std::atoi(e) != 0;
     }();
-    if (one_pass && n >= 16 && n - 12 <= 32) {
+    // (it writes out of place: without room for the second buffer, the in-place SWAP network)
+    if (one_pass && n >= 16 && n - 12 <= 32 && ensure_alt(s)) {
         const Plan plan = plan_permutation_pass(n, s->perm);
         s->stages.upload(plan.stages.data(), plan.stages.size() * sizeof(Stage), s->stream);
         launch_plan(s, plan, &s->timer, nullptr);
         s->perm.clear();  // (last_passes keeps describing the last circuit run)
+        if (!s->relayout) release_alt(s);  // (only relayout plans keep the second buffer)
         return;
     }
     std::vector<int> p = s->perm, inv(n);
@@ -417,7 +492,18 @@ static void choose_first_layout(qsim_state* s, const qsim_gate* gates, size_t co
         const TileHeightScope scope(th);  // (a single-height decision is keyed by its height)
         layout_memo_put(n, 0, gates, bytes, perm, heights ? s->tile_h : -1);
     };
-    const bool relayout = relayout_enabled(n) && !tile_height_is_set();
+    // Relayout plans permute qubit labels, so they follow the relabeling mode (not its size
+    // threshold), and they need the second buffer: without room for it, fixed layouts only.
+    const bool relayout = relayout_enabled(n) && relabel_mode_on() && !tile_height_is_set() && ensure_alt(s);
+    struct AltRelease {  // a first run that does not end on a relayout plan keeps one buffer
+        qsim_state* s;
+        ~AltRelease() {
+            if (!s->relayout) try {
+                    release_alt(s);
+                } catch (...) {
+                }
+        }
+    } alt_release{s};
     const bool timing = relabel_calibrate(n);
     {
         // a relayout choice made before for this circuit (by timing, or by pass count when
@@ -505,6 +591,7 @@ static void choose_first_layout(qsim_state* s, const qsim_gate* gates, size_t co
     if (!relabel_enabled(n)) {
         // relayout only (states below the relabeling threshold): taken when it needs fewer
         // passes than the circuit's plan under the identity labels
+        if (!relayout) return;  // (no room for the second buffer: nothing to decide, no memo)
         rc_worker.join();
         std::vector<int> id(n);
         for (int q = 0; q < n; ++q) id[q] = q;
@@ -520,7 +607,7 @@ static void choose_first_layout(qsim_state* s, const qsim_gate* gates, size_t co
             const char* e = std::getenv("QSIM_RELAYOUT_TIME_SMALL");
             return e == nullptr || std::atoi(e) != 0;
         }();
-        if (have_rc && !force_rc && time_small && jit_mode() == 2) {
+        if (have_rc && !force_rc && time_small && jit_mode() == 2 && calibrate_mode_on()) {
             add(th, {}, ops0, p0);
             for (const RelayoutChoice& v : rcs)
                 if (v.plan.passes.size() <= p0.passes.size()) add(6, v.perm, v.ops, v.plan, true);
@@ -546,16 +633,21 @@ static void choose_first_layout(qsim_state* s, const qsim_gate* gates, size_t co
         }
         return;
     }
-    for (const Gen& g : gens) {
-        const TileHeightScope scope(g.h, tile_rb_for(n, g.h));
-        const LayoutT13Scope t13(g.t13);
+    if (force_rc) {  // (tests: a relayout plan whenever one exists)
         rc_worker.join();
-        if (have_rc && force_rc) {
+        if (have_rc) {
             take_relayout();
             return;
         }
+    }
+    // The relayout planner keeps running on its worker while the fixed-layout candidates are
+    // chosen below; it is joined where its result is first needed.
+    for (const Gen& g : gens) {
+        const TileHeightScope scope(g.h, tile_rb_for(n, g.h));
+        const LayoutT13Scope t13(g.t13);
         LayoutChoice lc = choose_layout(n, lower_under, relabel_tries(), g.alts);
         if (lc.perm.empty()) {  // the identity is this height's choice
+            rc_worker.join();
             if (!heights && !(have_rc && timing)) {  // (nothing to time)
                 if (have_rc && rc.plan.passes.size() < lc.passes_before) {
                     take_relayout();
@@ -574,6 +666,7 @@ static void choose_first_layout(qsim_state* s, const qsim_gate* gates, size_t co
         }
         for (LayoutChoice::Alt& a : lc.alts) add(g.h, std::move(a.perm), std::move(a.ops), std::move(a.plan));
     }
+    rc_worker.join();
     if (have_rc) {
         if (timing) {
             for (const RelayoutChoice& v : rcs) add(6, v.perm, v.ops, v.plan, true);
@@ -724,6 +817,7 @@ int qsim_state_create_on(int device, int n_qubits, qsim_state** out) {
             QSIM_HIPCHK(hipMalloc(&s->base, sbytes));
         }
         s->d = reinterpret_cast<double2*>(reinterpret_cast<char*>(s->base) + off);
+        s->base_d = s->d;
         QSIM_HIPCHK(hipMalloc((void**)&s->d_partials, 4096 * sizeof(double)));
         QSIM_HIPCHK(hipMalloc((void**)&s->d_result, sizeof(double)));
         launch_init_basis(s->d, s->n, 1, 0, s->stream);
@@ -838,7 +932,7 @@ int qsim_run(qsim_state* s, const qsim_gate* gates, size_t count, int flags) {
         // First run on a basis state: choose the qubit labels (and, with cross-height calibration,
         // the tile height) for fewer passes and faster pass layouts (relabel.hip: choose_layout).
         if ((flags & QSIM_RUN_FUSED) && s->basis && s->perm.empty() && count > 0 &&
-            (relabel_enabled(s->n) || (relayout_enabled(s->n) && !tile_height_is_set()))) {
+            (relabel_enabled(s->n) || (relayout_enabled(s->n) && relabel_mode_on() && !tile_height_is_set()))) {
             choose_first_layout(s, gates, count);
             if (!s->perm.empty() && s->basis_idx) {  // relabel the basis state itself
                 uint64_t k = 0;
@@ -1225,6 +1319,31 @@ int qsim_state_prob_bit_zero(qsim_state* s, int bit, double* out) {
     });
 }
 
+int qsim_state_max_abs_diff(qsim_state* a, qsim_state* b, double* out) {
+    return guarded([&] {
+        check_state(a);
+        check_state(b);
+        QSIM_REQUIRE(out, QSIM_ERR_INVALID_ARGUMENT, "null out");
+        if (a->n != b->n) fail(QSIM_ERR_INVALID_ARGUMENT, "states have different qubit counts");
+        if (a->device != b->device) fail(QSIM_ERR_INVALID_ARGUMENT, "states live on different devices");
+        DeviceGuard dg(a->device);
+        prep(a, false);  // both in the identity layout
+        prep(b, false);
+        QSIM_HIPCHK(hipStreamSynchronize(a->stream));  // a's writes done; b's stream orders the rest
+        *out = a == b ? 0.0 : reduce_max_abs_diff(a->d, b->d, a->n, b->d_partials, b->d_result, b->stream);
+    });
+}
+
+int qsim_state_memory_bytes(qsim_state* s, uint64_t* bytes) {
+    return guarded([&] {
+        check_state(s);
+        QSIM_REQUIRE(bytes, QSIM_ERR_INVALID_ARGUMENT, "null out");
+        const uint64_t amps = sizeof(double2) << s->n;
+        *bytes = amps + (s->alt_base ? amps : 0) + 4096 * sizeof(double) + sizeof(double) + s->scratch.cap +
+                 s->ops.cap + s->stages.cap + s->noise_codes_cap + (s->noise_touched ? amps / 128 : 0);
+    });
+}
+
 int qsim_state_collapse(qsim_state* s, int bit, int result, double scale) {
     return guarded([&] {
         check_state(s);
@@ -1283,6 +1402,38 @@ int qsim_noisy_run(qsim_state* s, const qsim_gate* gates, size_t count,
             if (flags & QSIM_RUN_FUSED) run_fused(s, ops);
             else for (const Op& op : ops) launch_op(s->d, s->n, 1, op, s->stream, &s->timer);
             return;
+        }
+        std::vector<NoiseChan> chans;
+        for (size_t c = 0; c < n_channels; ++c)
+            chans.push_back(NoiseChan{channels[c].type, channels[c].qubit, channels[c].probability});
+        if (pull_noise_supported(s->n, chans) && ensure_noise_buffers(s, chans.size())) {
+            // Flip channels only: the noise after gate i is applied by gate i+1's pass (out of
+            // place), the noise after the last gate by one identity pass (noise.hip); the same
+            // draws as the per-channel passes below, so the same state.
+            bool pending = false;
+            uint64_t c_pending = 0;
+            auto step = [&](const Op* op) {
+                double2* dst = s->alt;
+                launch_pull_noise_step(s->d, dst, s->n, 1, 0, chans, seed, c_pending, op, s->noise_codes,
+                                       s->noise_touched, s->stream, &s->timer);
+                s->alt = s->d;
+                s->d = dst;
+            };
+            for (const Op& op : ops) {
+                if (!pending) launch_op(s->d, s->n, 1, op, s->stream, &s->timer);
+                else step(&op);
+                pending = true;
+                c_pending = *counter;
+                *counter += n_channels;
+            }
+            if (pending) step(nullptr);
+            if (s->pinned && s->d != s->base_d) {  // keep the amplitudes where the handed-out pointer points
+                QSIM_HIPCHK(hipMemcpyAsync(s->base_d, s->d, sizeof(double2) << s->n, hipMemcpyDeviceToDevice,
+                                           s->stream));
+                s->alt = s->d;
+                s->d = s->base_d;
+            }
+            return;  // (the second buffer stays for the next run: qsim_state_memory_bytes counts it)
         }
         for (const Op& op : ops) {
             launch_op(s->d, s->n, 1, op, s->stream, &s->timer);

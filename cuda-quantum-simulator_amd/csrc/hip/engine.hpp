@@ -231,6 +231,7 @@ struct TileHeightScope {
 // microseconds, the tiles of a plan's staged passes, and the permutation (logical -> physical)
 // minimising the predicted cost of `tiles` (empty: keep the identity, < min_gain better).
 bool relabel_enabled(int n);                        // policy (QSIM_RELABEL*, qsim_set_relabel)
+bool relabel_mode_on();  // the mode alone (QSIM_RELABEL / qsim_set_relabel != 0), whatever the size
 void relabel_configure(int mode, int min_qubits);   // < 0 leaves a setting unchanged
 double layout_cost_us(uint64_t tile);
 std::vector<uint64_t> plan_tiles(const Plan& plan);
@@ -261,6 +262,7 @@ LayoutChoice choose_layout(int n, const std::function<std::vector<Op>(const std:
 // its alternatives with their circuit-specialised kernels and keeps the fastest (capi.hip).
 bool relabel_calibrate(int n);
 void calibrate_configure(int mode, int min_qubits);  // negative: unchanged
+bool calibrate_mode_on();  // the calibration mode alone (QSIM_RELABEL_CALIBRATE / qsim_set_calibrate)
 int relabel_tries();  // QSIM_RELABEL_TRIES (default 7): random labelings planned per choice
 // Process-wide memo of layout choices per circuit (kind: 0 state, 1 batched with its run flags).
 // h != null / h >= 0: a decision that also chose the tile height (cross-height calibration).
@@ -350,6 +352,16 @@ struct NoiseChan {
 };
 void launch_noise_after_gate(double2* st, int n, const std::vector<NoiseChan>& chans, uint64_t seed,
                              uint64_t& counter, hipStream_t s, Timer* tm, uint64_t batch, uint64_t traj0);
+// Pulled noise (noise.hip): the noise step after one gate (channels `chans`, passes counter0,
+// counter0 + 1, ...; the push kernels' draws) applied by the NEXT gate's pass: dst = U (P src)
+// out of place, op == null: the identity (the last step of a run).  codes: >=
+// pull_noise_codes_bytes; touched: (batch << n) / 8 bytes.  Supported when n >= 9, every
+// channel flips (depolarizing / X / Y / Z) and at most 32 can fire.
+bool pull_noise_supported(int n, const std::vector<NoiseChan>& chans);
+size_t pull_noise_codes_bytes(int n, uint64_t batch, size_t nch);
+void launch_pull_noise_step(const double2* src, double2* dst, int n, uint64_t batch, uint64_t traj0,
+                            const std::vector<NoiseChan>& chans, uint64_t seed, uint64_t counter0,
+                            const Op* op, uint32_t* codes, uint32_t* touched, hipStream_t s, Timer* tm);
 
 // Density matrices as 2n-index-bit states (density.hip).
 void dm_lower(int n, const qsim_gate* gates, size_t count, const qsim_noise_channel* ch,
@@ -365,6 +377,9 @@ void launch_probabilities(const double2* st, uint64_t count, double* out, hipStr
 double reduce_norm(const double2* st, int n, int bit, double* d_partials, double* d_result,
                    hipStream_t s);
 void launch_collapse(double2* st, int n, int bit, int result, double scale, hipStream_t s);
+// max over the 2^n amplitudes of the larger per-component |a - b| (d_partials: >= 2048 doubles).
+double reduce_max_abs_diff(const double2* a, const double2* b, int n, double* d_partials, double* d_result,
+                           hipStream_t s);
 struct Scratch;
 void launch_histogram(const int64_t* d_idx, uint64_t count, uint64_t N, unsigned long long* d_hist,
                       hipStream_t s);

@@ -219,6 +219,7 @@ struct Gen {
 bool jit_pass_pipelined(const FusedPass& p) {
     static const int v = env_or("QSIM_JIT_PIPE", 1);
     if (p.single >= 0 || p.stage_end - p.stage_begin < 2) return false;
+    if (p.relayout) return false;  // (the generator has no pipelined relayout store)
     return v >= 2 || (v == 1 && p.h >= 7);
 }
 namespace {

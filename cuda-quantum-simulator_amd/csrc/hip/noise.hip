@@ -26,6 +26,7 @@
 #include <cstdlib>
 #include <string>
 
+#include "device_ops.hpp"
 #include "engine.hpp"
 #include "qsim_hip.h"
 
@@ -339,6 +340,257 @@ void launch_noise(double2* st, int n, int type, int qubit, double p, uint64_t se
     } else {
         hipLaunchKernelGGL(k_noise<2>, dim3((unsigned)blocks), dim3(256), 0, s, a);
     }
+    QSIM_HIPCHK(hipGetLastError());
+}
+
+
+// ---------------------------------------------------------------------------------------
+// Pulled noise: the flips after gate g applied by the NEXT gate's pass (BatchedSimulator's
+// reference process, NoisySimulator's flip channels).
+//
+// The flips of one noise step (every channel entry after one gate) form a signed permutation P
+// of the amplitudes (X swaps a pair, Y swaps it with phases -i / +i, Z negates its |1> member).
+// Pushing P into the state costs random 16-B reads and writes over most of the lines (one noise
+// step ~ one streaming pass of line traffic).  Instead the next gate's kernel reads
+// its inputs through P: (P psi)[k] = phase * psi[pi^-1(k)], found by walking the channels from
+// the last to the first (each flip on the current index moves it along the channel's qubit), and
+// writes U (P psi) out of place — one streaming pass per gate step instead of two.
+//
+// The draws are exactly the push kernels' (flip_block: blocks of 256 global pairs, geometric
+// walks from the same counter hash), so both paths produce the same states:
+//   k_noise_map   per step, one thread per 512-amplitude region: walks the blocks holding the
+//                 region's pairs for every channel and writes (a) the 2-bit flip code of every
+//                 pair (0 none, 1 X, 2 Y, 3 Z; each block written by exactly one thread, so no
+//                 memset) and (b) one "touched" bit per amplitude (some channel flipped a pair
+//                 holding it, by its own index: the pull of an untouched amplitude is itself).
+//   k_pull_gate   the gate (2x2 / diagonal / SWAP with controls, or the identity after the last
+//                 gate) over the pulled inputs, src -> dst.
+// Needs n >= 9 (blocks and regions inside one trajectory), every channel a flip channel, <= 32.
+// ---------------------------------------------------------------------------------------
+constexpr int kRegionLog = 9;  // 512 amplitudes: 16 touched words, <= 2 blocks of pairs per channel
+constexpr int kMaxPullChannels = 32;
+struct MapArgs {
+    uint32_t* codes;     // [nch][pairs / 16]
+    uint32_t* touched;   // [amps / 32]
+    uint64_t amps;       // batch << n (this object's)
+    uint64_t cstride;    // words per channel = pairs / 16
+    uint64_t blk0;       // global block of local pair 0 = idx0 >> 8
+    int nch;
+    FlipChan ch[kMaxPullChannels];
+};
+
+// One block's walk: flips (local pair l in [0, 256) of block gb) handed to `f(l, code)`.
+template <class F>
+__device__ __forceinline__ void walk_block(uint64_t gb, const FlipChan& c, F&& f) {
+    FlipCursor cur{nz_mix(c.key ^ nz_mix(gb ^ kBlockSalt)), 0, -1, false};
+    uint64_t g = 0, h = 0;
+    const uint64_t lo = gb << kFlipBlockLog, hi = lo + kFlipBlock;
+    while (next_flip(cur, gb, lo, hi, c, g, h)) {
+        int code = c.type == 3 ? 1 : (c.type == 4 ? 3 : 2);  // X / Z / Y (flip_block's picks)
+        if (c.type == 0) {
+            const float r2 = nz_uniform(nz_mix(h ^ 0x5bd1e9955bd1e995ull));
+            code = r2 < 1.0f / 3.0f ? 1 : (r2 < 2.0f / 3.0f ? 2 : 3);
+        }
+        f((uint32_t)(g - lo), (uint32_t)code);
+    }
+}
+
+constexpr int kMapThreads = 128;
+__global__ __launch_bounds__(kMapThreads) void k_noise_map(MapArgs a) {
+    // LDS, word-major so consecutive threads hit consecutive banks: touched mask (16 words) and
+    // the codes of up to two blocks (32 words) of the current channel
+    __shared__ uint32_t tw[16][kMapThreads];
+    __shared__ uint32_t cw[32][kMapThreads];
+    const int t = threadIdx.x;
+    const uint64_t r = (uint64_t)blockIdx.x * kMapThreads + t;
+    const bool live = (r << kRegionLog) < a.amps;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) tw[i][t] = 0u;
+    if (live) {
+        const uint64_t k0 = r << kRegionLog;
+        for (int c = 0; c < a.nch; ++c) {
+            const FlipChan ch = a.ch[c];
+            const int q = ch.target;
+            if (q >= kRegionLog) {
+                // every amplitude of the region has bit q = side; its pairs: 512 consecutive
+                const int side = (int)((k0 >> q) & 1ull);
+                const uint64_t l0 = ((k0 >> (q + 1)) << q) | (k0 & ((1ull << q) - 1ull));
+                const uint64_t lb = l0 >> kFlipBlockLog;
+#pragma unroll
+                for (int i = 0; i < 32; ++i) cw[i][t] = 0u;
+                for (int h = 0; h < 2; ++h) {
+                    walk_block(a.blk0 + lb + (uint64_t)h, ch, [&](uint32_t l, uint32_t code) {
+                        const uint32_t o = (uint32_t)h * 256u + l;  // region offset (side fixed)
+                        tw[o >> 5][t] |= 1u << (o & 31u);
+                        cw[o >> 4][t] |= code << (2u * (o & 15u));
+                    });
+                }
+                if (side == 0) {  // the block's other region (side 1) walks it too, writes nothing
+                    uint4* dst = reinterpret_cast<uint4*>(a.codes + (uint64_t)c * a.cstride + (lb << 4));
+#pragma unroll
+                    for (int i = 0; i < 8; ++i)
+                        dst[i] = make_uint4(cw[4 * i][t], cw[4 * i + 1][t], cw[4 * i + 2][t], cw[4 * i + 3][t]);
+                }
+            } else {
+                // both members of the region's pairs lie in it: one block of 256 pairs
+                const uint64_t lb = r;
+#pragma unroll
+                for (int i = 0; i < 16; ++i) cw[i][t] = 0u;
+                walk_block(a.blk0 + lb, ch, [&](uint32_t l, uint32_t code) {
+                    const uint32_t lo = l & ((1u << q) - 1u);
+                    const uint32_t o0 = ((l ^ lo) << 1) | lo, o1 = o0 | (1u << q);
+                    tw[o0 >> 5][t] |= 1u << (o0 & 31u);
+                    tw[o1 >> 5][t] |= 1u << (o1 & 31u);
+                    cw[l >> 4][t] |= code << (2u * (l & 15u));
+                });
+                uint4* dst = reinterpret_cast<uint4*>(a.codes + (uint64_t)c * a.cstride + (lb << 4));
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    dst[i] = make_uint4(cw[4 * i][t], cw[4 * i + 1][t], cw[4 * i + 2][t], cw[4 * i + 3][t]);
+            }
+        }
+        uint4* td = reinterpret_cast<uint4*>(a.touched + (r << 4));
+#pragma unroll
+        for (int i = 0; i < 4; ++i) td[i] = make_uint4(tw[4 * i][t], tw[4 * i + 1][t], tw[4 * i + 2][t], tw[4 * i + 3][t]);
+    }
+}
+
+struct PullArgs {
+    const double2* src;
+    double2* dst;
+    const uint32_t* codes;
+    const uint32_t* touched;
+    uint64_t cstride;
+    uint64_t items;      // pairs (2x2 / diagonal) or amplitudes (SWAP / identity)
+    int nch;
+    int q[kMaxPullChannels];
+    int kind;            // K_M1, K_DIAG, K_SWAP, or -1: identity
+    int sub, t0, t1, d0_one;
+    uint64_t cmask;
+    double2 m[4];
+};
+
+// (P psi)[k]: untouched amplitudes are themselves; otherwise walk the channels last to first.
+__device__ __forceinline__ double2 pulled(const PullArgs& a, uint64_t k) {
+    if (!((a.touched[k >> 5] >> (k & 31ull)) & 1u)) return a.src[k];
+    int e = 0;  // phase i^e
+    for (int c = a.nch - 1; c >= 0; --c) {
+        const int q = a.q[c];
+        const uint64_t l = ((k >> (q + 1)) << q) | (k & ((1ull << q) - 1ull));
+        const uint32_t code = (a.codes[(uint64_t)c * a.cstride + (l >> 4)] >> (2u * (uint32_t)(l & 15ull))) & 3u;
+        if (!code) continue;
+        const int bit = (int)((k >> q) & 1ull);
+        if (code == 1) {  // X: v[k ^ 2^q]
+            k ^= 1ull << q;
+        } else if (code == 2) {  // Y: |0> <- -i v[k1], |1> <- +i v[k0]
+            e += bit ? 1 : 3;
+            k ^= 1ull << q;
+        } else if (bit) {  // Z: |1> <- -v[k1]
+            e += 2;
+        }
+    }
+    const double2 v = a.src[k];
+    switch (e & 3) {
+        case 1: return make_double2(-v.y, v.x);
+        case 2: return make_double2(-v.x, -v.y);
+        case 3: return make_double2(v.y, -v.x);
+        default: return v;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_pull_gate(PullArgs a) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.items; i += stride) {
+        if (a.kind == K_M1 || a.kind == K_DIAG) {
+            const uint64_t lo = i & ((1ull << a.t0) - 1ull);
+            const uint64_t j0 = ((i ^ lo) << 1) | lo, j1 = j0 | (1ull << a.t0);
+            double2 x0 = pulled(a, j0), x1 = pulled(a, j1);
+            if ((j0 & a.cmask) == a.cmask) {
+                if (a.kind == K_M1) {
+                    m1_pair(a.sub, a.m[0], a.m[1], a.m[2], a.m[3], x0, x1);
+                } else {
+                    x0 = diag_apply(a.sub, a.d0_one, a.m[0], a.m[1], 0, x0);
+                    x1 = diag_apply(a.sub, a.d0_one, a.m[0], a.m[1], 1, x1);
+                }
+            }
+            a.dst[j0] = x0;
+            a.dst[j1] = x1;
+        } else {
+            uint64_t s = i;
+            if (a.kind == K_SWAP && (i & a.cmask) == a.cmask) {
+                const uint64_t b0 = (i >> a.t0) & 1ull, b1 = (i >> a.t1) & 1ull;
+                if (b0 != b1) s = i ^ ((1ull << a.t0) | (1ull << a.t1));
+            }
+            a.dst[i] = pulled(a, s);
+        }
+    }
+}
+
+bool pull_noise_supported(int n, const std::vector<NoiseChan>& chans) {
+    const char* e = std::getenv("QSIM_NOISE_PULL");  // (read per run: tests switch it)
+    const bool on = e == nullptr || std::atoi(e) != 0;
+    if (!on || n < kRegionLog || chans.empty()) return false;
+    int live = 0;
+    for (const NoiseChan& c : chans) {
+        if (!(c.type == 0 || c.type >= 3)) return false;  // damping channels stream every pair
+        live += flip_probability(c.p) > 0.0;
+    }
+    return live <= kMaxPullChannels;
+}
+
+size_t pull_noise_codes_bytes(int n, uint64_t batch, size_t nch) {
+    return std::max<size_t>(1, nch) * ((batch << (n - 1)) / 16) * sizeof(uint32_t);
+}
+
+void launch_pull_noise_step(const double2* src, double2* dst, int n, uint64_t batch, uint64_t traj0,
+                            const std::vector<NoiseChan>& chans, uint64_t seed, uint64_t counter0,
+                            const Op* op, uint32_t* codes, uint32_t* touched, hipStream_t s, Timer* tm) {
+    const uint64_t amps = batch << n, pairs = amps >> 1;
+    const uint64_t idx0 = traj0 << (n - 1);
+    MapArgs m{};
+    m.codes = codes;
+    m.touched = touched;
+    m.amps = amps;
+    m.cstride = pairs / 16;
+    m.blk0 = idx0 >> kFlipBlockLog;
+    PullArgs a{};
+    uint64_t counter = counter0;
+    for (const NoiseChan& ch : chans) {
+        check_channel(n, ch.type, ch.qubit, ch.p);
+        const uint64_t key = noise_key(seed, counter++);
+        if (!flip_channel(ch.type, ch.qubit, ch.p, key, m.ch[m.nch])) continue;
+        if (m.nch >= kMaxPullChannels) fail(QSIM_ERR_RUNTIME, "too many channels for the pulled noise path");
+        a.q[m.nch] = ch.qubit;
+        ++m.nch;
+    }
+    a.nch = m.nch;
+    if (m.nch) {
+        TimedLaunch tl(tm, "noise_map", 0.0, s);
+        const uint64_t regions = amps >> kRegionLog;
+        hipLaunchKernelGGL(k_noise_map, dim3((unsigned)((regions + kMapThreads - 1) / kMapThreads)),
+                           dim3(kMapThreads), 0, s, m);
+        QSIM_HIPCHK(hipGetLastError());
+    } else {  // no channel can fire: every amplitude untouched
+        QSIM_HIPCHK(hipMemsetAsync(touched, 0, (amps / 32) * sizeof(uint32_t), s));
+    }
+    a.src = src;
+    a.dst = dst;
+    a.codes = codes;
+    a.touched = touched;
+    a.cstride = m.cstride;
+    a.kind = op ? op->kind : -1;
+    if (op) {
+        a.sub = op->sub;
+        a.t0 = op->t0;
+        a.t1 = op->t1;
+        a.d0_one = op->d0_one ? 1 : 0;
+        a.cmask = op->cmask;
+        for (int i = 0; i < 4; ++i) a.m[i] = make_double2(op->m[2 * i], op->m[2 * i + 1]);
+    }
+    a.items = (a.kind == K_M1 || a.kind == K_DIAG) ? pairs : amps;
+    const uint64_t blocks = std::min<uint64_t>((a.items + 255) / 256, 256ull * 64);
+    TimedLaunch tl(tm, "pull_gate", 32.0 * (double)amps, s);
+    hipLaunchKernelGGL(k_pull_gate, dim3((unsigned)blocks), dim3(256), 0, s, a);
     QSIM_HIPCHK(hipGetLastError());
 }
 

@@ -105,6 +105,65 @@ double reduce_norm(const double2* st, int n, int bit, double* d_partials, double
     return h;
 }
 
+// max over i of max(|re a_i - re b_i|, |im a_i - im b_i|): the per-component bar of the parity
+// tests (reference tests/test_gpu_cpu_equivalence.cu:26), computed where both states live (a
+// 30-qubit comparison would otherwise copy 32 GiB to the host).  Max is order-free: deterministic.
+__global__ __launch_bounds__(256) void k_maxdiff_partial(const double2* a, const double2* b,
+                                                         uint64_t count, double* partials) {
+    __shared__ double wmax[4];
+    double m = 0.0;
+    const uint64_t step = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += step) {
+        const double2 x = a[i], y = b[i];
+        const double d = fmax(fabs(x.x - y.x), fabs(x.y - y.y));
+        m = d > m || d != d ? d : m;  // (a NaN difference propagates)
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const double o = __shfl_down(m, off);
+        m = o > m || o != o ? o : m;
+    }
+    if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double r = wmax[0];
+        for (int w = 1; w < 4; ++w) r = wmax[w] > r || wmax[w] != wmax[w] ? wmax[w] : r;
+        partials[blockIdx.x] = r;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_max_partials(const double* partials, int count, double* result) {
+    __shared__ double wmax[4];
+    double m = 0.0;
+    for (int i = threadIdx.x; i < count; i += 256) m = partials[i] > m || partials[i] != partials[i] ? partials[i] : m;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const double o = __shfl_down(m, off);
+        m = o > m || o != o ? o : m;
+    }
+    if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double r = wmax[0];
+        for (int w = 1; w < 4; ++w) r = wmax[w] > r || wmax[w] != wmax[w] ? wmax[w] : r;
+        *result = r;
+    }
+}
+
+double reduce_max_abs_diff(const double2* a, const double2* b, int n, double* d_partials, double* d_result,
+                           hipStream_t s) {
+    const uint64_t count = 1ull << n;
+    const int blocks = (int)std::min<uint64_t>((count + 255) / 256, kReduceBlocks);
+    hipLaunchKernelGGL(k_maxdiff_partial, dim3(blocks), dim3(256), 0, s, a, b, count, d_partials);
+    QSIM_HIPCHK(hipGetLastError());
+    hipLaunchKernelGGL(k_max_partials, dim3(1), dim3(256), 0, s, d_partials, blocks, d_result);
+    QSIM_HIPCHK(hipGetLastError());
+    double h = 0.0;
+    QSIM_HIPCHK(hipMemcpyAsync(&h, d_result, sizeof(double), hipMemcpyDeviceToHost, s));
+    QSIM_HIPCHK(hipStreamSynchronize(s));
+    return h;
+}
+
 __global__ __launch_bounds__(256) void k_collapse(double2* st, uint64_t count, int bit, int result,
                                                   double scale) {
     const uint64_t step = (uint64_t)gridDim.x * blockDim.x;

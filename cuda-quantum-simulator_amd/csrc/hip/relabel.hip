@@ -46,6 +46,10 @@ bool relabel_enabled(int n) {
     relabel_defaults();
     return g_relabel.load() != 0 && n >= g_relabel_min.load();
 }
+bool relabel_mode_on() {
+    relabel_defaults();
+    return g_relabel.load() != 0;
+}
 void relabel_configure(int mode, int min_qubits) {
     relabel_defaults();
     if (mode >= 0) g_relabel.store(mode);
@@ -114,6 +118,10 @@ bool relabel_calibrate(int n) {
         g_calib_min.store(e ? std::atoi(e) : 26);
     }
     return g_calib.load() != 0 && n >= g_calib_min.load() && jit_mode() == 2;
+}
+bool calibrate_mode_on() {
+    relabel_calibrate(0);  // defaults first
+    return g_calib.load() != 0;
 }
 void calibrate_configure(int mode, int min_qubits) {
     relabel_calibrate(0);  // defaults first

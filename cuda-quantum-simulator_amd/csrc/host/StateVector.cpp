@@ -117,6 +117,18 @@ double StateVector::getTotalProbability() const {
     return t;
 }
 
+double StateVector::maxAbsDiff(const StateVector& other) const {
+    double d = 0.0;
+    check(qsim_state_max_abs_diff(h_, other.h_, &d));
+    return d;
+}
+
+size_t StateVector::getDeviceMemoryBytes() const {
+    uint64_t b = 0;
+    check(qsim_state_memory_bytes(h_, &b));
+    return (size_t)b;
+}
+
 bool StateVector::isNormalized(double tolerance) const {
     return std::abs(getTotalProbability() - 1.0) <= tolerance;
 }

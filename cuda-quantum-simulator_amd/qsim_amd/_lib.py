@@ -124,6 +124,8 @@ _sig(hip, "qsim_state_total_probability", [_P, POINTER(c_double)])
 _sig(hip, "qsim_state_prob_bit_zero", [_P, c_int, POINTER(c_double)])
 _sig(hip, "qsim_state_collapse", [_P, c_int, c_int, c_double])
 _sig(hip, "qsim_state_sample", [_P, _P, c_int, _P])
+_sig(hip, "qsim_state_max_abs_diff", [_P, _P, POINTER(c_double)])
+_sig(hip, "qsim_state_memory_bytes", [_P, POINTER(c_uint64)])
 _sig(hip, "qsim_state_profile", [_P, c_int])
 _sig(hip, "qsim_state_profile_count", [_P, POINTER(c_int)])
 _sig(hip, "qsim_state_profile_get", [_P, c_int, c_char_p, c_size_t, POINTER(c_double),

@@ -81,6 +81,21 @@ def set_tile_rb7(rb: int = -1) -> None:
     _lib.check(_lib.hip.qsim_set_tile_rb7(rb))
 
 
+# The shipped policy (include/qsim_hip.h; environment variables unset).
+DEFAULTS = {"jit": (1, 20), "relabel": (1, 26), "relayout": (1, 20), "calibrate": (1, 26)}
+
+
+def restore_defaults() -> None:
+    """Put every process-wide planning policy back to the shipped defaults: background JIT from
+    20 qubits, relabeling from 26, relayout plans from 20, calibrated first runs from 26 (with
+    inline compilation), the size rule for tile heights (tests call this after changing any)."""
+    set_jit(*DEFAULTS["jit"])
+    set_relabel(*DEFAULTS["relabel"])
+    set_relayout(*DEFAULTS["relayout"])
+    set_calibrate(*DEFAULTS["calibrate"])
+    set_tile_height(-1)
+
+
 def plan_relabel(circuit: Circuit):
     """(perm, predicted_us_before, predicted_us_after): the logical -> physical qubit map the
     engine would choose for this circuit's fused plan (identity when none pays), host only."""

@@ -127,6 +127,20 @@ class StateVector:
         if abs(t - 1.0) > tolerance:
             raise RuntimeError(f"State vector not normalized: total probability = {t}")
 
+    def maxAbsDiff(self, other: "StateVector") -> float:
+        """Larger per-component |a - b| against another state of the same size, computed on the
+        device in the identity layout (qsim_state_max_abs_diff; the reference's 1e-12 per-component
+        bar, tests/test_gpu_cpu_equivalence.cu:26, without a host copy)."""
+        d = _c.c_double()
+        _lib.check(_lib.hip.qsim_state_max_abs_diff(self._h, other._h, _c.byref(d)))
+        return d.value
+
+    def getDeviceMemoryBytes(self) -> int:
+        """Device bytes this state owns now, the relayout plans' second buffer included."""
+        b = _c.c_uint64()
+        _lib.check(_lib.hip.qsim_state_memory_bytes(self._h, _c.byref(b)))
+        return b.value
+
     def probBitZero(self, bit: int) -> float:
         p = _c.c_double()
         _lib.check(_lib.hip.qsim_state_prob_bit_zero(self._h, bit, _c.byref(p)))

@@ -54,6 +54,11 @@ public:
     std::vector<double> getProbabilities() const;
     double getTotalProbability() const;  // device wave64 reduction
     bool isNormalized(double tolerance = 1e-10) const;
+    // Extensions (no reference counterpart): the larger per-component |a - b| against another
+    // state of the same size, on the device; the device bytes this state owns now
+    // (qsim_state_max_abs_diff / qsim_state_memory_bytes).
+    double maxAbsDiff(const StateVector& other) const;
+    size_t getDeviceMemoryBytes() const;
     void assertNormalized(double tolerance = 1e-10) const;  // std::runtime_error
 
     // Reference semantics (src/StateVector.cu:260-314): measures index bit n-1-qubit

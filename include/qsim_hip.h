@@ -167,12 +167,16 @@ int qsim_state_restore_layout(qsim_state* s);
 /* Whether the state's first fused run chose a relayout plan (no reference counterpart): every
  * 12-qubit tile pass stores its tile under the next pass's qubit layout, so each pass picks all
  * of its tile qubits except the four of the contiguous run (fewer passes); the last pass restores
- * the first layout.  QSIM_RELAYOUT=0 disables them (QSIM_RELAYOUT_MIN_QUBITS, default 20). */
+ * the first layout.  QSIM_RELAYOUT=0 disables them (QSIM_RELAYOUT_MIN_QUBITS, default 20).
+ * Relayout passes write out of place into a second 2^n buffer: a first run only considers them
+ * when the device has room for it (otherwise the fixed-layout plan runs in place), and the buffer
+ * is freed again unless the run keeps a relayout plan (qsim_state_memory_bytes). */
 int qsim_state_relayout(qsim_state* s, int* relayout);
 /* Relayout plans on (mode 1: when they need fewer passes, or win the device timing with
  * calibration) / off (0) / forced (2: whenever one exists — tests) for first runs from now on, for
- * states of at least min_qubits qubits (relabeling must be enabled too); negative arguments leave
- * a setting unchanged. */
+ * states of at least min_qubits qubits; they permute qubit labels, so relabeling mode 0
+ * (qsim_set_relabel / QSIM_RELABEL=0) turns them off too, whatever the state's size; negative
+ * arguments leave a setting unchanged. */
 int qsim_set_relayout(int mode, int min_qubits);
 /* Host-only: compile the relayout plan's pass kernels with hipRTC for gfx950 (no GPU needed);
  * code_bytes: the code object's size.  QSIM_ERR_RUNTIME when there is no relayout plan. */
@@ -233,6 +237,15 @@ int qsim_state_collapse(qsim_state* s, int bit, int result, double scale);
 /* Draw `shots` basis indices from |a|^2 with uniforms u[i] in [0,1) supplied by the caller
  * (host RNG keeps the reference's mt19937 stream): device CDF + binary search. */
 int qsim_state_sample(qsim_state* s, const double* uniforms, int shots, int64_t* out);
+/* max_i max(|Re a_i - Re b_i|, |Im a_i - Im b_i|) of two states of the same size on the same
+ * device, both read in the identity qubit layout, computed on the device (no reference
+ * counterpart: tests/test_gpu_cpu_equivalence.cu:26 compares per component on the host, which at
+ * 30 qubits would copy 32 GiB).  NaN when any difference is NaN. */
+int qsim_state_max_abs_diff(qsim_state* a, qsim_state* b, double* out);
+/* Device bytes the state owns now: the 2^n x 16 B amplitudes, the second buffer a relayout plan
+ * writes into (same size; allocated on a first run only when the device has room for it, freed
+ * when the run does not keep a relayout plan), reduction and plan buffers, readout scratch. */
+int qsim_state_memory_bytes(qsim_state* s, uint64_t* bytes);
 
 /* ---- timing (bench / profiling) ---- */
 /* Enable per-launch HIP-event timing on the state's stream; kernels are attributed by name. */

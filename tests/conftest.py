@@ -34,6 +34,16 @@ def pytest_collection_modifyitems(config, items):
     items[:] = first + rest
 
 
+@pytest.fixture(autouse=True)
+def _shipped_policy():
+    """Every test starts from, and leaves, the engine's shipped planning defaults (a test that
+    lowers a threshold must not make later tests run non-default paths)."""
+    yield
+    if "qsim_amd" in sys.modules:
+        from qsim_amd.plan import restore_defaults
+        restore_defaults()
+
+
 @pytest.fixture(scope="session")
 def qsim():
     import qsim_amd

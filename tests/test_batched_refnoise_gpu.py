@@ -114,8 +114,10 @@ def test_reference_compatible_profile_cpp_names(qsim, gpu_ready):
 def test_reference_noise_one_launch_per_gate(qsim, oracle, gpu_ready, monkeypatch, n, B, seed, traj0):
     """All Depolarizing passes after a gate in ONE launch (k_noise_units: a work-group per unit
     of whole trajectories, channels in order between work-group barriers), forced here at oracle
-    sizes (QSIM_NOISE_UNIT_MIN=1), also on a trajectory shard whose pairs start mid-block."""
+    sizes (QSIM_NOISE_UNIT_MIN=1), also on a trajectory shard whose pairs start mid-block.
+    (The push kernels: the pulled path, default from 9 qubits, is switched off here.)"""
     monkeypatch.setenv("QSIM_NOISE_UNIT_MIN", "1")
+    monkeypatch.setenv("QSIM_NOISE_PULL", "0")
     c = _circuit(qsim, n, 12, seed)
     nm = qsim.NoiseModel()
     nm.addDepolarizingAll(n, 0.2)
@@ -137,6 +139,7 @@ def test_reference_noise_one_launch_equals_per_channel_16q(qsim, gpu_ready, monk
     nm = qsim.NoiseModel()
     nm.addDepolarizingAll(n, 0.01)
     out = []
+    monkeypatch.setenv("QSIM_NOISE_PULL", "0")
     for unit_min in ("128", str(1 << 40)):
         monkeypatch.setenv("QSIM_NOISE_UNIT_MIN", unit_min)
         s = qsim.BatchedSimulator(n, B, nm, noise=qsim.BatchedNoise.Reference)
@@ -145,3 +148,62 @@ def test_reference_noise_one_launch_equals_per_channel_16q(qsim, gpu_ready, monk
         out.append(np.stack([s.getStateVector(t) for t in (0, 77, 255)]))
     assert np.array_equal(out[0], out[1])
     assert abs(np.sum(np.abs(out[0][1]) ** 2) - 1.0) < 1e-10
+
+
+# ---- pulled noise (noise.hip: k_noise_map + k_pull_gate, the default from 9 qubits) ----------
+# The flips after gate i are applied by gate i+1's pass, reading its inputs through the noise
+# permutation out of place; the flips after the last gate by one identity pass.  Same draws as
+# the push kernels, so the states are the push path's and the oracle's.
+
+@pytest.mark.parametrize("n,B,seed,traj0,refgates", [(9, 6, 5, 2, False), (10, 4, 8, 0, True),
+                                                     (12, 3, 6, 5, False), (14, 2, 11, 1, False)])
+def test_pulled_noise_matches_oracle(qsim, oracle, gpu_ready, n, B, seed, traj0, refgates):
+    c = _circuit(qsim, n, 14, seed)
+    nm = qsim.NoiseModel()
+    nm.addDepolarizingAll(n, 0.2)
+    s = qsim.BatchedSimulator(n, B, nm, noise=qsim.BatchedNoise.Reference,
+                              gate_set=qsim.BatchedGateSet.Reference if refgates else qsim.BatchedGateSet.Full)
+    s.setSeed(seed)
+    s.setTrajectoryOffset(traj0)
+    entries = [(0, q, 0.2) for q in range(n)]
+    whole, counter = None, 0
+    for _ in range(2):  # the second run continues the pass counter from the first's end
+        s.run(c)
+        whole, counter = oracle.batched_reference_run(n, traj0 + B, oracle.gates_of(c), entries, seed,
+                                                      refgates, states=whole, counter=counter)
+    for t in range(B):
+        np.testing.assert_allclose(s.getStateVector(t), whole[traj0 + t], atol=1e-12, rtol=0)
+
+
+def test_pulled_noise_equals_push_16q(qsim, gpu_ready, monkeypatch):
+    """BASELINE config-4 shape (16 qubits, depolarizing 0.01 on every qubit, W-HC): pulled and
+    pushed noise give bit-identical trajectories; also through a pinned device pointer."""
+    n, B = 16, 128
+    c = qsim.createRandomHCCircuit(n, 30, 42)
+    nm = qsim.NoiseModel()
+    nm.addDepolarizingAll(n, 0.01)
+    out = []
+    for pull in ("1", "0"):
+        monkeypatch.setenv("QSIM_NOISE_PULL", pull)
+        s = qsim.BatchedSimulator(n, B, nm, noise=qsim.BatchedNoise.Reference)
+        s.setSeed(9)
+        s.run(c)
+        s.run(c)
+        out.append(np.stack([s.getStateVector(t) for t in (0, 63, 127)]))
+        s.close()
+    assert np.array_equal(out[0], out[1])
+    assert abs(np.sum(np.abs(out[0][1]) ** 2) - 1.0) < 1e-10
+    # a raw pointer handed out: the pulled run copies its result back where it points
+    monkeypatch.setenv("QSIM_NOISE_PULL", "1")
+    s = qsim.BatchedSimulator(n, B, nm, noise=qsim.BatchedNoise.Reference)
+    s.setSeed(9)
+    from qsim_amd import _lib
+    import ctypes
+    ptr = ctypes.c_void_p()
+    _lib.check(_lib.hip.qsim_batch_device_ptr(s._h, ctypes.byref(ptr)))
+    s.run(c)
+    s.run(c)
+    ptr2 = ctypes.c_void_p()
+    _lib.check(_lib.hip.qsim_batch_device_ptr(s._h, ctypes.byref(ptr2)))
+    assert ptr.value == ptr2.value
+    assert np.array_equal(np.stack([s.getStateVector(t) for t in (0, 63, 127)]), out[0])

@@ -145,3 +145,21 @@ def test_noise_free_run_is_fused_and_exact(qsim, oracle, gpu_ready):
                                atol=1e-12, rtol=0)
     with pytest.raises(IndexError):
         sim.applyNoiseToQubit(qsim.NoiseType.BitFlip, n, 0.5)
+
+
+@pytest.mark.parametrize("n,seed,types", [(10, 4, (0, 3, 4, 5)), (12, 5, (0, 0, 5, 3)), (11, 6, (0, 1, 3))])
+def test_pulled_flip_noise_matches_oracle(qsim, oracle, gpu_ready, n, seed, types):
+    """From 9 qubits, flip-only noise models run pulled (the noise after gate i applied by gate
+    i+1's pass, out of place; noise.hip) — exactly the oracle's per-pair passes.  A damping
+    channel in the model keeps the per-channel passes (third case)."""
+    rng = np.random.default_rng(seed)
+    c = qsim.createRandomCircuit(n, 16, seed)
+    channels = [(int(t), int(rng.integers(0, n)), float(rng.uniform(0.1, 0.5))) for t in types]
+    sim = qsim.NoisySimulator(n, _model(qsim, channels))
+    sim.setSeed(2000 + seed)
+    sim.run(c)
+    want, ctr = oracle.noisy_run(n, oracle.gates_of(c), channels, 2000 + seed)
+    np.testing.assert_allclose(sim.getStateVector(), want, atol=1e-12, rtol=0)
+    sim.run(c)
+    want2, _ = oracle.noisy_run(n, oracle.gates_of(c), channels, 2000 + seed, ctr, want)
+    np.testing.assert_allclose(sim.getStateVector(), want2, atol=1e-12, rtol=0)

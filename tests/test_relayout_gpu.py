@@ -23,10 +23,8 @@ def relayout_low():
     set_relayout(2, 22)  # forced: a relayout plan whenever one exists
     set_calibrate(0, -1)
     yield
-    set_relabel(1, 26)
-    set_relayout(1, 22)
-    set_calibrate(1, 28)
-    set_jit(1, 20)
+    from qsim_amd.plan import restore_defaults
+    restore_defaults()  # (the shipped thresholds: later tests must run the default paths)
 
 
 @pytest.mark.parametrize("jit", [0, 2])
