@@ -624,6 +624,7 @@ int qsim_batch_run(qsim_batch* b, const qsim_gate* gates, size_t count,
                 QSIM_HIPCHK(hipGetLastError());
             }
             if (!fops.empty()) {
+                const CtrlOutOff ctrl_off;  // (Pauli-frame passes: every control is a tile bit)
                 PlanCache::Entry& pe = b->plans.get(fops, b->n, b->stream);
                 const Plan& plan = pe.plan;
                 // circuit-specialised kernels for the passes no frame conjugation reaches (all of

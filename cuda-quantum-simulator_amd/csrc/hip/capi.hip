@@ -746,6 +746,10 @@ int qsim_set_tile_height(int h) {
     return guarded([&] { tile_height_configure(h); });
 }
 
+int qsim_set_tile_ctrl_out(int mode) {
+    return guarded([&] { tile_ctrl_out_configure(mode); });
+}
+
 int qsim_set_tile_rb7(int rb) {
     return guarded([&] { tile_rb7_configure(rb); });
 }

@@ -130,6 +130,10 @@ struct TileOp {            // an Op re-expressed in tile-index bits
     int step, tq;
     int cq[2], cpos[2], cb[2];
     int _pad;
+    // Tile-constant controls (tile_ctrl_out): physical positions outside the tile the op is
+    // controlled on — the tile's non-tile bits are fixed, so the op runs on a whole tile or not
+    // at all (a uniform branch on the tile's base address, no tile slot used).
+    uint64_t cm_out;
     double m[8];
 };
 // A stage of a staged tile pass: every thread holds the 2^rb amplitudes spanned by `fix` (the
@@ -185,8 +189,23 @@ constexpr int kTileR0 = 6;    // contiguous run bits of a staged tile (QSIM_TILE
 // avoid: qubits no tile may contain (ops never act on them; only tile padding is affected).
 Plan plan_fused(const std::vector<Op>& ops, int n, int hmax = -1, uint64_t avoid = 0);
 // One tile pass appended to a plan (fused.hip; plan_fused and the relayout planner use it).
+// bit_of[q] < 0: op qubit q is not a tile qubit (a tile-constant control); phys_of (null: the
+// identity) gives such a control's physical position under the pass's load layout.
 void append_tile_pass(Plan& plan, const std::vector<Op>& ops, int n, int h, int r0, const int* hpos,
-                      const int* bit_of, const int* st_pos, const int* st_tid);
+                      const int* bit_of, const int* st_pos, const int* st_tid, const int* phys_of = nullptr);
+// Tile-constant controls (QSIM_TILE_CTRL_OUT, default 1; qsim_set_tile_ctrl_out): a control
+// qubit need not be a tile qubit — planners then only require an op's targets in the tile.
+// Off for the calling thread inside a CtrlOutOff scope (batched Pauli-frame plans).
+bool tile_ctrl_out();
+void tile_ctrl_out_configure(int mode);
+struct CtrlOutOff {
+    CtrlOutOff();
+    ~CtrlOutOff();
+    CtrlOutOff(const CtrlOutOff&) = delete;
+    CtrlOutOff& operator=(const CtrlOutOff&) = delete;
+  private:
+    bool prev_;
+};
 // Relayout plans (relayout.hip): every pass stores its tile under the next pass's layout, so
 // each pass may choose all of its tile qubits except the four of the contiguous run, which come
 // from the pass before (the last pass restores the first layout, so re-runs need no restore).

@@ -43,6 +43,13 @@ static uint64_t op_qubits(const Op& op) {
     if (op.kind == K_SWAP) m |= 1ull << op.t1;
     return m;
 }
+// The qubits a tile must hold for `op` (its targets with tile-constant controls, else all).
+static uint64_t op_need(const Op& op, bool ctrl_out) {
+    if (!ctrl_out) return op_qubits(op);
+    uint64_t m = 1ull << op.t0;
+    if (op.kind == K_SWAP) m |= 1ull << op.t1;
+    return m;
+}
 
 static TileOp make_tile_op(int kind, int sub, int b0, int b1, uint32_t cm, int d0_one,
                            const double* m) {
@@ -165,7 +172,10 @@ static void plan_stages(std::vector<TileOp>& pass_ops, std::vector<int>& pass_sr
             ops.push_back(make_tile_op(K_M1, S_X, t.b1, -1, t.cmask | a, 0, xm));
             ops.push_back(make_tile_op(K_M1, S_X, t.b0, -1, t.cmask | b, 0, xm));
             ops.push_back(make_tile_op(K_M1, S_X, t.b1, -1, t.cmask | a, 0, xm));
-            for (int k = 1; k <= 3; ++k) ops[ops.size() - k].step = t.step;
+            for (int k = 1; k <= 3; ++k) {
+                ops[ops.size() - k].step = t.step;
+                ops[ops.size() - k].cm_out = t.cm_out;
+            }
             src.push_back(pass_src[i]);  // the gate is reported once (introspection skips -1)
             src.push_back(-1);
             src.push_back(-1);
@@ -181,7 +191,7 @@ static void plan_stages(std::vector<TileOp>& pass_ops, std::vector<int>& pass_sr
             // unnormalized butterfly in the staged kernel: each one scales the tile's 2-norm by
             // exactly sqrt2, so at most kMaxUnnormH per pass bounds the growth to 2^(kMaxUnnormH/2)
             // (no overflow for any state of norm < 2^700); further H run as the normalised matrix
-            if (t.cmask == 0 && p.hu_count < kMaxUnnormH) ++p.hu_count;
+            if (t.cmask == 0 && t.cm_out == 0 && p.hu_count < kMaxUnnormH) ++p.hu_count;
             else t.sub = S_GEN;  // (also controlled H, not in the gate set; keep it exact)
         }
     }
@@ -360,16 +370,17 @@ struct PassChoice {
 static std::vector<PassChoice> choose_passes(const std::vector<Op>& ops, int n, int r0, int nfree,
                                              bool lookahead, uint64_t avoid) {
     const uint64_t low = (1ull << r0) - 1ull;
+    const bool co = tile_ctrl_out() && nfree + r0 >= 10;  // (staged tiles only)
     std::vector<PassChoice> out;
     std::vector<Op> rem = ops;
-    std::vector<uint64_t> qm;
+    std::vector<uint64_t> qm, nm;
     const size_t window = 512;  // gates scored per candidate (later ones are almost always blocked)
     auto score = [&](uint64_t allowed) {
         uint64_t blocked = 0;
         int c = 0;
         const size_t m = std::min(qm.size(), window);
         for (size_t i = 0; i < m; ++i) {
-            if ((qm[i] & blocked) == 0 && (qm[i] & ~allowed) == 0) ++c;
+            if ((qm[i] & blocked) == 0 && (nm[i] & ~allowed) == 0) ++c;
             else blocked |= qm[i];
         }
         return c;
@@ -377,7 +388,7 @@ static std::vector<PassChoice> choose_passes(const std::vector<Op>& ops, int n, 
     while (!rem.empty()) {
         // The first remaining gate is never blocked; if it needs more qubits than the tile's free
         // slots it runs as a per-gate step (keeps program order, guarantees progress).
-        if (__builtin_popcountll(op_qubits(rem.front()) & ~low) > nfree) {
+        if (__builtin_popcountll(op_need(rem.front(), co) & ~low) > nfree) {
             PassChoice c;
             c.single = true;
             c.ops.push_back(rem.front());
@@ -388,7 +399,11 @@ static std::vector<PassChoice> choose_passes(const std::vector<Op>& ops, int n, 
         uint64_t hi = 0;
         if (lookahead) {
             qm.resize(rem.size());
-            for (size_t i = 0; i < rem.size(); ++i) qm[i] = op_qubits(rem[i]);
+            nm.resize(rem.size());
+            for (size_t i = 0; i < rem.size(); ++i) {
+                qm[i] = op_qubits(rem[i]);
+                nm[i] = op_need(rem[i], co);
+            }
             while (__builtin_popcountll(hi) < nfree) {
                 const int base = score(low | hi);
                 int best = 2 * base + 1, bq = -1;  // key 2 * score + (not avoided)
@@ -415,13 +430,13 @@ static std::vector<PassChoice> choose_passes(const std::vector<Op>& ops, int n, 
                 if (pa < 0) break;
                 hi |= (1ull << pa) | (1ull << pb);
             }
-            if (score(low | hi) == 0) hi = op_qubits(rem.front()) & ~low;  // (3-qubit first gate)
+            if (score(low | hi) == 0) hi = op_need(rem.front(), co) & ~low;  // (3-qubit first gate)
         }
         PassChoice c;
         uint64_t blocked = 0;
         std::vector<Op> deferred;
         for (const Op& op : rem) {
-            const uint64_t q = op_qubits(op), qh = q & ~low;
+            const uint64_t q = op_qubits(op), qh = op_need(op, co) & ~low;
             const bool fits = lookahead ? (qh & ~hi) == 0 : __builtin_popcountll(hi | qh) <= nfree;
             if ((q & blocked) == 0 && fits) {
                 if (!lookahead) hi |= qh;
@@ -449,8 +464,12 @@ static std::vector<PassChoice> choose_passes(const std::vector<Op>& ops, int n, 
 static std::vector<PassChoice> beam_passes(const std::vector<Op>& ops, int n, int heff, int width,
                                            uint64_t avoid) {
     const size_t window = 512;
-    std::vector<uint64_t> qm(ops.size());
-    for (size_t i = 0; i < ops.size(); ++i) qm[i] = op_qubits(ops[i]);
+    const bool co = tile_ctrl_out();
+    std::vector<uint64_t> qm(ops.size()), nm(ops.size());
+    for (size_t i = 0; i < ops.size(); ++i) {
+        qm[i] = op_qubits(ops[i]);
+        nm[i] = op_need(ops[i], co);
+    }
     auto run_mask = [](int r0) { return (1ull << r0) - 1ull; };
     // (admitted, partly covered) over the first `window` remaining gates
     auto score = [&](const std::vector<int>& rem, uint64_t allowed, uint64_t low) {
@@ -458,13 +477,13 @@ static std::vector<PassChoice> beam_passes(const std::vector<Op>& ops, int n, in
         int full = 0, part = 0;
         const size_t m = std::min(rem.size(), window);
         for (size_t i = 0; i < m; ++i) {
-            const uint64_t q = qm[rem[i]];
+            const uint64_t q = qm[rem[i]], nd = nm[rem[i]];
             if (q & blocked) {
                 blocked |= q;
-            } else if ((q & ~allowed) == 0) {
+            } else if ((nd & ~allowed) == 0) {
                 ++full;
             } else {
-                if (q & allowed & ~low) ++part;
+                if (nd & allowed & ~low) ++part;
                 blocked |= q;
             }
         }
@@ -475,7 +494,7 @@ static std::vector<PassChoice> beam_passes(const std::vector<Op>& ops, int n, in
         uint64_t blocked = 0;
         for (int i : rem) {
             const uint64_t q = qm[i];
-            if ((q & blocked) == 0 && (q & ~allowed) == 0) continue;
+            if ((q & blocked) == 0 && (nm[i] & ~allowed) == 0) continue;
             out.push_back(i);
             blocked |= q;
         }
@@ -521,7 +540,7 @@ static std::vector<PassChoice> beam_passes(const std::vector<Op>& ops, int n, in
                     uint64_t blocked = 0;
                     for (const Op& op : rest) {
                         const uint64_t q = op_qubits(op);
-                        if ((q & blocked) == 0 && (q & ~allowed) == 0) {
+                        if ((q & blocked) == 0 && (op_need(op, co) & ~allowed) == 0) {
                             c.ops.push_back(op);
                         } else {
                             deferred.push_back(op);
@@ -540,7 +559,7 @@ static std::vector<PassChoice> beam_passes(const std::vector<Op>& ops, int n, in
             for (int r0 = 6; r0 >= 4; --r0) {
                 const uint64_t low = run_mask(r0);
                 const int nfree = 6 + heff - r0;
-                const uint64_t seed = qm[s.rem.front()] & ~low;
+                const uint64_t seed = nm[s.rem.front()] & ~low;
                 if (__builtin_popcountll(seed) > nfree) continue;
                 std::vector<std::pair<int, uint64_t>> part = {{score(s.rem, low | seed, low), seed}};
                 for (int k = __builtin_popcountll(seed); k < nfree; ++k) {
@@ -709,8 +728,25 @@ void tile_height_configure(int h) {
 // positions 0..r0-1, tile bits r0.. are hpos[] (ascending); bit_of[q] is the tile bit of qubit q
 // as the ops name it.  st_pos / st_tid (relayout passes, relayout.hip; null otherwise): store
 // positions of the tile bits and of the tile-id bits.
+static std::atomic<int> g_ctrl_out{-1};
+static thread_local bool t_ctrl_off = false;
+bool tile_ctrl_out() {
+    if (t_ctrl_off) return false;
+    if (g_ctrl_out.load() < 0) {
+        const char* e = std::getenv("QSIM_TILE_CTRL_OUT");
+        g_ctrl_out.store(e ? (std::atoi(e) != 0 ? 1 : 0) : 1);
+    }
+    return g_ctrl_out.load() != 0;
+}
+void tile_ctrl_out_configure(int mode) {
+    tile_ctrl_out();
+    if (mode >= 0) g_ctrl_out.store(mode ? 1 : 0);
+}
+CtrlOutOff::CtrlOutOff() : prev_(t_ctrl_off) { t_ctrl_off = true; }
+CtrlOutOff::~CtrlOutOff() { t_ctrl_off = prev_; }
+
 void append_tile_pass(Plan& plan, const std::vector<Op>& ops, int n, int h, int r0, const int* hpos,
-                      const int* bit_of, const int* st_pos, const int* st_tid) {
+                      const int* bit_of, const int* st_pos, const int* st_tid, const int* phys_of) {
     FusedPass p;
     p.h = h;
     p.r0 = r0;
@@ -729,11 +765,18 @@ void append_tile_pass(Plan& plan, const std::vector<Op>& ops, int n, int h, int 
     std::vector<int> tsrc;
     for (const Op& op : ops) {
         uint32_t cm = 0;
+        uint64_t cm_out = 0;
         for (int q = 0; q < n; ++q)
-            if ((op.cmask >> q) & 1ull) cm |= 1u << bit_of[q];
+            if ((op.cmask >> q) & 1ull) {
+                if (bit_of[q] >= 0) cm |= 1u << bit_of[q];
+                else cm_out |= 1ull << (phys_of ? phys_of[q] : q);
+            }
         int b0 = bit_of[op.t0], b1 = op.kind == K_SWAP ? bit_of[op.t1] : -1;
+        if (b0 < 0 || (op.kind == K_SWAP && b1 < 0)) fail(QSIM_ERR_RUNTIME, "tile pass: target outside the tile");
+        if (cm_out && h < 4) fail(QSIM_ERR_RUNTIME, "tile-constant controls need staged tiles");
         if (op.kind == K_SWAP && b0 > b1) std::swap(b0, b1);
         tops.push_back(make_tile_op(op.kind, op.sub, b0, b1, cm, op.d0_one ? 1 : 0, op.m));
+        tops.back().cm_out = cm_out;
         tops.back().step = op.src;
         tsrc.push_back(op.src);
     }
@@ -806,10 +849,7 @@ Plan plan_fused(const std::vector<Op>& ops, int n, int hmax, uint64_t avoid) {
         static const bool mix = env_int("QSIM_TILE_MIX", 1) != 0;
         if (heff == 7 && mix) {
             uint64_t need = 0;
-            for (const Op& op : ch.ops) {
-                need |= op.cmask | (1ull << op.t0);
-                if (op.kind == K_SWAP) need |= 1ull << op.t1;
-            }
+            for (const Op& op : ch.ops) need |= op_need(op, tile_ctrl_out());
             for (int r = 6; r >= 4; --r) {
                 const uint64_t above = need & ~((1ull << r) - 1ull);
                 if (__builtin_popcountll(above) <= 12 - r) {
@@ -830,6 +870,7 @@ Plan plan_fused(const std::vector<Op>& ops, int n, int hmax, uint64_t avoid) {
         for (int q = r0; q < n && __builtin_popcountll(hi) < nfree; ++q) hi |= 1ull << q;
         int hpos[kHposMax] = {0}, bit_of[64];
         int k = 0;
+        for (int q = 0; q < 64; ++q) bit_of[q] = -1;
         for (int q = 0; q < r0; ++q) bit_of[q] = q;
         for (int q = r0; q < n; ++q)
             if ((hi >> q) & 1ull) {
@@ -1303,7 +1344,13 @@ __global__ __launch_bounds__((64 << H) >> RBT, H >= 7 ? 1 : 2) void k_fused_stag
                 else stage_op_frame<RB>(v, jb, op, a.frames, a.nbatch, traj);
             }
         } else {
-            for (int o = sg.op_begin; o < sg.op_end; ++o) stage_op<RB>(v, jb, ldc(a.ops, o));
+            for (int o = sg.op_begin; o < sg.op_end; ++o) {
+                const TileOp op = ldc(a.ops, o);
+                // tile-constant controls: the tile's non-tile bits decide for the whole tile
+                // (uniform: the load base holds them, incl. a sub-space launch's fixed bits)
+                if ((base & op.cm_out) != op.cm_out) continue;
+                stage_op<RB>(v, jb, op);
+            }
         }
         if (s == se - 1) {
             uint64_t gb;
@@ -1412,8 +1459,10 @@ double2* launch_fused(double2* st, int n, uint64_t batch, const Plan& plan, cons
         bool framed = false;  // does any op of this pass run conjugated by the Pauli frame?
         if (frames)
             for (int k = p.stage_begin; k < p.stage_end && !framed; ++k)
-                for (int o = plan.stages[k].op_begin; o < plan.stages[k].op_end; ++o)
+                for (int o = plan.stages[k].op_begin; o < plan.stages[k].op_end; ++o) {
                     if (plan.ops[o].step >= 0) framed = true;
+                    if (plan.ops[o].cm_out) fail(QSIM_ERR_RUNTIME, "Pauli-frame pass with a tile-constant control");
+                }
         if (framed) {  // batched noisy run: non-Clifford ops under the trajectory's Pauli frame
             // the framed kernels exist at the default stage width only (their stage descriptors
             // must have been built for it)

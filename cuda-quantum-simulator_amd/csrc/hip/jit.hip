@@ -136,6 +136,19 @@ struct Gen {
     }
 
     void op(const TileOp& t) {
+        if (t.cm_out) {  // tile-constant controls: one uniform branch on the tile's load base
+            o << "  if ((base & " << hexu(t.cm_out) << ") == " << hexu(t.cm_out) << ") {\n";
+            const bool prev = no_rename;
+            no_rename = true;  // (register names must agree on both paths)
+            op_body(t);
+            no_rename = prev;
+            o << "  }\n";
+            return;
+        }
+        op_body(t);
+    }
+    bool no_rename = false;
+    void op_body(const TileOp& t) {
         const uint32_t cr = t.cm_reg;
         std::string pred;  // per-thread control predicate (thread-bit controls)
         if (t.cm_thr) {
@@ -170,7 +183,7 @@ struct Gen {
             if ((r >> P) & 1) continue;
             if ((r & cr) != cr) continue;  // register-bit controls: decided here, not on the GPU
             const int r1 = r | (1 << P);
-            if (t.sub == S_X && pred.empty()) {  // a relabel: no instruction at all
+            if (t.sub == S_X && pred.empty() && !no_rename) {  // a relabel: no instruction at all
                 std::swap(nm[r], nm[r1]);
                 continue;
             }

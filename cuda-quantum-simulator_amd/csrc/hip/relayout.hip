@@ -52,9 +52,19 @@ uint64_t op_mask(const Op& op) {
     return m;
 }
 
+// Qubits an op needs inside the tile: its targets; with tile-id controls (QSIM_TILE_CTRL_OUT) a
+// control outside the tile is a tile constant (the op runs on the tiles where it reads 1).
+uint64_t op_need(const Op& op, bool ctrl_out) {
+    if (!ctrl_out) return op_mask(op);
+    uint64_t m = 1ull << op.t0;
+    if (op.kind == K_SWAP) m |= 1ull << op.t1;
+    return m;
+}
+
 struct Search {
-    const std::vector<uint64_t>& qm;
+    const std::vector<uint64_t>& qm;   // every qubit of the op (ordering: ops on disjoint qubits commute)
     int n;
+    const std::vector<uint64_t>& need;  // the qubits the tile must hold
     size_t window = 512;
 
     // (gates admitted, gates partly covered) over the first `window` remaining gates
@@ -63,13 +73,13 @@ struct Search {
         int full = 0, part = 0;
         const size_t m = std::min(rem.size(), window);
         for (size_t i = 0; i < m; ++i) {
-            const uint64_t q = qm[rem[i]];
+            const uint64_t q = qm[rem[i]], nd = need[rem[i]];
             if (q & blocked) {
                 blocked |= q;
-            } else if ((q & ~allowed) == 0) {
+            } else if ((nd & ~allowed) == 0) {
                 ++full;
             } else {
-                if (q & allowed) ++part;
+                if (nd & allowed) ++part;
                 blocked |= q;
             }
         }
@@ -82,7 +92,7 @@ struct Search {
         uint64_t blocked = 0;
         for (int i : rem) {
             const uint64_t q = qm[i];
-            if ((q & blocked) == 0 && (q & ~allowed) == 0) {
+            if ((q & blocked) == 0 && (need[i] & ~allowed) == 0) {
                 if (ran) ran->push_back(i);
                 continue;
             }
@@ -143,7 +153,7 @@ std::vector<std::vector<uint64_t>> search_tiles(const Search& S, size_t nops, in
         std::unordered_set<std::vector<int>, VecHash> seen;
         for (const St& s : states) {
             const uint64_t prev = s.tiles.empty() ? 0ull : s.tiles.back();
-            const uint64_t seed = S.qm[s.rem.front()];
+            const uint64_t seed = S.need[s.rem.front()];
             std::vector<std::pair<int, uint64_t>> part = {{S.score(s.rem, seed), seed}};
             for (;;) {
                 bool grew = false;
@@ -193,7 +203,7 @@ std::vector<std::vector<uint64_t>> search_tiles(const Search& S, size_t nops, in
                 std::vector<int> ran;
                 rem = S.apply(rem, t, &ran);
                 uint64_t u = 0;
-                for (int i : ran) u |= S.qm[i];
+                for (int i : ran) u |= S.need[i];
                 U.push_back(u);
             }
             if (close_cycle(s.tiles, U)) {
@@ -380,7 +390,9 @@ bool build_choice(int n, const std::function<std::vector<Op>(const std::vector<i
         int r0 = 0;
         while (r0 < kTile && ld[tq[r0]] == r0) ++r0;
         if (r0 < kRun) return false;
-        int hpos[kHposMax] = {0}, bit_of[64], st_pos[13] = {0}, st_tid[32] = {0};
+        int hpos[kHposMax] = {0}, bit_of[64], st_pos[13] = {0}, st_tid[32] = {0}, phys_of[64] = {0};
+        for (int q = 0; q < 64; ++q) bit_of[q] = -1;
+        for (int q = 0; q < n; ++q) phys_of[out.perm[q]] = ld[q];  // plan qubit -> load position
         for (int x = r0; x < kTile; ++x) hpos[x - r0] = ld[tq[x]];
         bool moved = false;
         for (int x = 0; x < kTile; ++x) {
@@ -396,7 +408,7 @@ bool build_choice(int n, const std::function<std::vector<Op>(const std::vector<i
         for (int i : ran[k]) pops.push_back(out.ops[i]);
         {
             const TileHeightScope scope(6);
-            append_tile_pass(plan, pops, n, 6, r0, hpos, bit_of, moved ? st_pos : nullptr, st_tid);
+            append_tile_pass(plan, pops, n, 6, r0, hpos, bit_of, moved ? st_pos : nullptr, st_tid, phys_of);
         }
         uint64_t mld = 0, mst = 0;
         for (int q : tq) {
@@ -424,6 +436,7 @@ bool build_choice(int n, const std::function<std::vector<Op>(const std::vector<i
 // re-run, or another state running the same circuit, does not search again.
 struct RelayoutMemo {
     int n;
+    bool ctrl_out;  // planned with tile-constant controls
     size_t max_passes;
     std::vector<unsigned char> key;
     std::vector<RelayoutChoice> v;
@@ -457,20 +470,21 @@ size_t plan_relayout_variants(int n, const std::function<std::vector<Op>(const s
     {
         std::lock_guard<std::mutex> l(g_rl_mu);
         for (RelayoutMemo& m : g_rl_memo)
-            if (m.n == n && m.max_passes == max_passes && m.key == key) {
+            if (m.n == n && m.ctrl_out == tile_ctrl_out() && m.max_passes == max_passes && m.key == key) {
                 m.used = ++g_rl_clock;
                 out = m.v;
                 return out.size();
             }
     }
-    std::vector<uint64_t> qm(logical.size());
+    std::vector<uint64_t> qm(logical.size()), nd(logical.size());
     bool fits = true;
     for (size_t i = 0; i < logical.size(); ++i) {
         qm[i] = op_mask(logical[i]);
-        fits = fits && __builtin_popcountll(qm[i]) <= kTile - kRun;
+        nd[i] = op_need(logical[i], tile_ctrl_out());
+        fits = fits && __builtin_popcountll(nd[i]) <= kTile - kRun;
     }
     if (fits) {
-        const Search S{qm, n};
+        const Search S{qm, n, nd};
         static const int width = env_int("QSIM_RELAYOUT_BEAM", 96);
         static const int nvar = std::max(1, env_int("QSIM_RELAYOUT_VARIANTS", 3));
         static const int nlay = std::max(1, env_int("QSIM_RELAYOUT_LAYOUT_VARIANTS", 2));
@@ -494,7 +508,7 @@ size_t plan_relayout_variants(int n, const std::function<std::vector<Op>(const s
     if (g_rl_memo.size() >= 8)
         g_rl_memo.erase(std::min_element(g_rl_memo.begin(), g_rl_memo.end(),
                                          [](const RelayoutMemo& x, const RelayoutMemo& y) { return x.used < y.used; }));
-    g_rl_memo.push_back(RelayoutMemo{n, max_passes, key, out, ++g_rl_clock});
+    g_rl_memo.push_back(RelayoutMemo{n, tile_ctrl_out(), max_passes, key, out, ++g_rl_clock});
     return out.size();
 }
 
@@ -518,7 +532,8 @@ Plan plan_permutation_pass(int n, const std::vector<int>& perm) {
     for (int q = 0; q < 6; ++q) tile |= (1ull << q) | (1ull << perm[q]);
     for (int p = 6; p < n && __builtin_popcountll(tile) < kTile; ++p) tile |= 1ull << p;
     const int r0 = 6;  // (physical 0..5 are tile positions)
-    int hpos[kHposMax] = {0}, bit_of[64] = {0}, st_pos[13] = {0}, st_tid[32] = {0};
+    int hpos[kHposMax] = {0}, bit_of[64], st_pos[13] = {0}, st_tid[32] = {0};
+    for (int q = 0; q < 64; ++q) bit_of[q] = -1;
     int x = 0, i = 0;
     for (int p = 0; p < n; ++p) {
         if ((tile >> p) & 1ull) {
@@ -632,7 +647,11 @@ void exec_plan_host(const Plan& plan, int n, std::vector<cd>& st) {
                     }
                 }
                 for (int t = 0; t < nthr; ++t)
-                    for (int o = sg.op_begin; o < sg.op_end; ++o) exec_stage_op(plan.ops[o], &v[(size_t)t * R], R, jbs[t]);
+                    for (int o = sg.op_begin; o < sg.op_end; ++o) {
+                        const TileOp& op = plan.ops[o];
+                        if ((kt & op.cm_out) != op.cm_out) continue;  // tile-constant control reads 0
+                        exec_stage_op(op, &v[(size_t)t * R], R, jbs[t]);
+                    }
                 for (int t = 0; t < nthr; ++t) {
                     const uint32_t jb = jbs[t];
                     const cd* vt = &v[(size_t)t * R];

@@ -110,6 +110,7 @@ _sig(hip, "qsim_plan_exec_host", [c_int, POINTER(qsim_gate), c_size_t, c_int, _P
 _sig(hip, "qsim_set_calibrate", [c_int, c_int])
 _sig(hip, "qsim_set_tile_height", [c_int])
 _sig(hip, "qsim_set_tile_rb7", [c_int])
+_sig(hip, "qsim_set_tile_ctrl_out", [c_int])
 _sig(hip, "qsim_plan_relabel", [c_int, _P, c_size_t, POINTER(c_int32), POINTER(c_double), POINTER(c_double)])
 # Stop the background pass compiler before interpreter / library teardown (a hipRTC compile that
 # is still running while the compiler's statics are destroyed aborts the process).

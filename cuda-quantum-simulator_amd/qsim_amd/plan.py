@@ -81,6 +81,12 @@ def set_tile_rb7(rb: int = -1) -> None:
     _lib.check(_lib.hip.qsim_set_tile_rb7(rb))
 
 
+def set_tile_ctrl_out(mode: int = -1) -> None:
+    """Tile-constant controls (qsim_set_tile_ctrl_out): 1 (default) a control qubit need not be a
+    tile qubit (the op runs per tile where it reads 1), 0 every control is a tile qubit."""
+    _lib.check(_lib.hip.qsim_set_tile_ctrl_out(mode))
+
+
 # The shipped policy (include/qsim_hip.h; environment variables unset).
 DEFAULTS = {"jit": (1, 20), "relabel": (1, 26), "relayout": (1, 20), "calibrate": (1, 26)}
 
@@ -94,6 +100,7 @@ def restore_defaults() -> None:
     set_relayout(*DEFAULTS["relayout"])
     set_calibrate(*DEFAULTS["calibrate"])
     set_tile_height(-1)
+    set_tile_ctrl_out(1)
 
 
 def plan_relabel(circuit: Circuit):

@@ -207,6 +207,12 @@ int qsim_set_calibrate(int mode, int min_qubits);
  * kernels) needs fewer passes on some circuits but streams slower.  h < 0 restores
  * the default (QSIM_TILE_HMAX); plans already cached for a circuit keep their height. */
 int qsim_set_tile_height(int h);
+/* Tile-constant controls (no reference counterpart; default on, QSIM_TILE_CTRL_OUT): the fused
+ * planners require only an op's TARGETS to be tile qubits; a control outside the tile is fixed for
+ * the whole tile, so the op runs on the tiles where it reads 1 (a uniform branch on the tile's
+ * base address) — a CNOT costs one tile slot, not two.  mode 0 off, 1 on, negative: unchanged;
+ * plans made from now on.  Batched Pauli-frame passes always keep every control a tile qubit. */
+int qsim_set_tile_ctrl_out(int mode);
 /* Register bits per stage of 13-qubit tiles: 4 (16 amplitudes per thread, 512-thread workgroups,
  * the default) or 3 (8 per thread, 1024 threads); anything else restores QSIM_TILE_RB7. */
 int qsim_set_tile_rb7(int rb);

@@ -35,11 +35,19 @@ def test_plan_relabel_is_a_valid_improving_permutation(qsim, n, seed):
 
 
 def test_relabel_finds_fewer_passes_at_28_qubits(qsim):
-    """W-HC 28q plans into 6 passes as labelled and into 5 under the chosen labels."""
-    from qsim_amd.plan import plan_fused, plan_relabel
+    """W-HC 28q plans into 6 passes as labelled and into 5 under the chosen labels (every control
+    a tile qubit); with tile-constant controls (the default) into 5 as labelled, and relabeling
+    keeps that."""
+    from qsim_amd.plan import plan_fused, plan_relabel, set_tile_ctrl_out
     c = qsim.createRandomHCCircuit(28, 100, 42)
+    set_tile_ctrl_out(0)
+    try:
+        perm, _, _ = plan_relabel(c)
+        assert plan_fused(c)[2] == 6 and plan_fused(_relabeled(qsim, c, perm))[2] == 5
+    finally:
+        set_tile_ctrl_out(1)
     perm, _, _ = plan_relabel(c)
-    assert plan_fused(c)[2] == 6 and plan_fused(_relabeled(qsim, c, perm))[2] == 5
+    assert plan_fused(c)[2] == 5 and plan_fused(_relabeled(qsim, c, perm))[2] <= 5
 
 
 def test_small_circuit_keeps_identity(qsim):
