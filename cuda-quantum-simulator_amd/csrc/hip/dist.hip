@@ -587,13 +587,25 @@ struct qsim_dist {
     DevBuf ops, stages;
     // Plans of recent runs, keyed by (gate list, map at the start of the run): a repeated circuit
     // alternates between a few start maps, each with its own segment plans and compiled kernels.
+    // Fused remap (QSIM_DIST_FUSED_PACK, default on): the last pass before an exchange stores
+    // its tiles straight into the send buffer's slab layout and the step after it plans in that
+    // layout, loading from the receive buffer, its last pass storing back to the standard one —
+    // no pack / unpack kernels.  Per shard: the two plans, their compiled kernels, the decision.
+    struct FusedVariant {
+        Plan plan;
+        JitState jit;
+        bool ok = false;
+    };
     struct RunPlan {
         std::vector<qsim_gate> gates;
         std::vector<int> perm_in, perm_out;
         std::vector<std::vector<DStep>> steps;              // per shard
         std::vector<std::vector<std::unique_ptr<PlanCache>>> fplans;  // per shard, per step
+        std::vector<std::unique_ptr<FusedVariant>> fpack, funpack;    // per shard (the first exchange)
+        bool fused_decided = false;
         uint64_t used = 0;
     };
+    int fused_remaps = 0;  // exchanges of the last run whose pack / unpack ran inside the passes
     std::vector<std::unique_ptr<RunPlan>> run_plans;
     uint64_t run_clock = 0;
     Timer timer;
@@ -930,7 +942,15 @@ void post_transfers(qsim_dist* d, const std::vector<Post>& posts, const char* wh
     }
 }
 
-void exchange(qsim_dist* d, const DStep& ex) {
+// A fused shard's own slab of part `base`: the pass wrote it to the send buffer, the step after
+// reads the receive buffer (the slab never leaves the GPU: one device copy of 1 / 2^k of it).
+void own_slab_copy(qsim_dist* d, const Shard& sh, const XPlan& x, uint64_t base, uint64_t stride, uint64_t amps,
+                   hipStream_t s) {
+    const uint64_t at = base + (uint64_t)x.a.my_c * stride;
+    QSIM_HIPCHK(hipMemcpyAsync(sh.recvbuf + at, sh.sendbuf + at, amps * sizeof(double2), hipMemcpyDeviceToDevice, s));
+}
+
+void exchange(qsim_dist* d, const DStep& ex, const std::vector<char>& fused) {
     if (ex.k == 0) return;
     const uint64_t total = 1ull << d->L;
     const uint64_t chunk = total >> ex.k;
@@ -950,6 +970,10 @@ void exchange(qsim_dist* d, const DStep& ex) {
     for (Shard& sh : d->shards) xs.push_back(xplan(d, sh, ex));
     for (int p = 0; p < parts; ++p) {
         for (size_t i = 0; i < d->shards.size(); ++i) {
+            if (fused[i]) {  // (the pass before stored the slabs; the own slab moves on the device)
+                own_slab_copy(d, d->shards[i], xs[i], (uint64_t)p * sub, chunk, sub, d->stream);
+                continue;
+            }
             XArgs a = xs[i].a;
             a.buf = d->shards[i].sendbuf;
             copy_kernel(true, a, (uint64_t)p * sub, sub_log, d->stream);
@@ -967,6 +991,7 @@ void exchange(qsim_dist* d, const DStep& ex) {
     for (int p = 0; p < parts; ++p) {
         QSIM_HIPCHK(hipStreamWaitEvent(d->stream, d->events[parts + p], 0));
         for (size_t i = 0; i < d->shards.size(); ++i) {
+            if (fused[i]) continue;  // (the step after loads the receive buffer itself)
             XArgs a = xs[i].a;
             a.buf = d->shards[i].recvbuf;
             copy_kernel(false, a, (uint64_t)p * sub, sub_log, d->stream);
@@ -978,7 +1003,7 @@ void exchange(qsim_dist* d, const DStep& ex) {
 // each part waiting for its local work (event pev[j], recorded on the compute stream after the
 // role-1 step's part) and signalling pev[24 + j] when unpacked (the role-2 step's part waits for
 // it).  Part j uses part j of the send / receive buffers, so all parts can be in flight.
-void exchange_parts(qsim_dist* d, const DStep& ex) {
+void exchange_parts(qsim_dist* d, const DStep& ex, const std::vector<char>& fused) {
     const int K = 1 << __builtin_popcountll(ex.pmask);
     const uint64_t part_amps = 1ull << (d->L - __builtin_popcountll(ex.pmask));
     const uint64_t chunk = part_amps >> ex.k;
@@ -989,6 +1014,10 @@ void exchange_parts(qsim_dist* d, const DStep& ex) {
         for (Shard& sh : d->shards) xs.push_back(xplan(d, sh, ex, h));
         QSIM_HIPCHK(hipStreamWaitEvent(d->copy_stream, d->pev[h], 0));
         for (size_t i = 0; i < d->shards.size(); ++i) {
+            if (fused[i]) {  // (the tail pass of part h stored its slabs; own slab on the device)
+                own_slab_copy(d, d->shards[i], xs[i], (uint64_t)h * part_amps, chunk, chunk, d->copy_stream);
+                continue;
+            }
             XArgs a = xs[i].a;
             a.buf = d->shards[i].sendbuf + (uint64_t)h * part_amps;
             copy_kernel(true, a, 0, xs[i].a.chunk_log, d->copy_stream);
@@ -1002,6 +1031,7 @@ void exchange_parts(qsim_dist* d, const DStep& ex) {
         QSIM_HIPCHK(hipEventRecord(d->pev[16 + h], d->comm_stream));
         QSIM_HIPCHK(hipStreamWaitEvent(d->copy_stream, d->pev[16 + h], 0));
         for (size_t i = 0; i < d->shards.size(); ++i) {
+            if (fused[i]) continue;  // (the step after loads part h from the receive buffer)
             XArgs a = xs[i].a;
             a.buf = d->shards[i].recvbuf + (uint64_t)h * part_amps;
             copy_kernel(false, a, 0, xs[i].a.chunk_log, d->copy_stream);
@@ -1065,8 +1095,10 @@ StepRun prepare_step(qsim_dist* d, const std::vector<Op>& ops, int flags, PlanCa
 }
 // Launch passes [first, last) of a prepared step (part >= 0: the part whose pivot bits `pmask`
 // hold the bits of part); per-gate mode: the whole op list when called for the middle part.
+// home / alt: where the step's passes read, and where a relayout pass (fused remap) writes
+// (null: the shard's state, no second buffer).
 void run_part(qsim_dist* d, Shard& sh, const std::vector<Op>& ops, const StepRun& r, size_t first,
-              size_t last, uint64_t pmask = 0, int part = -1) {
+              size_t last, uint64_t pmask = 0, int part = -1, double2* home = nullptr, double2* alt = nullptr) {
     if (ops.empty() || first >= last) return;
     if (!r.plan) {
         for (const Op& op : ops) launch_op(sh.d, d->L, 1, op, d->stream, &d->timer);
@@ -1077,12 +1109,105 @@ void run_part(qsim_dist* d, Shard& sh, const std::vector<Op>& ops, const StepRun
     FusedRange rg;
     rg.first = first;
     rg.last = last;
+    rg.alt = alt;
     if (part >= 0) {
         rg.fix_mask = pmask;
         rg.fix_val = deposit_bits((uint64_t)part, pmask);
     }
-    launch_fused(sh.d, d->L, 1, *r.plan, (const TileOp*)d->ops.ptr, (const Stage*)d->stages.ptr, d->stream,
-                 &d->timer, r.jm, nullptr, rg);
+    launch_fused(home ? home : sh.d, d->L, 1, *r.plan, (const TileOp*)d->ops.ptr, (const Stage*)d->stages.ptr,
+                 d->stream, &d->timer, r.jm, nullptr, rg);
+}
+
+// The slab layout of exchange `ex` as a permutation of the local positions (the inverse of
+// xlocal): positions outside lpos and the pivots ascending -> 0 .. L-k-m-1, lpos[j] -> L-m-k+j,
+// the pivots ascending -> L-m .. L-1.  Part h of slab c is then the contiguous block at
+// h * 2^(L-m) + c * 2^(L-m-k) of the send / receive buffers.
+std::vector<int> slab_sigma(int L, const DStep& ex) {
+    std::vector<int> s(L, -1);
+    uint64_t moved = ex.pmask;
+    for (int j = 0; j < ex.k; ++j) moved |= 1ull << ex.lpos[j];
+    const int m = __builtin_popcountll(ex.pmask);
+    int k = 0;
+    for (int p = 0; p < L; ++p)
+        if (!((moved >> p) & 1ull)) s[p] = k++;
+    for (int j = 0; j < ex.k; ++j) s[ex.lpos[j]] = L - m - ex.k + j;
+    int i = 0;
+    for (uint64_t mm = ex.pmask; mm; mm &= mm - 1) s[__builtin_ctzll(mm)] = L - m + i++;
+    return s;
+}
+bool fused_pack_enabled() {
+    const char* e = std::getenv("QSIM_DIST_FUSED_PACK");  // (read per run: tests switch it)
+    return e == nullptr || std::atoi(e) != 0;
+}
+Op map_op_positions(Op op, const std::vector<int>& sg) {
+    op.t0 = sg[op.t0];
+    if (op.kind == K_SWAP) op.t1 = sg[op.t1];
+    uint64_t cm = 0;
+    for (uint64_t m = op.cmask; m; m &= m - 1) cm |= 1ull << sg[__builtin_ctzll(m)];
+    op.cmask = cm;
+    return op;
+}
+// Per shard, whether the first exchange of run plan `rp` runs fused (steps [A, X, B] at the
+// start of the run, fused ops plans on both sides; exchanged positions below 6 only cost the
+// storing pass some coalescing: its lanes are the tile bits with the lowest store positions),
+// and the two plans: A's with its last pass storing into
+// the slab layout, B's planned on positions sigma(p) (the receive buffer's layout) with its last
+// pass storing back to the standard positions.  The slab layout is the unfused exchange's, so
+// shards decide independently.
+void decide_fused(qsim_dist* d, qsim_dist::RunPlan& rp, int flags) {
+    if (rp.fused_decided) return;
+    rp.fused_decided = true;
+    const size_t S = d->shards.size();
+    rp.fpack.resize(S);
+    rp.funpack.resize(S);
+    const std::vector<DStep>& st0 = rp.steps[0];
+    if (!(flags & QSIM_RUN_FUSED) || !fused_pack_enabled() || st0.size() < 3 || st0[0].kind != 0 ||
+        st0[1].kind != 1 || st0[2].kind != 0 || (st0[2].role & 1))
+        return;
+    const DStep& ex = st0[1];
+    if (ex.pmask & 0x3full) return;  // (pivots are >= 6 by construction)
+    const std::vector<int> sg = slab_sigma(d->L, ex);
+    std::vector<int> inv(d->L);
+    for (int p = 0; p < d->L; ++p) inv[sg[p]] = p;
+    uint64_t pm_sigma = 0;
+    for (uint64_t m = ex.pmask; m; m &= m - 1) pm_sigma |= 1ull << sg[__builtin_ctzll(m)];
+    for (size_t i = 0; i < S; ++i) {
+        const DStep& A = rp.steps[i][0];
+        const DStep& B = rp.steps[i][2];
+        if (A.ops.empty() || B.ops.empty()) continue;
+        auto pk = std::make_unique<qsim_dist::FusedVariant>();
+        auto up = std::make_unique<qsim_dist::FusedVariant>();
+        try {
+            const uint64_t pa = (A.role & 1) ? ex.pmask : 0ull;
+            pk->plan = plan_fused(A.ops, d->L, -1, pa);
+            const FusedPass& la = pk->plan.passes.back();
+            if (la.single >= 0 || la.h < 4) continue;
+            relayout_last_pass(pk->plan, d->L, sg.data());
+            std::vector<Op> bops;
+            for (const Op& op : B.ops) bops.push_back(map_op_positions(op, sg));
+            up->plan = plan_fused(bops, d->L, -1, (B.role & 2) ? pm_sigma : 0ull);
+            const FusedPass& lb = up->plan.passes.back();
+            if (lb.single >= 0 || lb.h < 4) continue;
+            relayout_last_pass(up->plan, d->L, inv.data());
+        } catch (const Error&) {
+            continue;  // (this shard keeps the pack / unpack kernels)
+        }
+        pk->ok = up->ok = true;
+        rp.fpack[i] = std::move(pk);
+        rp.funpack[i] = std::move(up);
+    }
+}
+StepRun prepare_variant(qsim_dist* d, qsim_dist::FusedVariant& v, uint64_t pb, uint64_t pa) {
+    StepRun r;
+    r.plan = &v.plan;
+    r.jm = jit_for(v.jit, v.plan, d->L);
+    r.np = v.plan.passes.size();
+    if (pb)
+        while (r.j1 < r.np && pass_avoids(v.plan.passes[r.j1], pb)) ++r.j1;
+    r.j2 = r.np;
+    if (pa)
+        while (r.j2 > r.j1 && pass_avoids(v.plan.passes[r.j2 - 1], pa)) --r.j2;
+    return r;
 }
 // The cached plan of this run (same gates, same start map), or a new one (LRU of 8).
 qsim_dist::RunPlan& run_plan(qsim_dist* d, const qsim_gate* gates, size_t count) {
@@ -1329,6 +1454,11 @@ int qsim_dist_run(qsim_dist* d, const qsim_gate* gates, size_t count, int flags)
         for (size_t i = 1; i < S; ++i)
             if (plans[i].size() != plans[0].size()) fail(QSIM_ERR_RUNTIME, "exchange skeleton mismatch");
         d->overlapped = 0;
+        d->fused_remaps = 0;
+        decide_fused(d, rp, flags);
+        std::vector<char> fused(S, 0);  // per shard: the first exchange runs fused
+        for (size_t i = 0; i < S; ++i) fused[i] = rp.fpack[i] && rp.fpack[i]->ok;
+        const std::vector<char> unfused(S, 0);
         static const bool dbg = std::getenv("QSIM_DIST_DEBUG") != nullptr;
         if (dbg) {  // the exchange skeleton this run executes (kind, k, pivot mask, role)
             std::string line = "[dist] rank " + std::to_string(d->shards[0].rank) + " perm_in";
@@ -1352,6 +1482,8 @@ int qsim_dist_run(qsim_dist* d, const qsim_gate* gates, size_t count, int flags)
                 if (plans[i][k].kind != s0.kind || plans[i][k].role != s0.role)
                     fail(QSIM_ERR_RUNTIME, "exchange skeleton mismatch");
             if (s0.kind == 1) {
+                const std::vector<char>& fz = k == 1 ? fused : unfused;
+                for (char f : fz) d->fused_remaps += f ? 1 : 0;
                 if (s0.pmask) {
                     // the ops step before (role bit 1) recorded pev[j] after its tail part j;
                     // otherwise every part is ready now
@@ -1359,12 +1491,12 @@ int qsim_dist_run(qsim_dist* d, const qsim_gate* gates, size_t count, int flags)
                     wait_pending();
                     if (k == 0 || !(plans[0][k - 1].role & 1))
                         for (int h = 0; h < K; ++h) QSIM_HIPCHK(hipEventRecord(d->pev[h], d->stream));
-                    exchange_parts(d, s0);
+                    exchange_parts(d, s0, fz);
                     pending = K;
                     ++d->overlapped;
                 } else {
                     wait_pending();
-                    exchange(d, s0);
+                    exchange(d, s0, fz);
                 }
                 continue;
             }
@@ -1372,24 +1504,50 @@ int qsim_dist_run(qsim_dist* d, const qsim_gate* gates, size_t count, int flags)
             const uint64_t pb = (s0.role & 2) ? plans[0][k - 1].pmask : 0ull;
             const uint64_t pa = (s0.role & 1) ? plans[0][k + 1].pmask : 0ull;
             std::vector<StepRun> runs(S);
-            for (size_t i = 0; i < S; ++i) runs[i] = prepare_step(d, plans[i][k].ops, flags, *rp.fplans[i][k], pb, pa);
+            // fused first exchange: step 0 stores its last pass into the send buffer (slab
+            // layout), step 2 reads the receive buffer in that layout (pivots at sigma's top
+            // positions) and stores its last pass back to the state
+            std::vector<uint64_t> pbs(S, pb);
+            std::vector<double2*> homes(S, nullptr), alts(S, nullptr);
+            for (size_t i = 0; i < S; ++i) {
+                if (fused[i] && k == 0) {
+                    runs[i] = prepare_variant(d, *rp.fpack[i], pb, pa);
+                    alts[i] = d->shards[i].sendbuf;
+                } else if (fused[i] && k == 2) {
+                    const std::vector<int> sg = slab_sigma(d->L, plans[0][1]);
+                    uint64_t ps = 0;
+                    for (uint64_t m = pb; m; m &= m - 1) ps |= 1ull << sg[__builtin_ctzll(m)];
+                    pbs[i] = ps;
+                    runs[i] = prepare_variant(d, *rp.funpack[i], ps, 0);
+                    homes[i] = d->shards[i].recvbuf;
+                    alts[i] = d->shards[i].d;
+                } else {
+                    runs[i] = prepare_step(d, plans[i][k].ops, flags, *rp.fplans[i][k], pb, pa);
+                }
+            }
             const bool head = pb && pending;
             if (head) {
                 for (int h = 0; h < pending; ++h) {
                     QSIM_HIPCHK(hipStreamWaitEvent(d->stream, d->pev[24 + h], 0));
                     for (size_t i = 0; i < S; ++i)
-                        if (runs[i].plan) run_part(d, d->shards[i], plans[i][k].ops, runs[i], 0, runs[i].j1, pb, h);
+                        if (runs[i].plan)
+                            run_part(d, d->shards[i], plans[i][k].ops, runs[i], 0, runs[i].j1, pbs[i], h, homes[i],
+                                     alts[i]);
                 }
             }
             wait_pending();
             for (size_t i = 0; i < S; ++i) {
-                if (runs[i].plan) run_part(d, d->shards[i], plans[i][k].ops, runs[i], head ? runs[i].j1 : 0, runs[i].j2);
+                if (runs[i].plan)
+                    run_part(d, d->shards[i], plans[i][k].ops, runs[i], head ? runs[i].j1 : 0, runs[i].j2, 0, -1,
+                             homes[i], alts[i]);
                 else run_part(d, d->shards[i], plans[i][k].ops, runs[i], 0, 1);  // per-gate: the whole list
             }
             if (pa) {  // the exchange after waits for pev[h]
                 for (int h = 0; h < (1 << __builtin_popcountll(pa)); ++h) {
                     for (size_t i = 0; i < S; ++i)
-                        if (runs[i].plan) run_part(d, d->shards[i], plans[i][k].ops, runs[i], runs[i].j2, runs[i].np, pa, h);
+                        if (runs[i].plan)
+                            run_part(d, d->shards[i], plans[i][k].ops, runs[i], runs[i].j2, runs[i].np, pa, h, homes[i],
+                                     alts[i]);
                     QSIM_HIPCHK(hipEventRecord(d->pev[h], d->stream));
                 }
             }
@@ -1403,6 +1561,14 @@ int qsim_dist_remap_bytes(qsim_dist* d, double* sent) {
     return dguard([&] {
         need(d);
         if (sent) *sent = d->sent_bytes;
+    });
+}
+
+int qsim_dist_fused_remaps(qsim_dist* d, int* remaps) {
+    return dguard([&] {
+        need(d);
+        if (!remaps) fail(QSIM_ERR_INVALID_ARGUMENT, "null out");
+        *remaps = d->fused_remaps;
     });
 }
 

@@ -188,6 +188,9 @@ constexpr int kTileR0 = 6;    // contiguous run bits of a staged tile (QSIM_TILE
 // hmax < 0: the process default (kTileHDefault, or QSIM_TILE_HMAX up to kTileHMax).
 // avoid: qubits no tile may contain (ops never act on them; only tile padding is affected).
 Plan plan_fused(const std::vector<Op>& ops, int n, int hmax = -1, uint64_t avoid = 0);
+// Rebuild the last pass of `plan` (staged) as a relayout pass that stores load position p at
+// tau[p] (a permutation of 0..n-1; the sharded engine's fused remap pack / unpack).
+void relayout_last_pass(Plan& plan, int n, const int* tau);
 // One tile pass appended to a plan (fused.hip; plan_fused and the relayout planner use it).
 // bit_of[q] < 0: op qubit q is not a tile qubit (a tile-constant control); phys_of (null: the
 // identity) gives such a control's physical position under the pass's load layout.

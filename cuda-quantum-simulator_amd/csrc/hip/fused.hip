@@ -797,6 +797,40 @@ void append_tile_pass(Plan& plan, const std::vector<Op>& ops, int n, int h, int 
     plan.passes.push_back(p);
 }
 
+void relayout_last_pass(Plan& plan, int n, const int* tau) {
+    if (plan.passes.empty()) fail(QSIM_ERR_RUNTIME, "relayout_last_pass: empty plan");
+    FusedPass p = plan.passes.back();
+    if (p.single >= 0 || p.h < 4) fail(QSIM_ERR_RUNTIME, "relayout_last_pass: not a staged pass");
+    // the pass's ops in execution order (tile-bit space; SWAPs already lowered)
+    std::vector<TileOp> ops;
+    std::vector<int> src;
+    for (int k = p.stage_begin; k < p.stage_end; ++k)
+        for (int o = plan.stages[k].op_begin; o < plan.stages[k].op_end; ++o) {
+            ops.push_back(plan.ops[o]);
+            src.push_back(plan.order[o]);
+        }
+    const int tb = 6 + p.h;
+    int st_pos[13] = {0}, st_tid[32] = {0};
+    uint64_t hm = 0;
+    for (int x = 0; x < tb; ++x) {
+        const int pos = x < p.r0 ? x : p.hpos[x - p.r0];
+        if (x >= p.r0) hm |= 1ull << pos;
+        st_pos[x] = tau[pos];
+    }
+    int k = 0;
+    for (int q = p.r0; q < n; ++q)
+        if (!((hm >> q) & 1ull)) {
+            if (k >= 32) fail(QSIM_ERR_RUNTIME, "relayout_last_pass: too many tile-id bits");
+            st_tid[k++] = tau[q];
+        }
+    p.relayout = 1;
+    p.n_tid = k;
+    for (int x = 0; x < tb; ++x) p.st_pos[x] = st_pos[x];
+    for (int i = 0; i < k; ++i) p.st_tid[i] = st_tid[i];
+    plan_stages(ops, src, tb, p.rb, plan, p, st_pos);  // (appends its stages; the old ones idle)
+    plan.passes.back() = p;
+}
+
 Plan plan_fused(const std::vector<Op>& ops, int n, int hmax, uint64_t avoid) {
     if (hmax < 0) hmax = tile_height_default();
     Plan plan;
@@ -911,6 +945,7 @@ struct FArgs {
     int relayout, n_tid;
     int st_pos[13];
     int st_tid[32];
+    int nt_pos[32];  // the non-tile load positions, ascending (tile-id bit i <-> nt_pos[i])
 };
 
 // Runtime-count forms for the staged kernel (count = tile bits above the run, < kHposMax).
@@ -1306,10 +1341,11 @@ __global__ __launch_bounds__((64 << H) >> RBT, H >= 7 ? 1 : 2) void k_fused_stag
         kt = deposit_n(kt, a.hpos, nh);
     }
     const uint64_t base = (tile_id >> a.log_tpt) * a.stride + kt;
-    uint64_t base_st = 0;  // relayout: the tile's base under the next pass's layout
+    uint64_t base_st = 0;  // relayout: the tile's base under the store layout
     if (a.relayout) {
-        const uint64_t kl = tile_id & a.tpt_mask;
-        for (int i = 0; i < a.n_tid; ++i) base_st |= ((kl >> i) & 1ull) << a.st_tid[i];
+        // every non-tile load position's bit (tile-id bits, and a sub-space launch's fixed bits)
+        // moved to its store position
+        for (int i = 0; i < a.n_tid; ++i) base_st |= ((kt >> a.nt_pos[i]) & 1ull) << a.st_tid[i];
         base_st += (tile_id >> a.log_tpt) * a.stride;
     }
     const uint32_t run_mask = (1u << r0) - 1u;
@@ -1439,8 +1475,8 @@ double2* launch_fused(double2* st, int n, uint64_t batch, const Plan& plan, cons
         a.fix_val = range.fix_val;
         a.zmask = hmask | range.fix_mask;
         if (p.relayout) {
-            if (range.fix_mask || frames || p.h < 4 || p.stage_end - p.stage_begin < 2)
-                fail(QSIM_ERR_RUNTIME, "relayout pass outside a whole-state staged run");
+            if (frames || p.h < 4 || p.stage_end - p.stage_begin < 2)
+                fail(QSIM_ERR_RUNTIME, "relayout pass outside a staged run");
             if (n - 6 - p.h != p.n_tid || p.n_tid > 32) fail(QSIM_ERR_RUNTIME, "relayout pass planned for another size");
             if (!range.alt || batch != 1) fail(QSIM_ERR_RUNTIME, "relayout pass without a second buffer");
             a.relayout = 1;
@@ -1449,6 +1485,10 @@ double2* launch_fused(double2* st, int n, uint64_t batch, const Plan& plan, cons
             a.n_tid = p.n_tid;
             for (int i = 0; i < 13; ++i) a.st_pos[i] = p.st_pos[i];
             for (int i = 0; i < 32; ++i) a.st_tid[i] = p.st_tid[i];
+            int k = 0;
+            for (int q = 0; q < n && k < 32; ++q)
+                if (q >= p.r0 && !((hmask >> q) & 1ull)) a.nt_pos[k++] = q;
+            if (k != p.n_tid) fail(QSIM_ERR_RUNTIME, "relayout pass: non-tile positions do not match");
         }
         const int lt = n - 6 - p.h - nfix;
         a.log_tpt = lt;

@@ -254,6 +254,24 @@ std::string scatter_expr(const std::string& src, const int* dst, int cnt, bool w
     }
     return e.empty() ? (wide ? std::string("0ull") : std::string("0u")) : e;
 }
+// OR over i of bit src_pos[i] of `src` moved to bit dst_pos[i] (64-bit), runs of consecutive
+// positions (on both sides) moved by one mask + shift
+std::string gather_scatter_expr(const std::string& src, const int* src_pos, const int* dst_pos, int cnt) {
+    std::string e;
+    for (int i = 0; i < cnt;) {
+        int k = 1;
+        while (i + k < cnt && src_pos[i + k] == src_pos[i] + k && dst_pos[i + k] == dst_pos[i] + k) ++k;
+        const uint64_t m = ((1ull << k) - 1ull) << src_pos[i];
+        std::string t = "((" + src + " & " + hexu(m) + ")";
+        const int sh = dst_pos[i] - src_pos[i];
+        if (sh > 0) t += " << " + std::to_string(sh);
+        else if (sh < 0) t += " >> " + std::to_string(-sh);
+        t += ")";
+        e += e.empty() ? t : " | " + t;
+        i += k;
+    }
+    return e.empty() ? std::string("0ull") : e;
+}
 // Thread index spread over the tile bits that are not register bits of stage `st`.
 std::string jb_expr(const Stage& st, int rb, int tile_bits) {
     if (st.tscatter) return scatter_expr("tid", st.tmap, tile_bits - rb, false);
@@ -369,9 +387,17 @@ void gen_pass(std::ostringstream& out, const Plan& plan, const FusedPass& p, int
     } else {
         o << tile_id_expr() << "  unsigned long long base;\n";
         tile_base("tile_id", "base");
-        if (p.relayout)  // the tile's base under the next pass's layout
-            o << "  const unsigned long long base_st = (tile_id >> log_tpt) * stride | ("
-              << scatter_expr("(tile_id & tpt_mask)", p.st_tid, p.n_tid, true) << ");\n";
+        if (p.relayout) {  // the tile's base under the store layout: every non-tile load
+                           // position's bit (tile-id and a sub-space launch's fixed bits) moved
+            int nt_pos[32], k = 0;
+            uint64_t hm = 0;
+            for (int i = 0; i < nh; ++i) hm |= 1ull << p.hpos[i];
+            for (int q = r0; k < p.n_tid && q < 64; ++q)
+                if (!((hm >> q) & 1ull)) nt_pos[k++] = q;
+            o << "  const unsigned long long bl = base - (tile_id >> log_tpt) * stride;\n"
+              << "  const unsigned long long base_st = (tile_id >> log_tpt) * stride | ("
+              << gather_scatter_expr("bl", nt_pos, p.st_tid, p.n_tid) << ");\n";
+        }
     }
     auto body = [&]() {
         for (int r = 0; r < R; ++r) g.nm[r] = r;

@@ -621,8 +621,12 @@ void exec_plan_host(const Plan& plan, int n, std::vector<cd>& st) {
                 kt = ((kt ^ lo) << 1) | lo;
             }
             uint64_t base_st = 0;
-            if (p.relayout)
-                for (int i = 0; i < p.n_tid; ++i) base_st |= ((tile >> i) & 1ull) << p.st_tid[i];
+            if (p.relayout) {  // (as the kernels: the non-tile load positions' bits, moved)
+                uint64_t hm = 0;
+                for (int i = 0; i < nh; ++i) hm |= 1ull << p.hpos[i];
+                for (int q = r0, i = 0; q < n && i < p.n_tid; ++q)
+                    if (!((hm >> q) & 1ull)) base_st |= ((kt >> q) & 1ull) << p.st_tid[i++];
+            }
             for (int s = p.stage_begin; s < p.stage_end; ++s) {
                 const Stage& sg = plan.stages[s];
                 const bool first = s == p.stage_begin, last = s == p.stage_end - 1;

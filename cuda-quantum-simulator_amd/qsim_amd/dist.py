@@ -116,6 +116,13 @@ class DistributedSimulator:
         v = _c.c_int(0)
         _lib.check(_lib.hip.qsim_dist_overlapped(self._h, _c.byref(v)))
         return v.value
+    def fusedRemaps(self) -> int:
+        """Exchanges of the last run whose pack / unpack ran inside the local passes (the pass
+        before stored into the slab layout, the step after loaded from it), summed over shards."""
+        v = _c.c_int(0)
+        _lib.check(_lib.hip.qsim_dist_fused_remaps(self._h, _c.byref(v)))
+        return v.value
+
     def remapBytes(self) -> float:
         """Bytes this rank sent in the last run's remaps (it received as many)."""
         v = _c.c_double(0)

@@ -398,6 +398,11 @@ int qsim_dist_create_virtual(int n_qubits, int world, int device, qsim_dist** ou
  * its all-reduces through RCCL — the multi-rank call sequence (non-blocking init, groups,
  * settle, watchdog) on one GPU (tests). */
 int qsim_dist_virtual_rccl(qsim_dist* d, const void* unique_id);
+/* Exchanges of the last qsim_dist_run (summed over this process's shards) whose pack and unpack
+ * ran inside the local passes: the last pass before the remap stored its tiles straight into the
+ * send buffer's slab layout and the step after it planned in that layout, loading from the receive
+ * buffer, its last pass storing back to the standard positions (no k_exchange_copy). */
+int qsim_dist_fused_remaps(qsim_dist* d, int* remaps);
 /* Host-staged transport (no RCCL): one shard per process like qsim_dist_create, but every
  * point-to-point transfer is handed to `fn` as host buffers.  A post sends `bytes` from `send` to
  * rank `peer` and receives `bytes` from `peer` into `recv` (either may be NULL for a one-sided

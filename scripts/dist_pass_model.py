@@ -12,6 +12,7 @@ c = q.createRandomHCCircuit(n, 100, seed)
 arr, cnt = c.to_abi()
 perm = (ctypes.c_int32 * n)(*range(n))
 tot = 0
+rows = []
 for r in range(runs):
     passes = (ctypes.c_int32 * (3 * 64))()
     ns = ctypes.c_size_t(0)
@@ -19,6 +20,7 @@ for r in range(runs):
     steps = [tuple(passes[3 * i:3 * i + 3]) for i in range(ns.value)]
     p = sum(x[0] for x in steps if x[0] > 0)
     tot += p
+    rows.append(steps)
     print(f"run {r}: steps (passes, head, tail) {steps} passes {p}")
 print("mean passes per run", tot / runs)
 
@@ -34,3 +36,25 @@ for r in range(runs):
     vol += sum(1 - 2.0 ** -k for k in ks)
     print(f"run {r}: remap k {ks} pivots {[steps[i].pivot for i in range(ns.value) if steps[i].kind == 1]}")
 print("mean shard fraction sent per run", vol / runs)
+
+# The time model of DESIGN §5 per run (one remap between ops steps A and B):
+#   T = max(T_x + (nA - t + nB - h) * P + (t + h) * P / K,  (nA + nB) * P + T_x / K)
+# P: one local pass over the 2 GiB shard (32 B x 2^27 at 6.4 TB/s), K = 2^(pivots).
+P = float(os.environ.get("PASS_MS", 32 * 2 ** (n - 3) / 6.4e12 * 1e3))
+perm = (ctypes.c_int32 * n)(*range(n))
+for r in range(runs):
+    steps = (_lib.qsim_dist_step * 64)()
+    ns, no = ctypes.c_size_t(0), ctypes.c_size_t(0)
+    _lib.check(_lib.hip.qsim_dist_plan(n, world, 0, arr, cnt, perm, steps, 64, ctypes.byref(ns), None, 0,
+                                       ctypes.byref(no)))
+    ps = rows[r]
+    for i in range(ns.value):
+        if steps[i].kind != 1 or i == 0 or i + 1 >= ns.value:
+            continue
+        K = 2 ** bin(steps[i].pmask).count("1")
+        nA, _, t = ps[i - 1]
+        nB, h, _ = ps[i + 1]
+        for tx in (4.4, 3.5):
+            T = max(tx + (nA - t + nB - h) * P + (t + h) * P / K, (nA + nB) * P + tx / K)
+            print(f"run {r}: nA {nA} t {t} nB {nB} h {h} K {K}: T_x {tx} ms -> {T:.2f} ms per run "
+                  f"(pass {P:.3f} ms; pack/unpack not counted)")

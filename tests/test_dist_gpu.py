@@ -186,3 +186,31 @@ def test_virtual_30q_8_shards_over_rccl_matches_single_gpu(qsim, gpu_ready):
     del s
     err = float(np.max(np.abs(got - ref)))
     assert err < 1e-12, err
+
+
+@pytest.mark.parametrize("n,world", [(20, 8), (24, 8), (22, 4)])
+def test_fused_remap_equals_pack_unpack(qsim, oracle, gpu_ready, monkeypatch, n, world):
+    """The fused remap (qsim_dist_fused_remaps): the last pass before the exchange stores into the
+    send buffer's slab layout, the step after loads from the receive buffer in that layout and
+    stores back (sub-space relayout passes per pivot part) — the same state as the pack / unpack
+    kernels, over two runs (the second from the first's map) and against the oracle."""
+    from qsim_amd.dist import DistributedSimulator
+    c = qsim.createRandomHCCircuit(n, 100, 42)
+    out = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("QSIM_DIST_FUSED_PACK", mode)
+        d = DistributedSimulator.virtual(n, world)
+        d.run(c)
+        fused1 = d.fusedRemaps()
+        d.run(c)
+        fused2 = d.fusedRemaps()
+        out[mode] = d.getStateVector()
+        if mode == "1":
+            assert fused1 + fused2 > 0
+        else:
+            assert fused1 == fused2 == 0
+        d.close()
+    g = oracle.gates_of(c)
+    ref = oracle.run_cpu(n, g + g)
+    assert np.max(np.abs(out["1"] - ref)) < 1e-12
+    assert np.max(np.abs(out["0"] - ref)) < 1e-12
