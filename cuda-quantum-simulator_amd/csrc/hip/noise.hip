@@ -106,12 +106,15 @@ __device__ __forceinline__ bool next_flip(FlipCursor& cur, uint64_t b, uint64_t 
 
 // Walks block b and applies its flips.  (Batching several flips' loads before their stores was
 // measured: no change — the launch is bound by random-access memory throughput, not latency.)
+// bad (QSIM_NOISE_CHECK, tests): counts accesses outside the caller's pairs [lo, hi).
 __device__ __forceinline__ void flip_block(double2* st, uint64_t b, uint64_t lo, uint64_t hi,
-                                           uint64_t idx0, int log_ppt, const FlipChan& c) {
+                                           uint64_t idx0, int log_ppt, const FlipChan& c,
+                                           unsigned int* bad = nullptr) {
     const uint64_t mask = (1ull << c.target) - 1ull;
     FlipCursor cur{nz_mix(c.key ^ nz_mix(b ^ kBlockSalt)), 0, -1, false};
     uint64_t g = 0, h = 0;
     while (next_flip(cur, b, lo, hi, c, g, h)) {
+        if (bad && (g < lo || g >= hi)) atomicAdd(bad, 1u);
         int pauli = c.type == 3 ? 1 : (c.type == 4 ? 3 : 2);  // 1 X, 2 Y, 3 Z
         if (c.type == 0) {                                      // depolarizing (:191-216)
             const float r2 = nz_uniform(nz_mix(h ^ 0x5bd1e9955bd1e995ull));
@@ -122,6 +125,11 @@ __device__ __forceinline__ void flip_block(double2* st, uint64_t b, uint64_t lo,
         const uint64_t traj = idx >> log_ppt, pr = idx & ((1ull << log_ppt) - 1ull);
         const uint64_t i0 = (traj << (log_ppt + 1)) | (pr & mask) | ((pr & ~mask) << 1);
         const uint64_t i1 = i0 | (1ull << c.target);
+        if (bad) {  // both amplitudes must belong to trajectories of [lo, hi)
+            const uint64_t t_lo = (lo - idx0) >> log_ppt, t_hi = (hi - 1 - idx0) >> log_ppt;
+            if ((i0 >> (log_ppt + 1)) < t_lo || (i1 >> (log_ppt + 1)) > t_hi) atomicAdd(bad, 1u);
+            atomicAdd(bad + 1, 1u);  // flips applied (coverage)
+        }
         if (pauli == 3) {
             const double2 v = st[i1];
             st[i1] = make_double2(-v.x, -v.y);
@@ -164,20 +172,37 @@ struct UArgs {
     int log_ppt, log_unit, nch;
     FlipChan ch[kMaxUnitChannels];
 };
-__global__ __launch_bounds__(256) void k_noise_units(UArgs a) {
+// Why this is race-free (the round-2 "batched-load variant" that returned
+// wrong states when lanes also walked blocks wholly outside [lo, hi) was never committed and
+// cannot be recovered, so the argument is made for this kernel and checked on the device):
+//   1. a work-group loads and stores only amplitudes of its own pairs [lo, hi): next_flip
+//      filters every flip by [lo, hi) BEFORE flip_block touches memory, so a block outside the
+//      range (or the foreign part of a block that straddles a shard boundary) costs hashes only;
+//      units are disjoint, so no amplitude has two writers;
+//   2. within one channel two flips are two different pairs (positions strictly increase within
+//      a block, blocks are disjoint) and the pairs of one target partition the amplitudes, so no
+//      two lanes touch the same amplitude;
+//   3. between channels the barrier (s_waitcnt vmcnt(0) then s_barrier) retires every lane's
+//      stores before any lane's next loads, and the work-group's waves share one CU's L1.
+// The failure class left open by the variant's description is a write-back of a loaded value
+// for a flip that the range test rejects AFTER the load (a branch-free batched form: load K
+// flips, select, store K): that rewrites another work-group's pair with a stale value while its
+// owner flips it — exactly "wrong states only when lanes walk blocks outside the range".  This
+// kernel has no such store.  QSIM_NOISE_CHECK=1 runs it with every access range-checked on the
+// device (violations counted with atomics and turned into an error by the launcher);
+// tests/test_batched_refnoise_gpu.py runs that check on units that start and end mid-block.
+template <bool CHECK>
+__global__ __launch_bounds__(256) void k_noise_units(UArgs a, unsigned int* bad) {
     const uint64_t base = ((a.idx0 >> a.log_unit) + blockIdx.x) << a.log_unit;
     const uint64_t lo = base > a.idx0 ? base : a.idx0;
     const uint64_t end = a.idx0 + a.pairs, top = base + (1ull << a.log_unit);
     const uint64_t hi = top < end ? top : end;
-    // only the blocks that overlap [lo, hi) (a batched-load variant of flip_block that also let
-    // lanes walk blocks wholly outside the range returned wrong states; not understood, so such
-    // lanes are never launched; tests/test_batched_refnoise_gpu.py covers ranges that start and
-    // end mid-block)
+    // the blocks that overlap [lo, hi)
     const uint64_t b0 = lo >> kFlipBlockLog, nb = ((hi - 1) >> kFlipBlockLog) - b0 + 1;
     for (int c = 0; c < a.nch; ++c) {
         if (c) __syncthreads();
         for (uint64_t j = threadIdx.x; j < nb; j += blockDim.x)
-            flip_block(a.st, b0 + j, lo, hi, a.idx0, a.log_ppt, a.ch[c]);
+            flip_block(a.st, b0 + j, lo, hi, a.idx0, a.log_ppt, a.ch[c], CHECK ? bad : nullptr);
     }
 }
 
@@ -268,6 +293,8 @@ static bool flip_channel(int type, int qubit, double p, uint64_t key, FlipChan& 
     return true;
 }
 
+uint64_t noise_check_flips = 0;  // flips applied by range-checked launches (qsim_noise_check_flips)
+
 void launch_noise_after_gate(double2* st, int n, const std::vector<NoiseChan>& chans, uint64_t seed,
                              uint64_t& counter, hipStream_t s, Timer* tm, uint64_t batch, uint64_t traj0) {
     const int log_ppt = n - 1;
@@ -300,10 +327,27 @@ void launch_noise_after_gate(double2* st, int n, const std::vector<NoiseChan>& c
             bytes += 32.0 * (double)pairs * std::min(1.0, std::max(0.0, ch.p));
         }
         if (!u.nch) continue;
+        const char* ce = std::getenv("QSIM_NOISE_CHECK");
+        if (ce && std::atoi(ce) != 0) {  // range-checked launch (tests): violations -> error
+            unsigned int* d_bad = nullptr;
+            QSIM_HIPCHK(hipMalloc((void**)&d_bad, 2 * sizeof(unsigned int)));
+            QSIM_HIPCHK(hipMemsetAsync(d_bad, 0, 2 * sizeof(unsigned int), s));
+            hipLaunchKernelGGL(k_noise_units<true>, dim3((unsigned)units), dim3(256), 0, s, u, d_bad);
+            QSIM_HIPCHK(hipGetLastError());
+            unsigned int h_bad[2] = {0, 0};
+            QSIM_HIPCHK(hipMemcpyAsync(h_bad, d_bad, sizeof h_bad, hipMemcpyDeviceToHost, s));
+            QSIM_HIPCHK(hipStreamSynchronize(s));
+            (void)hipFree(d_bad);
+            noise_check_flips += h_bad[1];
+            if (h_bad[0])
+                fail(QSIM_ERR_RUNTIME, "noise unit kernel touched " + std::to_string(h_bad[0]) +
+                                           " amplitudes outside its pairs");
+            continue;
+        }
         TimedLaunch tl(tm, "noise", bytes, s);
         // one work-group per unit (fewer work-groups looping over units measured slower: the
         // walk is latency-bound)
-        hipLaunchKernelGGL(k_noise_units, dim3((unsigned)units), dim3(256), 0, s, u);
+        hipLaunchKernelGGL(k_noise_units<false>, dim3((unsigned)units), dim3(256), 0, s, u, nullptr);
         QSIM_HIPCHK(hipGetLastError());
     }
 }
@@ -595,3 +639,9 @@ void launch_pull_noise_step(const double2* src, double2* dst, int n, uint64_t ba
 }
 
 }  // namespace qsim_hip
+
+extern "C" int qsim_noise_check_flips(uint64_t* flips) {
+    if (!flips) return QSIM_ERR_INVALID_ARGUMENT;
+    *flips = qsim_hip::noise_check_flips;
+    return QSIM_OK;
+}

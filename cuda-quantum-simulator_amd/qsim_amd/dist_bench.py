@@ -113,6 +113,10 @@ def run(args, metric: str, peak_gbps: float) -> None:
     stats = sim.profileStats()
     gates = circuit.getGateCount()
     comm = comm_summary(stats, args.steps, wall, sim.remapBytes())
+    comm["fused_remaps_last_run"] = sim.fusedRemaps()
+    comm["remap_path"] = ("fused: the last pass before the remap stores into the send buffer's slab "
+                          "layout, the step after loads from the receive buffer (no pack / unpack "
+                          "kernels)" if comm["fused_remaps_last_run"] else "pack / unpack kernels")
     comms = [json.loads(b.decode()) for b in grp.all_gather(json.dumps(comm).encode())]
     if rank == 0:
         dom = max((s for s in stats if s["name"] != "alltoall_remap"), key=lambda s: s["ms"],

@@ -325,6 +325,10 @@ int qsim_batch_profile_get(qsim_batch* b, int i, char* name, size_t name_len,
  * pair draws from a counter hash of (seed, counter, pair index).  Asynchronous. */
 int qsim_noise_apply(qsim_state* s, int type, int qubit, double probability, uint64_t seed,
                      uint64_t counter);
+/* Flips applied so far by range-checked noise launches (QSIM_NOISE_CHECK=1: the one-launch
+ * reference noise kernel counts every access outside its work-group's pairs on the device and
+ * fails the call if there is one; tests read this to see the check had work to do). */
+int qsim_noise_check_flips(uint64_t* flips);
 /* NoisySimulator::run (src/NoiseModel.cu:369-382): each gate, then every channel entry in order,
  * one noise pass each; *counter advances by one per pass.  With no channel entries the circuit
  * runs as fused passes (flags = QSIM_RUN_*), else one kernel per gate (the noise interleaves). */

@@ -207,3 +207,32 @@ def test_pulled_noise_equals_push_16q(qsim, gpu_ready, monkeypatch):
     _lib.check(_lib.hip.qsim_batch_device_ptr(s._h, ctypes.byref(ptr2)))
     assert ptr.value == ptr2.value
     assert np.array_equal(np.stack([s.getStateVector(t) for t in (0, 63, 127)]), out[0])
+
+
+@pytest.mark.parametrize("n,B,seed,traj0", [(6, 5, 5, 3), (3, 50, 7, 3), (7, 9, 8, 1), (9, 6, 5, 2)])
+def test_one_launch_noise_accesses_stay_in_unit(qsim, oracle, gpu_ready, monkeypatch, n, B, seed, traj0):
+    """the one-launch kernel (k_noise_units) run range-checked on the device
+    (QSIM_NOISE_CHECK=1: every load / store outside the work-group's pairs is counted and fails
+    the run) on units whose pairs start and end mid-block (trajectory offsets at n <= 8): no
+    violation, flips applied, and the states equal the oracle."""
+    import ctypes
+    from qsim_amd import _lib
+    monkeypatch.setenv("QSIM_NOISE_UNIT_MIN", "1")
+    monkeypatch.setenv("QSIM_NOISE_PULL", "0")
+    monkeypatch.setenv("QSIM_NOISE_CHECK", "1")
+    before = ctypes.c_uint64(0)
+    _lib.check(_lib.hip.qsim_noise_check_flips(ctypes.byref(before)))
+    c = _circuit(qsim, n, 12, seed)
+    nm = qsim.NoiseModel()
+    nm.addDepolarizingAll(n, 0.3)
+    s = qsim.BatchedSimulator(n, B, nm, noise=qsim.BatchedNoise.Reference)
+    s.setSeed(seed)
+    s.setTrajectoryOffset(traj0)
+    s.run(c)  # raises if any access left its unit
+    after = ctypes.c_uint64(0)
+    _lib.check(_lib.hip.qsim_noise_check_flips(ctypes.byref(after)))
+    assert after.value > before.value
+    entries = [(0, q, 0.3) for q in range(n)]
+    whole, _ = oracle.batched_reference_run(n, traj0 + B, oracle.gates_of(c), entries, seed)
+    for t in range(B):
+        np.testing.assert_allclose(s.getStateVector(t), whole[traj0 + t], atol=1e-12, rtol=0)
