@@ -88,7 +88,14 @@ static uint64_t deposit_bits(uint64_t v, uint64_t mask) {  // bit j of v -> j-th
 // are only marked when `ref` aliases `steps`, i.e. on rank 0).  QSIM_DIST_PIVOTS caps m
 // (default kMaxPivots); QSIM_DIST_PIVOT_PLAN=0: one pivot by the cheaper gate-level score
 // (trailing / leading gates that do not touch the position).
-static void mark_overlap(std::vector<DStep>& steps, int L, int world, const std::vector<DStep>& ref) {
+// carry: pivots of the previous run's last exchange whose parts are still in flight when this
+// run starts (qsim_dist_run merges that run's last step into this one's first): the first ops
+// step's leading passes that avoid them run per part too (role bit 2 on step 0).
+// next_ops: the first ops step of the NEXT run of the circuit (from this run's end map, rank 0's
+// lowering): the last remap's pivots are also scored by the passes of it they let run per part
+// (carried into the next run, qsim_dist_run).
+static void mark_overlap(std::vector<DStep>& steps, int L, int world, const std::vector<DStep>& ref,
+                         uint64_t carry = 0, const std::vector<Op>* next_ops = nullptr) {
     static const int enabled = [] {
         const char* e = std::getenv("QSIM_DIST_OVERLAP");
         return e ? std::atoi(e) : 1;
@@ -102,6 +109,7 @@ static void mark_overlap(std::vector<DStep>& steps, int L, int world, const std:
         return e ? std::max(1, std::min(kMaxPivots, std::atoi(e))) : kMaxPivots;
     }();
     if (!enabled || L < 8) return;
+    if (carry && !steps.empty() && steps[0].kind == 0) steps[0].role |= 2;
     const int min_gates = 4;
     const double R = 50.0 / std::max(2, world);
     for (size_t i = 1; i + 1 < steps.size(); ++i) {
@@ -129,18 +137,34 @@ static void mark_overlap(std::vector<DStep>& steps, int L, int world, const std:
         const DStep& rA = ref[i - 1];
         const DStep& rB = ref[i + 1];
         if (by_plan && !rA.ops.empty() && !rB.ops.empty() && !cand.empty()) {
-            const uint64_t avoidA0 = (A.role & 2) ? steps[i - 2].pmask : 0ull;
+            const uint64_t avoidA0 = (A.role & 2) ? (i >= 2 ? steps[i - 2].pmask : carry) : 0ull;
             // T of a pivot set (pass counts in units of one pass); +inf when planning failed
             auto model = [&](uint64_t set) {
-                const Plan pA = plan_fused(rA.ops, L, -1, avoidA0 | set);
-                const Plan pB = plan_fused(rB.ops, L, -1, set);
+                const Plan pA = plan_fused(rA.ops, L, -1, set, avoidA0);
+                const Plan pB = plan_fused(rB.ops, L, -1, 0, set);
                 const int na = (int)pA.passes.size(), nb = (int)pB.passes.size();
-                int t = 0, h = 0;
-                while (t < na && pass_avoids(pA.passes[na - 1 - t], set)) ++t;
+                int t = 0, h = 0, ha = 0;
+                // A's leading passes that run per part of the exchange before it (or of the
+                // previous run's last one, `carry`) are hidden behind that exchange; the trailing
+                // ones that avoid this set feed this one (a pass counts once: head first, as the
+                // run splits a step)
+                if (avoidA0)
+                    while (ha < na && pass_avoids(pA.passes[ha], avoidA0)) ++ha;
+                while (t < na - ha && pass_avoids(pA.passes[na - 1 - t], set)) ++t;
                 while (h < nb && pass_avoids(pB.passes[h], set)) ++h;
                 const double K = (double)(1 << __builtin_popcountll(set));
                 if (t + h == 0) return 1e30;
-                return std::max(R + (na - t) + (nb - h) + (t + h) / K, na + nb + R / K);
+                // The next run's first pass, if it avoids the set, is hidden behind this remap too
+                // (carried, qsim_dist_run); at most one is credited — more would only shorten that
+                // run's own tail, whose remap hides it anyway (crediting them all makes the greedy
+                // pick few pivots: big parts, a long exposed last part).  A's leading `ha` passes
+                // were hidden behind the remap before this one and cost nothing here.
+                int hn = 0;
+                if (next_ops && !next_ops->empty() && i + 2 == steps.size() && h == nb && !(B.role & 1)) {
+                    const Plan pN = plan_fused(*next_ops, L, -1, set);
+                    hn = !pN.passes.empty() && pass_avoids(pN.passes[0], set) ? 1 : 0;
+                }
+                return std::max(R + (na - t - ha) + (nb - h) + (t + h + hn) / K - hn, na + nb + R / K);
             };
             auto score_all = [&](uint64_t base, const std::vector<int>& cs) {
                 std::vector<double> sc(cs.size(), 1e30);
@@ -431,6 +455,7 @@ static std::vector<DStep> plan_dist_core(const qsim_gate* gates, size_t count, i
 namespace {
 struct PivotMemo {
     int n, g;
+    uint64_t carry;
     std::vector<qsim_gate> gates;
     std::vector<int> perm;
     std::vector<uint64_t> pmask;  // per step (0: none)
@@ -442,12 +467,17 @@ uint64_t g_pivot_clock = 0;
 }  // namespace
 
 static std::vector<DStep> plan_dist(const qsim_gate* gates, size_t count, int n, int g, int rank,
-                                    std::vector<int>& perm) {
+                                    std::vector<int>& perm, uint64_t carry = 0) {
     const std::vector<int> perm_in = perm;
     std::vector<DStep> steps = plan_dist_core(gates, count, n, g, rank, perm);
     const int L = n - g;
+    static const int overlap = [] {
+        const char* e = std::getenv("QSIM_DIST_OVERLAP");
+        return e ? std::atoi(e) : 1;
+    }();
+    if (!overlap || L < 8 || steps.empty() || steps[0].kind != 0) carry = 0;
     auto same = [&](const PivotMemo& m) {
-        return m.n == n && m.g == g && m.perm == perm_in && m.gates.size() == count &&
+        return m.n == n && m.g == g && m.carry == carry && m.perm == perm_in && m.gates.size() == count &&
                (count == 0 || std::memcmp(m.gates.data(), gates, count * sizeof(qsim_gate)) == 0);
     };
     {
@@ -455,6 +485,7 @@ static std::vector<DStep> plan_dist(const qsim_gate* gates, size_t count, int n,
         for (PivotMemo& m : g_pivots)
             if (same(m) && m.pmask.size() == steps.size()) {
                 m.used = ++g_pivot_clock;
+                if (carry) steps[0].role |= 2;
                 for (size_t k = 0; k < steps.size(); ++k)
                     if (m.pmask[k]) {
                         steps[k].pmask = m.pmask[k];
@@ -465,15 +496,27 @@ static std::vector<DStep> plan_dist(const qsim_gate* gates, size_t count, int n,
                 return steps;
             }
     }
+    // the next run's first ops step (rank 0's lowering, from this run's end map: the same on every
+    // rank), for scoring the last remap's pivots by the passes it can carry
+    std::vector<Op> next_ops;
+    static const bool carry_on = [] {  // (off by default: see qsim_dist_run)
+        const char* e = std::getenv("QSIM_DIST_CARRY");
+        return e != nullptr && std::atoi(e) != 0;
+    }();
+    if (carry_on && overlap && L >= 8) {
+        std::vector<int> pn = perm;
+        const std::vector<DStep> nxt = plan_dist_core(gates, count, n, g, 0, pn);
+        if (!nxt.empty() && nxt[0].kind == 0) next_ops = nxt[0].ops;
+    }
     if (rank == 0) {
-        mark_overlap(steps, L, 1 << g, steps);
+        mark_overlap(steps, L, 1 << g, steps, carry, &next_ops);
     } else {
         std::vector<int> p0 = perm_in;
         const std::vector<DStep> ref = plan_dist_core(gates, count, n, g, 0, p0);
         if (ref.size() != steps.size()) fail(QSIM_ERR_RUNTIME, "exchange skeleton mismatch");
-        mark_overlap(steps, L, 1 << g, ref);
+        mark_overlap(steps, L, 1 << g, ref, carry, &next_ops);
     }
-    PivotMemo m{n, g, std::vector<qsim_gate>(gates, gates + count), perm_in, {}, 0};
+    PivotMemo m{n, g, carry, std::vector<qsim_gate>(gates, gates + count), perm_in, {}, 0};
     for (const DStep& st : steps) m.pmask.push_back(st.kind == 1 ? st.pmask : 0ull);
     std::lock_guard<std::mutex> l(g_pivot_mu);
     m.used = ++g_pivot_clock;
@@ -544,6 +587,13 @@ __global__ __launch_bounds__(256) void k_exchange_copy(XArgs a, uint64_t lo, int
             fail(QSIM_ERR_DEVICE, std::string("RCCL error: ") + ncclGetErrorString(r_)); \
     } while (0)
 
+// A prepared ops step (see prepare_step): its plan, kernels and the pass ranges around pivots.
+struct StepRun {
+    const Plan* plan = nullptr;
+    const JitModule* jm = nullptr;
+    size_t j1 = 0, j2 = 0, np = 0;
+};
+
 // One rank's share: its amplitudes and the exchange staging buffers.
 struct Shard {
     int rank = 0;
@@ -599,6 +649,8 @@ struct qsim_dist {
     struct RunPlan {
         std::vector<qsim_gate> gates;
         std::vector<int> perm_in, perm_out;
+        uint64_t carry_in = 0;  // pivots of the previous run's exchange still in flight at the start
+        bool in_use = false;    // a deferred step of this plan is pending (never evicted then)
         std::vector<std::vector<DStep>> steps;              // per shard
         std::vector<std::vector<std::unique_ptr<PlanCache>>> fplans;  // per shard, per step
         std::vector<std::unique_ptr<FusedVariant>> fpack, funpack;    // per shard (the first exchange)
@@ -606,6 +658,22 @@ struct qsim_dist {
         uint64_t used = 0;
     };
     int fused_remaps = 0;  // exchanges of the last run whose pack / unpack ran inside the passes
+    // Cross-run overlap: a run whose last step is the per-part head of an overlapped remap (every
+    // pass of it avoids the pivots) leaves that step pending; the next run of a circuit runs its
+    // first step's leading passes per part too, interleaved with it (part h of both as soon as
+    // part h has landed), so the remap also hides the next run's first passes.  Anything else
+    // that touches the state runs it first (flush_carry).
+    struct Carry {
+        bool active = false;
+        uint64_t pmask = 0;  // the remap's pivots (the run's standard positions)
+        int parts = 0;
+        RunPlan* rp = nullptr;
+        size_t step = 0;
+        std::vector<StepRun> runs;
+        std::vector<uint64_t> pbs;
+        std::vector<double2*> homes, alts;
+    } carry;
+    int carried = 0;  // runs of this object whose first step merged a carried step
     std::vector<std::unique_ptr<RunPlan>> run_plans;
     uint64_t run_clock = 0;
     Timer timer;
@@ -1073,16 +1141,11 @@ double allreduce_sum(qsim_dist* d, double local) {
 //          event its half-exchange waits for.
 // The plan is the step's ordinary fused plan with tiles padded away from both pivots, so the
 // split costs no extra HBM pass.  Per-gate mode (or a plan without such passes) runs whole.
-struct StepRun {
-    const Plan* plan = nullptr;
-    const JitModule* jm = nullptr;
-    size_t j1 = 0, j2 = 0, np = 0;
-};
 StepRun prepare_step(qsim_dist* d, const std::vector<Op>& ops, int flags, PlanCache& pc, uint64_t pb,
                      uint64_t pa) {
     StepRun r;
     if (ops.empty() || !(flags & QSIM_RUN_FUSED)) return r;
-    PlanCache::Entry& pe = pc.get(ops, d->L, d->stream, pb | pa);
+    PlanCache::Entry& pe = pc.get(ops, d->L, d->stream, pa, pb);
     r.plan = &pe.plan;
     r.jm = jit_for(pe.jit, pe.plan, d->L);
     r.np = pe.plan.passes.size();
@@ -1179,13 +1242,14 @@ void decide_fused(qsim_dist* d, qsim_dist::RunPlan& rp, int flags) {
         auto up = std::make_unique<qsim_dist::FusedVariant>();
         try {
             const uint64_t pa = (A.role & 1) ? ex.pmask : 0ull;
-            pk->plan = plan_fused(A.ops, d->L, -1, pa);
+            const uint64_t pb = (A.role & 2) ? rp.carry_in : 0ull;
+            pk->plan = plan_fused(A.ops, d->L, -1, pa, pb);
             const FusedPass& la = pk->plan.passes.back();
             if (la.single >= 0 || la.h < 4) continue;
             relayout_last_pass(pk->plan, d->L, sg.data());
             std::vector<Op> bops;
             for (const Op& op : B.ops) bops.push_back(map_op_positions(op, sg));
-            up->plan = plan_fused(bops, d->L, -1, (B.role & 2) ? pm_sigma : 0ull);
+            up->plan = plan_fused(bops, d->L, -1, 0ull, (B.role & 2) ? pm_sigma : 0ull);
             const FusedPass& lb = up->plan.passes.back();
             if (lb.single >= 0 || lb.h < 4) continue;
             relayout_last_pass(up->plan, d->L, inv.data());
@@ -1210,9 +1274,9 @@ StepRun prepare_variant(qsim_dist* d, qsim_dist::FusedVariant& v, uint64_t pb, u
     return r;
 }
 // The cached plan of this run (same gates, same start map), or a new one (LRU of 8).
-qsim_dist::RunPlan& run_plan(qsim_dist* d, const qsim_gate* gates, size_t count) {
+qsim_dist::RunPlan& run_plan(qsim_dist* d, const qsim_gate* gates, size_t count, uint64_t carry) {
     for (auto& rp : d->run_plans)
-        if (rp->perm_in == d->perm && rp->gates.size() == count &&
+        if (rp->perm_in == d->perm && rp->carry_in == carry && rp->gates.size() == count &&
             (count == 0 || std::memcmp(rp->gates.data(), gates, count * sizeof(qsim_gate)) == 0)) {
             rp->used = ++d->run_clock;
             return *rp;
@@ -1220,10 +1284,11 @@ qsim_dist::RunPlan& run_plan(qsim_dist* d, const qsim_gate* gates, size_t count)
     auto rp = std::make_unique<qsim_dist::RunPlan>();
     rp->gates.assign(gates, gates + count);
     rp->perm_in = d->perm;
+    rp->carry_in = carry;
     // Plan per shard (ranks differ only in which global controls/phases apply).
     for (const Shard& sh : d->shards) {
         std::vector<int> perm = d->perm;
-        rp->steps.push_back(plan_dist(gates, count, d->n, d->g, sh.rank, perm));
+        rp->steps.push_back(plan_dist(gates, count, d->n, d->g, sh.rank, perm, carry));
         rp->perm_out = perm;
         rp->fplans.emplace_back();
         for (const DStep& s : rp->steps.back())
@@ -1231,13 +1296,30 @@ qsim_dist::RunPlan& run_plan(qsim_dist* d, const qsim_gate* gates, size_t count)
     }
     rp->used = ++d->run_clock;
     if (d->run_plans.size() >= 8) {
-        auto lru = std::min_element(d->run_plans.begin(), d->run_plans.end(),
-                                    [](const auto& a, const auto& b) { return a->used < b->used; });
+        auto lru = std::min_element(d->run_plans.begin(), d->run_plans.end(), [](const auto& a, const auto& b) {
+            return a->in_use != b->in_use ? !a->in_use : a->used < b->used;  // (a pending step's plan stays)
+        });
         QSIM_HIPCHK(hipStreamSynchronize(d->stream));  // its compiled kernels may still be queued
         d->run_plans.erase(lru);
     }
     d->run_plans.push_back(std::move(rp));
     return *d->run_plans.back();
+}
+// Run the carried step (the per-part head of the previous run's last remap) now, part by part as
+// each part lands; every entry that touches the state, or a run that cannot merge it, calls this.
+void flush_carry(qsim_dist* d) {
+    qsim_dist::Carry& c = d->carry;
+    if (!c.active) return;
+    for (int h = 0; h < c.parts; ++h) {
+        QSIM_HIPCHK(hipStreamWaitEvent(d->stream, d->pev[24 + h], 0));
+        for (size_t i = 0; i < d->shards.size(); ++i)
+            if (c.runs[i].plan)
+                run_part(d, d->shards[i], c.rp->steps[i][c.step].ops, c.runs[i], 0, c.runs[i].j1, c.pbs[i], h,
+                         c.homes[i], c.alts[i]);
+    }
+    c.active = false;
+    c.rp->in_use = false;
+    c.rp = nullptr;
 }
 // Physical (rank-major) amplitudes -> logical index order (dst: 2 * 2^n doubles).  The map
 // i -> p(i) moves bit q to perm[q], so p is the OR of per-11-bit-chunk tables; threads split i.
@@ -1420,6 +1502,8 @@ int qsim_dist_reset(qsim_dist* d) {
     return dguard_comm(d, [&] {
         need(d);
         QSIM_HIPCHK(hipSetDevice(d->device));
+        flush_carry(d);  // (the previous run's last step, if it was left pending)
+        QSIM_HIPCHK(hipSetDevice(d->device));
         init_zero(d);
     });
 }
@@ -1448,11 +1532,20 @@ int qsim_dist_run(qsim_dist* d, const qsim_gate* gates, size_t count, int flags)
         }
         d->fresh = false;
         d->sent_bytes = 0.0;
-        qsim_dist::RunPlan& rp = run_plan(d, gates, count);
+        static const bool carry_on = [] {  // QSIM_DIST_CARRY=1: carry the last step into the next run
+            const char* e = std::getenv("QSIM_DIST_CARRY");
+            return e != nullptr && std::atoi(e) != 0;
+        }();
+        if (!(flags & QSIM_RUN_FUSED) || !carry_on) flush_carry(d);
+        const uint64_t carry_in = d->carry.active ? d->carry.pmask : 0ull;
+        qsim_dist::RunPlan& rp = run_plan(d, gates, count, carry_in);
         const auto& plans = rp.steps;
         const size_t S = d->shards.size();
         for (size_t i = 1; i < S; ++i)
             if (plans[i].size() != plans[0].size()) fail(QSIM_ERR_RUNTIME, "exchange skeleton mismatch");
+        // merge the carried step into this run's first one (its leading passes per part too)
+        const bool merge = d->carry.active && !plans[0].empty() && plans[0][0].kind == 0 && (plans[0][0].role & 2);
+        if (!merge) flush_carry(d);
         d->overlapped = 0;
         d->fused_remaps = 0;
         decide_fused(d, rp, flags);
@@ -1469,7 +1562,8 @@ int qsim_dist_run(qsim_dist* d, const qsim_gate* gates, size_t count, int flags)
                                      : " O" + std::to_string(st.ops.size()) + "r" + std::to_string(st.role);
             std::fprintf(stderr, "%s\n", line.c_str());
         }
-        int pending = 0;  // parts of an overlapped remap still to be waited for (0: none)
+        int pending = merge ? d->carry.parts : 0;  // parts of an overlapped remap still to be waited for
+        if (merge) ++d->carried;
         auto wait_pending = [&]() {
             for (int h = 0; h < pending; ++h) QSIM_HIPCHK(hipStreamWaitEvent(d->stream, d->pev[24 + h], 0));
             pending = 0;
@@ -1501,7 +1595,7 @@ int qsim_dist_run(qsim_dist* d, const qsim_gate* gates, size_t count, int flags)
                 continue;
             }
             // ops step: head per half (after the exchange before), middle, tail per half
-            const uint64_t pb = (s0.role & 2) ? plans[0][k - 1].pmask : 0ull;
+            const uint64_t pb = (s0.role & 2) ? (k == 0 ? carry_in : plans[0][k - 1].pmask) : 0ull;
             const uint64_t pa = (s0.role & 1) ? plans[0][k + 1].pmask : 0ull;
             std::vector<StepRun> runs(S);
             // fused first exchange: step 0 stores its last pass into the send buffer (slab
@@ -1526,13 +1620,47 @@ int qsim_dist_run(qsim_dist* d, const qsim_gate* gates, size_t count, int flags)
                 }
             }
             const bool head = pb && pending;
+            // the run's last step, every pass of it in the per-part head: leave it pending (the next
+            // run merges it into its first step's head; anything else flushes it)
+            if (head && carry_on && k + 1 == plans[0].size() && !pa && (flags & QSIM_RUN_FUSED) && !(k == 0 && merge)) {
+                bool all = true;
+                for (size_t i = 0; i < S; ++i) all = all && runs[i].plan && runs[i].j1 == runs[i].np;
+                if (all) {
+                    qsim_dist::Carry& c = d->carry;
+                    c.active = true;
+                    c.pmask = pb;
+                    c.parts = pending;
+                    c.rp = &rp;
+                    c.step = k;
+                    c.runs = runs;
+                    c.pbs = pbs;
+                    c.homes = homes;
+                    c.alts = alts;
+                    rp.in_use = true;
+                    pending = 0;
+                    continue;
+                }
+            }
             if (head) {
+                const bool carried = k == 0 && merge;
                 for (int h = 0; h < pending; ++h) {
                     QSIM_HIPCHK(hipStreamWaitEvent(d->stream, d->pev[24 + h], 0));
+                    if (carried) {  // part h of the previous run's last step, then part h of this one
+                        const qsim_dist::Carry& c = d->carry;
+                        for (size_t i = 0; i < S; ++i)
+                            if (c.runs[i].plan)
+                                run_part(d, d->shards[i], c.rp->steps[i][c.step].ops, c.runs[i], 0, c.runs[i].j1,
+                                         c.pbs[i], h, c.homes[i], c.alts[i]);
+                    }
                     for (size_t i = 0; i < S; ++i)
                         if (runs[i].plan)
                             run_part(d, d->shards[i], plans[i][k].ops, runs[i], 0, runs[i].j1, pbs[i], h, homes[i],
                                      alts[i]);
+                }
+                if (carried) {
+                    d->carry.active = false;
+                    d->carry.rp->in_use = false;
+                    d->carry.rp = nullptr;
                 }
             }
             wait_pending();
@@ -1583,6 +1711,8 @@ int qsim_dist_sync(qsim_dist* d) {
     return dguard_comm(d, [&] {
         need(d);
         QSIM_HIPCHK(hipSetDevice(d->device));
+        flush_carry(d);  // (the previous run's last step, if it was left pending)
+        QSIM_HIPCHK(hipSetDevice(d->device));
         stream_wait(d, d->comm_stream);
         stream_wait(d, d->copy_stream);
         stream_wait(d, d->stream);
@@ -1600,6 +1730,8 @@ int qsim_dist_local_state(qsim_dist* d, double* dst) {
     return dguard_comm(d, [&] {
         need(d);
         QSIM_HIPCHK(hipSetDevice(d->device));
+        flush_carry(d);  // (the previous run's last step, if it was left pending)
+        QSIM_HIPCHK(hipSetDevice(d->device));
         const size_t bytes = sizeof(double2) << d->L;
         for (size_t i = 0; i < d->shards.size(); ++i)  // virtual mode: all shards, rank order
             QSIM_HIPCHK(hipMemcpyAsync((char*)dst + i * bytes, d->shards[i].d, bytes,
@@ -1611,6 +1743,8 @@ int qsim_dist_local_state(qsim_dist* d, double* dst) {
 int qsim_dist_gather_state(qsim_dist* d, double* dst) {
     return dguard_comm(d, [&] {
         need(d);
+        QSIM_HIPCHK(hipSetDevice(d->device));
+        flush_carry(d);  // (the previous run's last step, if it was left pending)
         QSIM_HIPCHK(hipSetDevice(d->device));
         const uint64_t shard = 1ull << d->L;
         const bool root = d->virt || d->shards[0].rank == 0;
@@ -1662,6 +1796,8 @@ int qsim_dist_total_probability(qsim_dist* d, double* out) {
     return dguard_comm(d, [&] {
         need(d);
         QSIM_HIPCHK(hipSetDevice(d->device));
+        flush_carry(d);  // (the previous run's last step, if it was left pending)
+        QSIM_HIPCHK(hipSetDevice(d->device));
         double local = 0.0;
         for (const Shard& s : d->shards)
             local += reduce_norm(s.d, d->L, -1, d->d_partials, d->d_result, d->stream);
@@ -1672,6 +1808,8 @@ int qsim_dist_total_probability(qsim_dist* d, double* out) {
 int qsim_dist_prob_bit_zero(qsim_dist* d, int q, double* out) {
     return dguard_comm(d, [&] {
         need(d);
+        QSIM_HIPCHK(hipSetDevice(d->device));
+        flush_carry(d);  // (the previous run's last step, if it was left pending)
         if (q < 0 || q >= d->n) fail(QSIM_ERR_INVALID_ARGUMENT, "bit out of range");
         QSIM_HIPCHK(hipSetDevice(d->device));
         const int p = d->perm[q];
@@ -1769,22 +1907,25 @@ int qsim_dist_plan(int n, int world, int rank, const qsim_gate* gates, size_t co
     });
 }
 
-int qsim_dist_plan_passes(int n, int world, int rank, const qsim_gate* gates, size_t count,
-                          int32_t* perm_inout, int32_t* passes, size_t cap, size_t* n_steps) {
+int qsim_dist_plan_passes_carry(int n, int world, int rank, const qsim_gate* gates, size_t count,
+                                int32_t* perm_inout, uint64_t* carry_inout, int32_t* passes, size_t cap,
+                                size_t* n_steps) {
     return dguard([&] {
         const int g = log2_exact(world);
         check_sizes(n, g);
         if (rank < 0 || rank >= world) fail(QSIM_ERR_INVALID_ARGUMENT, "rank out of range");
         std::vector<int> perm(n);
         for (int q = 0; q < n; ++q) perm[q] = perm_inout ? perm_inout[q] : q;
-        const std::vector<DStep> st = plan_dist(gates, count, n, g, rank, perm);
+        const uint64_t carry = carry_inout ? *carry_inout : 0ull;
+        const std::vector<DStep> st = plan_dist(gates, count, n, g, rank, perm, carry);
         const int L = n - g;
+        uint64_t carry_out = 0;
         for (size_t k = 0; k < st.size(); ++k) {
             int np = 0, head = 0, tail = 0;
             if (st[k].kind == 0 && !st[k].ops.empty()) {  // as prepare_step plans it
-                const uint64_t pb = (st[k].role & 2) ? st[k - 1].pmask : 0ull;
+                const uint64_t pb = (st[k].role & 2) ? (k == 0 ? carry : st[k - 1].pmask) : 0ull;
                 const uint64_t pa = (st[k].role & 1) ? st[k + 1].pmask : 0ull;
-                const Plan pl = plan_fused(st[k].ops, L, -1, pb | pa);
+                const Plan pl = plan_fused(st[k].ops, L, -1, pa, pb);
                 np = (int)pl.passes.size();
                 if (pb)
                     while (head < np && pass_avoids(pl.passes[head], pb)) ++head;
@@ -1796,11 +1937,21 @@ int qsim_dist_plan_passes(int n, int world, int rank, const qsim_gate* gates, si
                 passes[3 * k + 1] = head;
                 passes[3 * k + 2] = tail;
             }
+            // a last step run wholly per part is carried into the next run (qsim_dist_run)
+            if (k + 1 == st.size() && k > 0 && st[k].kind == 0 && (st[k].role & 2) && !(st[k].role & 1) && np > 0 &&
+                head == np)
+                carry_out = st[k - 1].pmask;
         }
         if (n_steps) *n_steps = st.size();
         if (perm_inout)
             for (int q = 0; q < n; ++q) perm_inout[q] = perm[q];
+        if (carry_inout) *carry_inout = carry_out;
     });
+}
+
+int qsim_dist_plan_passes(int n, int world, int rank, const qsim_gate* gates, size_t count,
+                          int32_t* perm_inout, int32_t* passes, size_t cap, size_t* n_steps) {
+    return qsim_dist_plan_passes_carry(n, world, rank, gates, count, perm_inout, nullptr, passes, cap, n_steps);
 }
 
 int qsim_dist_plan_memo_clear(void) {

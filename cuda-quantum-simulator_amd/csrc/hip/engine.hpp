@@ -187,7 +187,9 @@ constexpr int stage_threads(int h) { return (64 << h) >> stage_rb(h); }
 constexpr int kTileR0 = 6;    // contiguous run bits of a staged tile (QSIM_TILE_R0 in 4..6)
 // hmax < 0: the process default (kTileHDefault, or QSIM_TILE_HMAX up to kTileHMax).
 // avoid: qubits no tile may contain (ops never act on them; only tile padding is affected).
-Plan plan_fused(const std::vector<Op>& ops, int n, int hmax = -1, uint64_t avoid = 0);
+// avoid_first: the same for the plan's FIRST pass only (the sharded engine: the pivots of the
+// remap before a step steer its leading pass, those of the remap after it every pass).
+Plan plan_fused(const std::vector<Op>& ops, int n, int hmax = -1, uint64_t avoid = 0, uint64_t avoid_first = 0);
 // Rebuild the last pass of `plan` (staged) as a relayout pass that stores load position p at
 // tau[p] (a permutation of 0..n-1; the sharded engine's fused remap pack / unpack).
 void relayout_last_pass(Plan& plan, int n, const int* tau);
@@ -330,7 +332,7 @@ const JitModule* jit_for(JitState& js, const Plan& plan, int n);
 struct PlanCache {
     struct Entry {
         int n = -1, h = -1;  // h: the tile height the plan was made for
-        uint64_t avoid = 0;
+        uint64_t avoid = 0, avoid_first = 0;
         std::vector<Op> key;
         Plan plan;
         JitState jit;
@@ -340,7 +342,8 @@ struct PlanCache {
     std::vector<std::unique_ptr<Entry>> entries;
     uint64_t clock = 0;
     // stream: where the owner runs this cache's plans (drained before a plan is evicted)
-    Entry& get(const std::vector<Op>& ops, int n_qubits, hipStream_t stream, uint64_t avoid = 0);
+    Entry& get(const std::vector<Op>& ops, int n_qubits, hipStream_t stream, uint64_t avoid = 0,
+               uint64_t avoid_first = 0);
     // insert a plan computed elsewhere under `ops` (relabeling plans its candidates itself)
     void put(std::vector<Op> ops, int n_qubits, Plan plan, hipStream_t stream);
 };

@@ -368,7 +368,7 @@ struct PassChoice {
 //     a time, each time taking the choice that lets the most upcoming gates into the pass.
 // avoid: qubits a tile should contain only when that lets more gates in (ties go to others).
 static std::vector<PassChoice> choose_passes(const std::vector<Op>& ops, int n, int r0, int nfree,
-                                             bool lookahead, uint64_t avoid) {
+                                             bool lookahead, uint64_t avoid_all, uint64_t avoid_first = 0) {
     const uint64_t low = (1ull << r0) - 1ull;
     const bool co = tile_ctrl_out() && nfree + r0 >= 10;  // (staged tiles only)
     std::vector<PassChoice> out;
@@ -397,6 +397,7 @@ static std::vector<PassChoice> choose_passes(const std::vector<Op>& ops, int n, 
             continue;
         }
         uint64_t hi = 0;
+        const uint64_t avoid = avoid_all | (out.empty() ? avoid_first : 0ull);
         if (lookahead) {
             qm.resize(rem.size());
             nm.resize(rem.size());
@@ -462,7 +463,7 @@ static std::vector<PassChoice> choose_passes(const std::vector<Op>& ops, int n, 
 // the fewest remaining gates survive each step.  The first state to run out of gates gives the
 // plan.  W-HC 30q: 7 passes (one-tile-at-a-time lookahead) -> 5.
 static std::vector<PassChoice> beam_passes(const std::vector<Op>& ops, int n, int heff, int width,
-                                           uint64_t avoid) {
+                                           uint64_t avoid_all, uint64_t avoid_first = 0) {
     const size_t window = 512;
     const bool co = tile_ctrl_out();
     std::vector<uint64_t> qm(ops.size()), nm(ops.size());
@@ -556,6 +557,7 @@ static std::vector<PassChoice> beam_passes(const std::vector<Op>& ops, int n, in
         std::vector<St> next;
         std::vector<std::vector<int>> seen;
         for (const St& s : states) {
+            const uint64_t avoid = avoid_all | (s.hist.empty() ? avoid_first : 0ull);
             for (int r0 = 6; r0 >= 4; --r0) {
                 const uint64_t low = run_mask(r0);
                 const int nfree = 6 + heff - r0;
@@ -614,9 +616,10 @@ static bool same_op(const Op& a, const Op& b) {
 }
 
 PlanCache::Entry& PlanCache::get(const std::vector<Op>& ops, int n_qubits, hipStream_t stream,
-                                 uint64_t avoid) {
+                                 uint64_t avoid, uint64_t avoid_first) {
     for (auto& e : entries) {
         bool hit = e->n == n_qubits && e->h == tile_height_default() && e->avoid == avoid &&
+                   e->avoid_first == avoid_first &&
                    e->key.size() == ops.size();
         for (size_t i = 0; hit && i < ops.size(); ++i) hit = same_op(e->key[i], ops[i]);
         if (hit) {
@@ -632,7 +635,8 @@ PlanCache::Entry& PlanCache::get(const std::vector<Op>& ops, int n_qubits, hipSt
         entries.erase(lru);
     }
     auto e = std::make_unique<Entry>();
-    e->plan = plan_fused(ops, n_qubits, -1, avoid);
+    e->plan = plan_fused(ops, n_qubits, -1, avoid, avoid_first);
+    e->avoid_first = avoid_first;
     e->key = ops;
     e->n = n_qubits;
     e->h = tile_height_default();
@@ -831,7 +835,7 @@ void relayout_last_pass(Plan& plan, int n, const int* tau) {
     plan.passes.back() = p;
 }
 
-Plan plan_fused(const std::vector<Op>& ops, int n, int hmax, uint64_t avoid) {
+Plan plan_fused(const std::vector<Op>& ops, int n, int hmax, uint64_t avoid, uint64_t avoid_first) {
     if (hmax < 0) hmax = tile_height_default();
     Plan plan;
     auto add_single = [&](const Op& op) {
@@ -857,7 +861,7 @@ Plan plan_fused(const std::vector<Op>& ops, int n, int hmax, uint64_t avoid) {
         if (r0_pin && heff >= 4 && r0 != std::min(6, std::max(4, r0_pin))) continue;
         for (int la = 0; la <= (heff >= 4 ? 1 : 0); ++la) {
             if (strat_pin >= 0 && heff >= 4 && la != (strat_pin ? 1 : 0)) continue;
-            std::vector<PassChoice> c = choose_passes(ops, n, r0, 6 + heff - r0, la != 0, avoid);
+            std::vector<PassChoice> c = choose_passes(ops, n, r0, 6 + heff - r0, la != 0, avoid, avoid_first);
             for (PassChoice& ch : c) ch.r0 = r0;
             if (best.empty() || c.size() < best.size()) best.swap(c);
         }
@@ -867,14 +871,16 @@ Plan plan_fused(const std::vector<Op>& ops, int n, int hmax, uint64_t avoid) {
     if (beam > 0 && heff >= 4 && n >= beam_min_q && !r0_pin && strat_pin < 0 && best.size() > 1) {
         // width shrinks with the circuit so the search stays ~O(10^8) simple steps
         const int w = std::max(2, (int)(beam * 256.0 / std::max<size_t>(256, ops.size())));
-        std::vector<PassChoice> c = beam_passes(ops, n, heff, w, avoid);
+        std::vector<PassChoice> c = beam_passes(ops, n, heff, w, avoid, avoid_first);
         if (!c.empty() && c.size() < best.size()) best.swap(c);
     }
-    for (PassChoice& ch : best) {
+    for (size_t pi = 0; pi < best.size(); ++pi) {
+        PassChoice& ch = best[pi];
         if (ch.single) {
             add_single(ch.ops.front());
             continue;
         }
+        const uint64_t pav = avoid | (pi == 0 ? avoid_first : 0ull);  // (padding of this pass)
         int r0 = ch.r0, hp = heff;
         uint64_t hi = ch.hi;
         // Mixed heights: a pass of a 13-qubit plan whose gates fit a 12-qubit tile runs as one
@@ -897,7 +903,7 @@ Plan plan_fused(const std::vector<Op>& ops, int n, int hmax, uint64_t avoid) {
         const int nfree = 6 + hp - r0;
         // Pad the tile to nfree chosen qubits (uniform tile size / occupancy).
         for (int q = r0; q < n && __builtin_popcountll(hi) < nfree; ++q)
-            if (!((avoid >> q) & 1ull)) hi |= 1ull << q;
+            if (!((pav >> q) & 1ull)) hi |= 1ull << q;
         // too few qubits outside `avoid` (small states): fill up anyway — such a tile contains
         // the avoided qubit, which the caller detects (the sharded engine then runs the step on
         // the whole shard)

@@ -215,6 +215,9 @@ _sig(hip, "qsim_dist_plan", [c_int, c_int, c_int, POINTER(qsim_gate), c_size_t, 
                              POINTER(qsim_op), c_size_t, POINTER(c_size_t)])
 _sig(hip, "qsim_dist_plan_passes", [c_int, c_int, c_int, POINTER(qsim_gate), c_size_t,
                                     POINTER(c_int32), POINTER(c_int32), c_size_t, POINTER(c_size_t)])
+_sig(hip, "qsim_dist_plan_passes_carry", [c_int, c_int, c_int, POINTER(qsim_gate), c_size_t,
+                                          POINTER(c_int32), POINTER(c_uint64), POINTER(c_int32), c_size_t,
+                                          POINTER(c_size_t)])
 
 # ---- C++ API library (libqsim.so): circuit factories
 _sig(api, "qsim_circuit_make", [c_int, c_int, c_int, c_uint, POINTER(qsim_gate), c_size_t,

@@ -451,6 +451,13 @@ int qsim_dist_plan(int n_qubits, int world, int rank, const qsim_gate* gates, si
  * `cap` counts steps.  perm_inout updated as by qsim_dist_plan. */
 int qsim_dist_plan_passes(int n_qubits, int world, int rank, const qsim_gate* gates, size_t count,
                           int32_t* perm_inout, int32_t* passes, size_t cap, size_t* n_steps);
+/* As qsim_dist_plan_passes, with the cross-run overlap of qsim_dist_run: *carry_inout (in) the
+ * pivots of the previous run's last remap still in flight when this run starts (0: none; the first
+ * step's leading passes that avoid them run per part), (out) the pivots this run carries into the
+ * next (its last step runs wholly per part and is merged into the next run's first step). */
+int qsim_dist_plan_passes_carry(int n, int world, int rank, const qsim_gate* gates, size_t count,
+                                int32_t* perm_inout, uint64_t* carry_inout, int32_t* passes, size_t cap,
+                                size_t* n_steps);
 
 /* Host-only: forget the process-wide memo of remap pivots (planning is then redone from scratch,
  * as in a fresh rank process). */

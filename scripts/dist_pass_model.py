@@ -1,60 +1,79 @@
-"""Host-only model of the sharded engine's local work: fused passes per step for W-HC at n
-qubits on `world` ranks, over consecutive runs (each run starts from the map the last one ended
-with, as a benchmark loop does).  No GPU: the planner is host code (qsim_dist_plan_passes)."""
-import ctypes, os, sys
-sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "cuda-quantum-simulator_amd"))
-import qsim_amd as q
-from qsim_amd import _lib
+"""Host-only model of the sharded engine's local work and run time: fused passes per step for
+W-HC at n qubits on `world` ranks over consecutive runs (each run starts from the map the last
+one ended with, and from the remap it left in flight, as a benchmark loop does).  No GPU: the
+planner is host code (qsim_dist_plan_passes_carry, qsim_dist_plan).
 
-n = int(os.environ.get("QUBITS", 30)); world = int(os.environ.get("WORLD", 8))
-runs = int(os.environ.get("RUNS", 4)); seed = int(os.environ.get("SEED", 42))
+Time model per run: one remap X per run between ops steps A and B, K = 2^pivots
+parts; the cycle from X_{i-1}'s first part leaving to X_i's first part leaving is
+    T_i = max(T_x + (h_{i-1} + hA_i) * P / K_{i-1} + (nA_i - hA_i - t_i) * P + t_i * P / K_i
+                   + (nB_{i-1} - h_{i-1}) * P,
+              (nA_i + nB_{i-1}) * P + T_x / K_i)
+t: A's trailing passes that avoid X's pivots (run per part, feeding the transfer), h: B's leading
+passes that avoid them (run per part as each part lands), hA: A's leading passes that avoid the
+pivots of the PREVIOUS run's remap (run per part, interleaved with that run's carried B, after its
+last part landed); P: one local pass over the shard (32 B x 2^L at 6.4 TB/s).  The remap's pack /
+unpack run inside the passes (fused remap), so they add no HBM time.  Without a carry (hA = 0) and
+with h = nB this is the round-3 formula max(T_x + (nA - t) P + (t + h) P / K, (nA + nB) P + T_x / K).
+"""
+import ctypes
+import os
+import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "cuda-quantum-simulator_amd"))
+import qsim_amd as q  # noqa: E402
+from qsim_amd import _lib  # noqa: E402
+
+n = int(os.environ.get("QUBITS", 30))
+world = int(os.environ.get("WORLD", 8))
+runs = int(os.environ.get("RUNS", 6))
+seed = int(os.environ.get("SEED", 42))
+carry_on = os.environ.get("QSIM_DIST_CARRY", "0") != "0"  # (the engine's default: off)
+L = n - (world.bit_length() - 1)
+P = float(os.environ.get("PASS_MS", 32 * 2 ** L / 6.4e12 * 1e3))
 c = q.createRandomHCCircuit(n, 100, seed)
 arr, cnt = c.to_abi()
 perm = (ctypes.c_int32 * n)(*range(n))
-tot = 0
-rows = []
+carry = ctypes.c_uint64(0)
+tot, Ts = 0, []
+prev = None  # (K, nB, h) of the previous run's remap
 for r in range(runs):
+    perm_in = list(perm)
+    carry_in = carry.value if carry_on else 0
+    carry.value = carry_in
     passes = (ctypes.c_int32 * (3 * 64))()
     ns = ctypes.c_size_t(0)
-    _lib.check(_lib.hip.qsim_dist_plan_passes(n, world, 0, arr, cnt, perm, passes, 64, ctypes.byref(ns)))
+    _lib.check(_lib.hip.qsim_dist_plan_passes_carry(n, world, 0, arr, cnt, perm, ctypes.byref(carry), passes, 64,
+                                                    ctypes.byref(ns)))
     steps = [tuple(passes[3 * i:3 * i + 3]) for i in range(ns.value)]
     p = sum(x[0] for x in steps if x[0] > 0)
     tot += p
-    rows.append(steps)
-    print(f"run {r}: steps (passes, head, tail) {steps} passes {p}")
-print("mean passes per run", tot / runs)
-
-# exchange sizes: k globals swapped per remap -> fraction (1 - 2^-k) of the shard leaves each rank
-perm = (ctypes.c_int32 * n)(*range(n))
-vol = 0.0
-for r in range(runs):
-    steps = (_lib.qsim_dist_step * 64)()
-    ns, no = ctypes.c_size_t(0), ctypes.c_size_t(0)
-    _lib.check(_lib.hip.qsim_dist_plan(n, world, 0, arr, cnt, perm, steps, 64, ctypes.byref(ns), None, 0,
+    # the exchange skeleton (pivots) of the same run
+    pp = (ctypes.c_int32 * n)(*perm_in)
+    st = (_lib.qsim_dist_step * 64)()
+    ns2, no = ctypes.c_size_t(0), ctypes.c_size_t(0)
+    _lib.check(_lib.hip.qsim_dist_plan(n, world, 0, arr, cnt, pp, st, 64, ctypes.byref(ns2), None, 0,
                                        ctypes.byref(no)))
-    ks = [steps[i].k for i in range(ns.value) if steps[i].kind == 1]
-    vol += sum(1 - 2.0 ** -k for k in ks)
-    print(f"run {r}: remap k {ks} pivots {[steps[i].pivot for i in range(ns.value) if steps[i].kind == 1]}")
-print("mean shard fraction sent per run", vol / runs)
-
-# The time model of DESIGN §5 per run (one remap between ops steps A and B):
-#   T = max(T_x + (nA - t + nB - h) * P + (t + h) * P / K,  (nA + nB) * P + T_x / K)
-# P: one local pass over the 2 GiB shard (32 B x 2^27 at 6.4 TB/s), K = 2^(pivots).
-P = float(os.environ.get("PASS_MS", 32 * 2 ** (n - 3) / 6.4e12 * 1e3))
-perm = (ctypes.c_int32 * n)(*range(n))
-for r in range(runs):
-    steps = (_lib.qsim_dist_step * 64)()
-    ns, no = ctypes.c_size_t(0), ctypes.c_size_t(0)
-    _lib.check(_lib.hip.qsim_dist_plan(n, world, 0, arr, cnt, perm, steps, 64, ctypes.byref(ns), None, 0,
-                                       ctypes.byref(no)))
-    ps = rows[r]
-    for i in range(ns.value):
-        if steps[i].kind != 1 or i == 0 or i + 1 >= ns.value:
-            continue
-        K = 2 ** bin(steps[i].pmask).count("1")
-        nA, _, t = ps[i - 1]
-        nB, h, _ = ps[i + 1]
+    ks = [st[i].k for i in range(ns2.value) if st[i].kind == 1]
+    line = f"run {r}: steps (passes, head, tail) {steps} passes {p} carry_in {carry_in:#x} remap k {ks}"
+    xs = [i for i in range(1, len(steps) - 1) if steps[i][0] == -1]
+    if len(xs) == 1:
+        i = xs[0]
+        K = 2 ** bin(st[i].pmask).count("1")
+        nA, hA, t = steps[i - 1]
+        nB, h, _ = steps[i + 1]
+        if not carry_in:
+            hA = 0  # (no earlier remap in flight before A)
+        Kp, nBp, hp = prev if prev else (K, nB, h)
         for tx in (4.4, 3.5):
-            T = max(tx + (nA - t + nB - h) * P + (t + h) * P / K, (nA + nB) * P + tx / K)
-            print(f"run {r}: nA {nA} t {t} nB {nB} h {h} K {K}: T_x {tx} ms -> {T:.2f} ms per run "
-                  f"(pass {P:.3f} ms; pack/unpack not counted)")
+            T = max(tx + (hp + hA) * P / Kp + (nA - hA - t) * P + t * P / K + (nBp - hp) * P,
+                    (nA + nBp) * P + tx / K)
+            if tx == 4.4:
+                Ts.append(T)
+            line += (f"\n    nA {nA} hA {hA} t {t} | nB {nB} h {h} | K {K} (previous K {Kp}): T_x {tx} ms "
+                     f"-> {T:.2f} ms per run")
+        prev = (K, nB, h)
+    print(line)
+print(f"mean passes per run {tot / runs:.2f}; pass {P:.3f} ms")
+if Ts:
+    steady = Ts[len(Ts) // 2:]
+    print(f"steady-state model at T_x = 4.4 ms: {sum(steady) / len(steady):.2f} ms per run")
