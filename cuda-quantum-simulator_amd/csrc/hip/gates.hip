@@ -161,35 +161,67 @@ __device__ __forceinline__ uint64_t item_base(const GArgs& a, uint64_t item, int
 }
 
 // Slice mode: target >= 6, each wave-item is 64 pairs (two 1 KiB runs).
-template <int U, bool NT>
-__global__ __launch_bounds__(256) void k_m1_slice(GArgs a) {
+// MODE (far-partner targets, QSIM_SLICE_FAR_MODE): 0 the block's 4 waves interleave items and
+// each lane alternates the two runs' loads; 1 the loads grouped by run (all |0> runs, then all
+// |1> runs); 2 grouped, and each wave takes U consecutive items (U KiB contiguous per run).
+template <int U, bool NT, int MODE>
+__device__ __forceinline__ void m1_slice_body(const GArgs& a) {
     const int lane = threadIdx.x & 63;
-    const uint64_t first = (uint64_t)blockIdx.x * (4 * U) + (threadIdx.x >> 6);
+    const uint64_t first = MODE == 2 ? (uint64_t)blockIdx.x * (4 * U) + (uint64_t)(threadIdx.x >> 6) * U
+                                     : (uint64_t)blockIdx.x * (4 * U) + (threadIdx.x >> 6);
+    const uint64_t step = MODE == 2 ? 1 : 4;
     const uint64_t tb = 1ull << a.t0;
     double2 v0[U], v1[U];
     uint64_t i0[U];
     // lanes failing a low control never load: with controls on bits >= 3 whole 128-B lines are
     // skipped (CNOT with a low control moves N/2 amplitudes, not N)
     const bool lane_ok = (lane & a.lane_ctrl) == a.lane_ctrl;
+    if constexpr (MODE == 0) {
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-        const uint64_t item = first + 4 * u;
-        if (item < a.items && lane_ok) {
-            i0[u] = item_base(a, item, lane);
-            v0[u] = ld<NT>(a.st + i0[u]);
-            v1[u] = ld<NT>(a.st + (i0[u] | tb));
+        for (int u = 0; u < U; ++u) {
+            const uint64_t item = first + step * u;
+            if (item < a.items && lane_ok) {
+                i0[u] = item_base(a, item, lane);
+                v0[u] = ld<NT>(a.st + i0[u]);
+                v1[u] = ld<NT>(a.st + (i0[u] | tb));
+            }
+        }
+    } else {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t item = first + step * u;
+            if (item < a.items && lane_ok) {
+                i0[u] = item_base(a, item, lane);
+                v0[u] = ld<NT>(a.st + i0[u]);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t item = first + step * u;
+            if (item < a.items && lane_ok) v1[u] = ld<NT>(a.st + (i0[u] | tb));
         }
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-        const uint64_t item = first + 4 * u;
+        const uint64_t item = first + step * u;
         if (item < a.items && lane_ok) {
             m1_pair(a.sub, a.m0, a.m1, a.m2, a.m3, v0[u], v1[u]);
             st<NT>(a.st + i0[u], v0[u]);
-            st<NT>(a.st + (i0[u] | tb), v1[u]);
         }
     }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const uint64_t item = first + step * u;
+        if (item < a.items && lane_ok) st<NT>(a.st + (i0[u] | tb), v1[u]);
+    }
 }
+
+template <int U, bool NT>
+__global__ __launch_bounds__(256) void k_m1_slice(GArgs a) { m1_slice_body<U, NT, 0>(a); }
+template <int U, bool NT>
+__global__ __launch_bounds__(256) void k_m1_slice_g(GArgs a) { m1_slice_body<U, NT, 1>(a); }
+template <int U, bool NT>
+__global__ __launch_bounds__(256) void k_m1_slice_c(GArgs a) { m1_slice_body<U, NT, 2>(a); }
 
 // Lane mode: target < 6, each wave-item is 64 consecutive amplitudes; partner via shuffle.
 template <int U, bool NT>
@@ -423,7 +455,7 @@ static void add_fix(GArgs& a, int pos) {
 // 28 qubits vs 0.74-0.84 for the others); they get QSIM_SLICE_U_FAR items.
 struct Tune {
     int slice_u = 1, lane_u = 2, diag_u = 2;
-    int slice_u_far = 4, far_lo = 20, far_hi = 25;
+    int slice_u_far = 4, far_lo = 20, far_hi = 25, far_mode = 0;
     bool nt = true;
     Tune() {
         auto env = [](const char* k, int d) {
@@ -434,6 +466,7 @@ struct Tune {
         slice_u_far = env("QSIM_SLICE_U_FAR", slice_u_far);
         far_lo = env("QSIM_SLICE_FAR_LO", far_lo);
         far_hi = env("QSIM_SLICE_FAR_HI", far_hi);
+        far_mode = env("QSIM_SLICE_FAR_MODE", far_mode);
         lane_u = env("QSIM_LANE_U", lane_u);
         diag_u = env("QSIM_DIAG_U", diag_u);
         nt = env("QSIM_NT", nt ? 1 : 0) != 0;
@@ -521,7 +554,13 @@ void launch_op(double2* st, int n, uint64_t batch, const Op& op, hipStream_t s, 
                 finish();
                 TimedLaunch tl(tm, "m1_slice", bytes, s, true);
                 const bool far = op.t0 >= T.far_lo && op.t0 <= T.far_hi;
-                QSIM_GO_U(k_m1_slice, far ? T.slice_u_far : T.slice_u, QSIM_U248);
+                if (far && T.far_mode == 1) {
+                    QSIM_GO_U(k_m1_slice_g, T.slice_u_far, QSIM_U248);
+                } else if (far && T.far_mode == 2) {
+                    QSIM_GO_U(k_m1_slice_c, T.slice_u_far, QSIM_U248);
+                } else {
+                    QSIM_GO_U(k_m1_slice, far ? T.slice_u_far : T.slice_u, QSIM_U248);
+                }
             } else {
                 finish();
                 TimedLaunch tl(tm, "m1_lane", bytes, s, true);

@@ -70,8 +70,9 @@ def _pin_against_per_gate(qsim, n, seed, expect_relayout=None, expect_passes=Non
 
 
 def test_w_hc_30q_headline_path_equals_per_gate(qsim, gpu_ready, jit2):
-    """The bench's line: W-HC 30q seed 42, calibrated, relayout plan of 4 passes."""
-    info, passes = _pin_against_per_gate(qsim, 30, 42, expect_relayout=True, expect_passes=4)
+    """The bench's line: W-HC 30q seed 42, calibrated first run (fixed-layout and relayout
+    candidates timed on the device, 4 passes either way with tile-constant controls)."""
+    info, passes = _pin_against_per_gate(qsim, 30, 42, expect_passes=4)
     assert info["calibrated"] and info["tile_qubits"] == 12
 
 
@@ -81,12 +82,15 @@ def test_w_hc_28q_config3_equals_per_gate(qsim, gpu_ready, jit2):
     assert info["calibrated"] and passes <= 5
 
 
-def test_w_hc_30q_seed2_five_pass_relayout_equals_per_gate(qsim, gpu_ready, jit2):
-    """W-HC 30q seed 2 under its relayout plan (5 passes; forced so the timing cannot pick
-    another plan and leave the 5-pass relayout cycle untested)."""
-    from qsim_amd.plan import set_relayout
+@pytest.mark.parametrize("seed,ctrl_out,passes", [(2, 1, 4), (42, 1, 4), (2, 0, 5)])
+def test_w_hc_30q_relayout_plans_equal_per_gate(qsim, gpu_ready, jit2, seed, ctrl_out, passes):
+    """W-HC 30q under its relayout plan (forced, so the timing cannot pick another plan and leave
+    the relayout cycle untested): seeds 2 and 42 with tile-constant controls (4 passes), and seed 2
+    with every control a tile qubit (the 5-pass relayout plan of round 3)."""
+    from qsim_amd.plan import set_relayout, set_tile_ctrl_out
     set_relayout(2, -1)
-    _pin_against_per_gate(qsim, 30, 2, expect_relayout=True, expect_passes=5)
+    set_tile_ctrl_out(ctrl_out)
+    _pin_against_per_gate(qsim, 30, seed, expect_relayout=True, expect_passes=passes)
 
 
 def test_w_hc_30q_headline_path_round_trip(qsim, gpu_ready, jit2):
