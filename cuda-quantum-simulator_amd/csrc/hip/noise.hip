@@ -515,23 +515,43 @@ struct PullArgs {
 };
 
 // (P psi)[k]: untouched amplitudes are themselves; otherwise walk the channels last to first.
+// The code words of channels [0, hi] are fetched for the current index at once (independent
+// loads: one memory latency, not one per channel); only a flip that moves the index (X / Y)
+// starts another such round for the channels below it.
 __device__ __forceinline__ double2 pulled(const PullArgs& a, uint64_t k) {
     if (!((a.touched[k >> 5] >> (k & 31ull)) & 1u)) return a.src[k];
     int e = 0;  // phase i^e
-    for (int c = a.nch - 1; c >= 0; --c) {
-        const int q = a.q[c];
-        const uint64_t l = ((k >> (q + 1)) << q) | (k & ((1ull << q) - 1ull));
-        const uint32_t code = (a.codes[(uint64_t)c * a.cstride + (l >> 4)] >> (2u * (uint32_t)(l & 15ull))) & 3u;
-        if (!code) continue;
-        const int bit = (int)((k >> q) & 1ull);
-        if (code == 1) {  // X: v[k ^ 2^q]
-            k ^= 1ull << q;
-        } else if (code == 2) {  // Y: |0> <- -i v[k1], |1> <- +i v[k0]
-            e += bit ? 1 : 3;
-            k ^= 1ull << q;
-        } else if (bit) {  // Z: |1> <- -v[k1]
-            e += 2;
+    int hi = a.nch - 1;
+    while (hi >= 0) {
+        uint32_t cw[kMaxPullChannels];
+#pragma unroll
+        for (int c = 0; c < kMaxPullChannels; ++c) {
+            if (c <= hi) {
+                const int q = a.q[c];
+                const uint64_t l = ((k >> (q + 1)) << q) | (k & ((1ull << q) - 1ull));
+                cw[c] = a.codes[(uint64_t)c * a.cstride + (l >> 4)] >> (2u * (uint32_t)(l & 15ull));
+            }
         }
+        int next = -1;
+#pragma unroll
+        for (int c = kMaxPullChannels - 1; c >= 0; --c) {
+            if (c > hi || next >= 0) continue;
+            const uint32_t code = cw[c] & 3u;
+            if (!code) continue;
+            const int q = a.q[c];
+            const int bit = (int)((k >> q) & 1ull);
+            if (code == 1) {  // X: v[k ^ 2^q]
+                k ^= 1ull << q;
+                next = c - 1;
+            } else if (code == 2) {  // Y: |0> <- -i v[k1], |1> <- +i v[k0]
+                e += bit ? 1 : 3;
+                k ^= 1ull << q;
+                next = c - 1;
+            } else if (bit) {  // Z: |1> <- -v[k1] (the index stays)
+                e += 2;
+            }
+        }
+        hi = next;  // (-1: done; else the channels below a move, fetched for the new index)
     }
     const double2 v = a.src[k];
     switch (e & 3) {
