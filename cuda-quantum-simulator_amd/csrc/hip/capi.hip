@@ -510,7 +510,8 @@ static void choose_first_layout(qsim_state* s, const qsim_gate* gates, size_t co
         // candidates are not timed: memoised apart)
         std::vector<int> memo;
         int mh = -1;
-        if (relayout && layout_memo_get(n, 2, gates, bytes, memo, timing ? &mh : nullptr)) {
+        if (relayout && layout_memo_get(n, 2, gates, bytes, memo, timing ? &mh : nullptr) &&
+            !(memo.empty() && relayout_forced())) {
             if (memo.empty()) return;  // (decided: no relayout plan, and no relabeling below)
             std::vector<RelayoutChoice> vs;
             plan_relayout_variants(n, lower_under, SIZE_MAX, vs);
@@ -530,7 +531,8 @@ static void choose_first_layout(qsim_state* s, const qsim_gate* gates, size_t co
         std::vector<int> memo;
         int mh = -1;
         const TileHeightScope scope(th);
-        if (layout_memo_get(n, 0, gates, bytes, memo, heights ? &mh : nullptr)) {
+        // (a forced relayout plan does not take a fixed-layout decision made before)
+        if (!relayout_forced() && layout_memo_get(n, 0, gates, bytes, memo, heights ? &mh : nullptr)) {
             s->perm = memo;  // decided before for this circuit (its plan: the plan cache)
             if (heights) s->tile_h = mh;
             s->calibrated = heights;  // (a cross-height decision is always a timed one)

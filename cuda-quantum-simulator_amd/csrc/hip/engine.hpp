@@ -332,6 +332,7 @@ const JitModule* jit_for(JitState& js, const Plan& plan, int n);
 struct PlanCache {
     struct Entry {
         int n = -1, h = -1;  // h: the tile height the plan was made for
+        int ctrl_out = -1;   // tile_ctrl_out() when it was planned
         uint64_t avoid = 0, avoid_first = 0;
         std::vector<Op> key;
         Plan plan;

@@ -619,7 +619,7 @@ PlanCache::Entry& PlanCache::get(const std::vector<Op>& ops, int n_qubits, hipSt
                                  uint64_t avoid, uint64_t avoid_first) {
     for (auto& e : entries) {
         bool hit = e->n == n_qubits && e->h == tile_height_default() && e->avoid == avoid &&
-                   e->avoid_first == avoid_first &&
+                   e->avoid_first == avoid_first && e->ctrl_out == (tile_ctrl_out() ? 1 : 0) &&
                    e->key.size() == ops.size();
         for (size_t i = 0; hit && i < ops.size(); ++i) hit = same_op(e->key[i], ops[i]);
         if (hit) {
@@ -640,6 +640,7 @@ PlanCache::Entry& PlanCache::get(const std::vector<Op>& ops, int n_qubits, hipSt
     e->key = ops;
     e->n = n_qubits;
     e->h = tile_height_default();
+    e->ctrl_out = tile_ctrl_out() ? 1 : 0;
     e->avoid = avoid;
     e->used = ++clock;
     entries.push_back(std::move(e));
@@ -658,6 +659,7 @@ void PlanCache::put(std::vector<Op> ops, int n_qubits, Plan plan, hipStream_t st
     e->key = std::move(ops);
     e->n = n_qubits;
     e->h = tile_height_default();
+    e->ctrl_out = tile_ctrl_out() ? 1 : 0;
     e->used = ++clock;
     entries.push_back(std::move(e));
 }

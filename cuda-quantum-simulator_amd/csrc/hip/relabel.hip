@@ -58,7 +58,8 @@ void relabel_configure(int mode, int min_qubits) {
 
 // Process-wide memo of layout choices: the same circuit on a reset state (trajectory loops,
 // one state per shot batch, benchmark repetitions) re-uses the decision instead of planning the
-// candidates again.  Keyed by (n, kind, tile height, the exact gate bytes); LRU of kMemo entries.
+// candidates again.  Keyed by (n, kind, tile height, tile-constant controls on / off, the exact
+// gate bytes); LRU of kMemo entries.
 namespace {
 struct MemoEntry {
     int n, kind;
@@ -76,7 +77,7 @@ constexpr size_t kMemo = 16;
 bool layout_memo_get(int n, int kind, const void* gates, size_t bytes, std::vector<int>& perm, int* h) {
     std::lock_guard<std::mutex> l(g_memo_mu);
     // a choice made for one tile height only, unless the height was chosen with it (h != null)
-    kind = kind * 16 + (h ? 15 : tile_height_default());
+    kind = (kind * 16 + (h ? 15 : tile_height_default())) * 2 + (tile_ctrl_out() ? 1 : 0);
     for (MemoEntry& e : g_memo)
         if (e.n == n && e.kind == kind && e.key.size() == bytes && std::memcmp(e.key.data(), gates, bytes) == 0) {
             e.used = ++g_memo_clock;
@@ -91,7 +92,7 @@ void layout_memo_put(int n, int kind, const void* gates, size_t bytes, const std
     if (g_memo.size() >= kMemo)
         g_memo.erase(std::min_element(g_memo.begin(), g_memo.end(),
                                       [](const MemoEntry& a, const MemoEntry& b) { return a.used < b.used; }));
-    kind = kind * 16 + (h >= 0 ? 15 : tile_height_default());
+    kind = (kind * 16 + (h >= 0 ? 15 : tile_height_default())) * 2 + (tile_ctrl_out() ? 1 : 0);
     const unsigned char* p = static_cast<const unsigned char*>(gates);
     g_memo.push_back(MemoEntry{n, kind, std::vector<unsigned char>(p, p + bytes), perm, h, ++g_memo_clock});
 }
