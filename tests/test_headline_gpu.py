@@ -122,6 +122,7 @@ def test_relayout_on_a_pinned_state_copies_back(qsim, oracle, gpu_ready):
     c = qsim.createRandomHCCircuit(n, 100, 42)
     sv = qsim.StateVector(n)
     ptr = sv.devicePtr()
+    sv.initializeZero()  # (a basis state again, pointer still out: its first run chooses relayout)
     sv.run(c, qsim.RunMode.Fused)
     assert sv.layoutInfo()["relayout"]
     ref = oracle.run_cpu(n, oracle.gates_of(c))
@@ -136,11 +137,17 @@ def test_relayout_on_a_pinned_state_copies_back(qsim, oracle, gpu_ready):
     h.h(17)
     ref2 = oracle.run_cpu(n, oracle.gates_of(h), state=ref)
     assert float(np.max(np.abs(sv.toHost() - ref2))) < 1e-12
-    # a second run under the memoised relayout plan, still pinned
+    # a run from that (non-basis) state: identity labels, in place
     sv.run(c, qsim.RunMode.Fused)
     ref3 = oracle.run_cpu(n, oracle.gates_of(c), state=ref2)
     assert sv.devicePtr() == ptr
     assert float(np.max(np.abs(sv.toHost() - ref3))) < 1e-12
+    # back to |0..0>: the memoised relayout plan, still pinned
+    sv.initializeZero()
+    sv.run(c, qsim.RunMode.Fused)
+    assert sv.layoutInfo()["relayout"]
+    assert sv.devicePtr() == ptr
+    assert float(np.max(np.abs(sv.toHost() - ref))) < 1e-12
 
 
 def _hip():
