@@ -59,7 +59,7 @@ struct DStep {
     std::vector<int> op_gate;
 };
 
-constexpr int kMaxPivots = 3;
+constexpr int kMaxPivots = 4;
 static bool pass_avoids(const FusedPass& p, uint64_t pmask) {
     if (p.single >= 0 || p.h < 4) return false;
     for (int i = 0; i < 6 + p.h - p.r0; ++i)

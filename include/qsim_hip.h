@@ -377,7 +377,7 @@ typedef struct qsim_op {
 } qsim_op;
 /* One plan step: kind 0 = ops[op_begin, op_end) on the local shard; kind 1 = exchange that
  * swaps global physical positions gpos[i] with local positions lpos[i], i < k.  Overlapped
- * remaps: an exchange with pivots (pmask != 0: up to 3 local physical positions; pivot = the
+ * remaps: an exchange with pivots (pmask != 0: up to 4 local physical positions; pivot = the
  * lowest, -1 if none) runs as 2^m part-exchanges, one per value of the pivot bits.  An ops step
  * with role bit 1 runs the trailing passes of its fused plan that avoid the pivots of the
  * exchange after it per part (each part's transfer then overlaps the later parts' passes); role
