@@ -60,6 +60,7 @@ struct DStep {
 };
 
 constexpr int kMaxPivots = 4;
+constexpr int kMaxParts = 1 << kMaxPivots;  // part-exchanges of one overlapped remap
 static bool pass_avoids(const FusedPass& p, uint64_t pmask) {
     if (p.single >= 0 || p.h < 4) return false;
     for (int i = 0; i < 6 + p.h - p.r0; ++i)
@@ -627,8 +628,9 @@ struct qsim_dist {
     hipStream_t comm_stream = nullptr;  // remap transfers (RCCL or, virtual, device copies)
     hipStream_t copy_stream = nullptr;  // pack / unpack of overlapped (half) remaps
     std::vector<hipEvent_t> events;     // remap pipeline: packed part p, transferred part p
-    // overlapped remap, per part h < 8: tail done (pev[h]), packed (8 + h), sent (16 + h), unpacked (24 + h)
-    hipEvent_t pev[32] = {};
+    // overlapped remap, per part h < kMaxParts: tail done (pev[h]), packed (kMaxParts + h), sent
+    // (2 kMaxParts + h), unpacked (3 kMaxParts + h)
+    hipEvent_t pev[4 * kMaxParts] = {};
     int overlapped = 0;                 // remaps of the last run that overlapped local work
     ncclComm_t comm = nullptr;
     bool aborted = false;  // the communicator was aborted after an RCCL / HIP error or a timeout
@@ -1069,7 +1071,7 @@ void exchange(qsim_dist* d, const DStep& ex, const std::vector<char>& fused) {
 // One overlapped remap: the K = 2^m parts of every shard (the values of the m pivot bits) are
 // exchanged one after the other — pack and unpack on copy_stream, transfers on comm_stream —
 // each part waiting for its local work (event pev[j], recorded on the compute stream after the
-// role-1 step's part) and signalling pev[24 + j] when unpacked (the role-2 step's part waits for
+// role-1 step's part) and signalling pev[3 kMaxParts + j] when unpacked (the role-2 step's part waits for
 // it).  Part j uses part j of the send / receive buffers, so all parts can be in flight.
 void exchange_parts(qsim_dist* d, const DStep& ex, const std::vector<char>& fused) {
     const int K = 1 << __builtin_popcountll(ex.pmask);
@@ -1090,21 +1092,21 @@ void exchange_parts(qsim_dist* d, const DStep& ex, const std::vector<char>& fuse
             a.buf = d->shards[i].sendbuf + (uint64_t)h * part_amps;
             copy_kernel(true, a, 0, xs[i].a.chunk_log, d->copy_stream);
         }
-        QSIM_HIPCHK(hipEventRecord(d->pev[8 + h], d->copy_stream));
-        QSIM_HIPCHK(hipStreamWaitEvent(d->comm_stream, d->pev[8 + h], 0));
+        QSIM_HIPCHK(hipEventRecord(d->pev[kMaxParts + h], d->copy_stream));
+        QSIM_HIPCHK(hipStreamWaitEvent(d->comm_stream, d->pev[kMaxParts + h], 0));
         std::vector<Post> posts;
         for (size_t i = 0; i < d->shards.size(); ++i)
             slab_posts(posts, d->shards[i], xs[i], ex.k, (uint64_t)h * part_amps, chunk, chunk);
         post_transfers(d, posts, "overlapped remap send/recv");
-        QSIM_HIPCHK(hipEventRecord(d->pev[16 + h], d->comm_stream));
-        QSIM_HIPCHK(hipStreamWaitEvent(d->copy_stream, d->pev[16 + h], 0));
+        QSIM_HIPCHK(hipEventRecord(d->pev[2 * kMaxParts + h], d->comm_stream));
+        QSIM_HIPCHK(hipStreamWaitEvent(d->copy_stream, d->pev[2 * kMaxParts + h], 0));
         for (size_t i = 0; i < d->shards.size(); ++i) {
             if (fused[i]) continue;  // (the step after loads part h from the receive buffer)
             XArgs a = xs[i].a;
             a.buf = d->shards[i].recvbuf + (uint64_t)h * part_amps;
             copy_kernel(false, a, 0, xs[i].a.chunk_log, d->copy_stream);
         }
-        QSIM_HIPCHK(hipEventRecord(d->pev[24 + h], d->copy_stream));
+        QSIM_HIPCHK(hipEventRecord(d->pev[3 * kMaxParts + h], d->copy_stream));
     }
 }
 
@@ -1311,7 +1313,7 @@ void flush_carry(qsim_dist* d) {
     qsim_dist::Carry& c = d->carry;
     if (!c.active) return;
     for (int h = 0; h < c.parts; ++h) {
-        QSIM_HIPCHK(hipStreamWaitEvent(d->stream, d->pev[24 + h], 0));
+        QSIM_HIPCHK(hipStreamWaitEvent(d->stream, d->pev[3 * kMaxParts + h], 0));
         for (size_t i = 0; i < d->shards.size(); ++i)
             if (c.runs[i].plan)
                 run_part(d, d->shards[i], c.rp->steps[i][c.step].ops, c.runs[i], 0, c.runs[i].j1, c.pbs[i], h,
@@ -1565,7 +1567,7 @@ int qsim_dist_run(qsim_dist* d, const qsim_gate* gates, size_t count, int flags)
         int pending = merge ? d->carry.parts : 0;  // parts of an overlapped remap still to be waited for
         if (merge) ++d->carried;
         auto wait_pending = [&]() {
-            for (int h = 0; h < pending; ++h) QSIM_HIPCHK(hipStreamWaitEvent(d->stream, d->pev[24 + h], 0));
+            for (int h = 0; h < pending; ++h) QSIM_HIPCHK(hipStreamWaitEvent(d->stream, d->pev[3 * kMaxParts + h], 0));
             pending = 0;
         };
         // Every rank's plan has the same step skeleton (mark_overlap decides from
@@ -1644,7 +1646,7 @@ int qsim_dist_run(qsim_dist* d, const qsim_gate* gates, size_t count, int flags)
             if (head) {
                 const bool carried = k == 0 && merge;
                 for (int h = 0; h < pending; ++h) {
-                    QSIM_HIPCHK(hipStreamWaitEvent(d->stream, d->pev[24 + h], 0));
+                    QSIM_HIPCHK(hipStreamWaitEvent(d->stream, d->pev[3 * kMaxParts + h], 0));
                     if (carried) {  // part h of the previous run's last step, then part h of this one
                         const qsim_dist::Carry& c = d->carry;
                         for (size_t i = 0; i < S; ++i)
