@@ -160,7 +160,10 @@ def _hip():
 
 def test_relayout_buffer_that_does_not_fit_falls_back(qsim, gpu_ready, jit2):
     """Fill device memory until a second 26-qubit buffer (1 GiB) cannot fit: the first run must
-    keep the in-place fixed-layout plan (no relayout, no extra buffer) and equal per-gate."""
+    keep the in-place fixed-layout plan (no relayout, no extra buffer) and equal per-gate.
+    Relayout is forced (the calibrated choice at 26 qubits may be a fixed layout either way)."""
+    from qsim_amd.plan import set_relayout
+    set_relayout(2, -1)
     n = 26
     c = qsim.createRandomHCCircuit(n, 100, 42)
     free_run = qsim.Simulator(n)
