@@ -267,12 +267,20 @@ struct qsim_batch {
     // pinned: a raw pointer to d0 was handed out, so a run that ends in d1 copies back.
     double2* d0 = nullptr;
     double2* d1 = nullptr;
-    uint32_t* d_codes = nullptr;  // per-step flip codes, 2 bits per pair per channel
-    size_t codes_cap = 0;
-    uint32_t* d_touched = nullptr;  // per-step touched bits, one per amplitude
+    // Two sets (noise steps alternate), so the next step's map is built on map_stream while
+    // this step's pass runs: per-step flip codes (2 bits per pair per channel), touched bits.
+    uint32_t* d_codes = nullptr;
+    size_t codes_cap = 0;           // bytes of ONE set
+    uint32_t* d_touched = nullptr;
+    hipStream_t map_stream = nullptr;
+    hipEvent_t ev_map[2] = {}, ev_pull[2] = {}, ev_start = nullptr;
     bool pinned = false;
     ~qsim_batch() {
         if (stream) (void)hipStreamSynchronize(stream);
+        if (map_stream) (void)hipStreamSynchronize(map_stream);
+        for (hipEvent_t e : {ev_map[0], ev_map[1], ev_pull[0], ev_pull[1], ev_start})
+            if (e) (void)hipEventDestroy(e);
+        if (map_stream) (void)hipStreamDestroy(map_stream);
         if (d0) (void)hipFree(d0);
         if (d1) (void)hipFree(d1);
         if (d_codes) (void)hipFree(d_codes);
@@ -324,7 +332,8 @@ bool ensure_pull_buffers(qsim_batch* b, size_t nch) {
     const size_t state_b = amps * sizeof(double2);
     const size_t codes_b = pull_noise_codes_bytes(b->n, (uint64_t)b->batch, nch);
     const size_t touched_b = amps / 8;
-    size_t need_b = (b->d1 ? 0 : state_b) + (codes_b > b->codes_cap ? codes_b : 0) + (b->d_touched ? 0 : touched_b);
+    size_t need_b = (b->d1 ? 0 : state_b) + (codes_b > b->codes_cap ? 2 * codes_b : 0) +
+                    (b->d_touched ? 0 : 2 * touched_b);
     if (need_b == 0) return true;
     size_t free_b = 0, total_b = 0;
     if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) {
@@ -348,10 +357,15 @@ bool ensure_pull_buffers(qsim_batch* b, size_t nch) {
             b->d_codes = nullptr;
             b->codes_cap = 0;
         }
-        if (!grab((void**)&b->d_codes, codes_b)) return false;
+        if (!grab((void**)&b->d_codes, 2 * codes_b)) return false;
         b->codes_cap = codes_b;
     }
-    if (!b->d_touched && !grab((void**)&b->d_touched, touched_b)) return false;
+    if (!b->d_touched && !grab((void**)&b->d_touched, 2 * touched_b)) return false;
+    if (!b->map_stream) {
+        QSIM_HIPCHK(hipStreamCreateWithFlags(&b->map_stream, hipStreamNonBlocking));
+        for (hipEvent_t* e : {&b->ev_map[0], &b->ev_map[1], &b->ev_pull[0], &b->ev_pull[1], &b->ev_start})
+            QSIM_HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
+    }
     return true;
 }
 // Apply the carried Pauli frames to the stored vectors (one pass), frames back to 1.
@@ -547,27 +561,46 @@ int qsim_batch_run(qsim_batch* b, const qsim_gate* gates, size_t count,
             if (pull_noise_supported(b->n, dep) && ensure_pull_buffers(b, dep.size())) {
                 // Pulled: the noise after gate i is applied by gate i+1's pass (out of place),
                 // the noise after the last gate by one identity pass; same draws, same states.
-                bool pending = false;
-                uint64_t c_pending = 0;
-                for (const Op& op : ops) {
-                    if (!pending) {
-                        if (op.kind >= 0) launch_op(b->d, b->n, (uint64_t)b->batch, op, b->stream, &b->timer);
-                    } else {
-                        double2* dst = b->d == b->d0 ? b->d1 : b->d0;
-                        launch_pull_noise_step(b->d, dst, b->n, (uint64_t)b->batch, b->traj0, dep, b->seed, c_pending,
-                                               op.kind >= 0 ? &op : nullptr, b->d_codes, b->d_touched, b->stream,
-                                               &b->timer);
-                        b->d = dst;
-                    }
-                    pending = true;
-                    c_pending = b->ncounter;
-                    b->ncounter += dep.size();  // (one pass counter per channel entry, as the push path)
+                // The map of noise step i (codes set i & 1) is built on map_stream while the pass
+                // of step i - 1 runs; the pass of step i waits for it, the map of step i + 2
+                // waits for that pass (QSIM_NOISE_MAP_OVERLAP=0: one stream, one set in turn).
+                const char* oe = std::getenv("QSIM_NOISE_MAP_OVERLAP");
+                const bool overlap = oe == nullptr || std::atoi(oe) != 0;
+                const size_t G = ops.size();
+                const size_t set_words = b->codes_cap / sizeof(uint32_t);
+                const size_t tw_words = ((uint64_t)b->batch << b->n) / 32;
+                auto codes_of = [&](size_t i) { return b->d_codes + (i & 1) * set_words; };
+                auto touched_of = [&](size_t i) { return b->d_touched + (i & 1) * tw_words; };
+                const uint64_t c0 = b->ncounter;
+                b->ncounter += (uint64_t)G * dep.size();  // (one pass counter per channel entry, as the push path)
+                hipStream_t ms = overlap ? b->map_stream : b->stream;
+                auto map = [&](size_t i) {
+                    if (overlap && i >= 2) QSIM_HIPCHK(hipStreamWaitEvent(ms, b->ev_pull[i & 1], 0));
+                    launch_noise_map(b->n, (uint64_t)b->batch, b->traj0, dep, b->seed, c0 + i * dep.size(), codes_of(i),
+                                     touched_of(i), ms, &b->timer);
+                    if (overlap) QSIM_HIPCHK(hipEventRecord(b->ev_map[i & 1], ms));
+                };
+                if (overlap) {  // (the previous run's passes may still read both sets)
+                    QSIM_HIPCHK(hipEventRecord(b->ev_start, b->stream));
+                    QSIM_HIPCHK(hipStreamWaitEvent(ms, b->ev_start, 0));
+                    for (size_t i = 0; i < std::min<size_t>(G, 2); ++i) map(i);
                 }
-                if (pending) {
+                if (G && ops[0].kind >= 0) launch_op(b->d, b->n, (uint64_t)b->batch, ops[0], b->stream, &b->timer);
+                for (size_t i = 0; i < G; ++i) {
+                    if (overlap) {
+                        QSIM_HIPCHK(hipStreamWaitEvent(b->stream, b->ev_map[i & 1], 0));
+                    } else {
+                        map(i);
+                    }
+                    const Op* op = i + 1 < G && ops[i + 1].kind >= 0 ? &ops[i + 1] : nullptr;
                     double2* dst = b->d == b->d0 ? b->d1 : b->d0;
-                    launch_pull_noise_step(b->d, dst, b->n, (uint64_t)b->batch, b->traj0, dep, b->seed, c_pending,
-                                           nullptr, b->d_codes, b->d_touched, b->stream, &b->timer);
+                    launch_pull_gate(b->d, dst, b->n, (uint64_t)b->batch, dep, op, codes_of(i), touched_of(i),
+                                     b->stream, &b->timer);
                     b->d = dst;
+                    if (overlap && i + 2 < G) {
+                        QSIM_HIPCHK(hipEventRecord(b->ev_pull[i & 1], b->stream));
+                        map(i + 2);
+                    }
                 }
                 if (b->pinned) settle_in_d0(b);
                 return;

@@ -388,6 +388,13 @@ size_t pull_noise_codes_bytes(int n, uint64_t batch, size_t nch);
 void launch_pull_noise_step(const double2* src, double2* dst, int n, uint64_t batch, uint64_t traj0,
                             const std::vector<NoiseChan>& chans, uint64_t seed, uint64_t counter0,
                             const Op* op, uint32_t* codes, uint32_t* touched, hipStream_t s, Timer* tm);
+// Its two halves, for callers that build the next step's map on another stream while this
+// step's pass runs (the map reads no amplitudes): the codes / touched bits of one noise step, and
+// the pass that pulls through them.
+void launch_noise_map(int n, uint64_t batch, uint64_t traj0, const std::vector<NoiseChan>& chans, uint64_t seed,
+                      uint64_t counter0, uint32_t* codes, uint32_t* touched, hipStream_t s, Timer* tm);
+void launch_pull_gate(const double2* src, double2* dst, int n, uint64_t batch, const std::vector<NoiseChan>& chans,
+                      const Op* op, const uint32_t* codes, const uint32_t* touched, hipStream_t s, Timer* tm);
 
 // Density matrices as 2n-index-bit states (density.hip).
 void dm_lower(int n, const qsim_gate* gates, size_t count, const qsim_noise_channel* ch,

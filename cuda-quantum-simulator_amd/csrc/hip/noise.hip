@@ -606,42 +606,55 @@ size_t pull_noise_codes_bytes(int n, uint64_t batch, size_t nch) {
     return std::max<size_t>(1, nch) * ((batch << (n - 1)) / 16) * sizeof(uint32_t);
 }
 
-void launch_pull_noise_step(const double2* src, double2* dst, int n, uint64_t batch, uint64_t traj0,
-                            const std::vector<NoiseChan>& chans, uint64_t seed, uint64_t counter0,
-                            const Op* op, uint32_t* codes, uint32_t* touched, hipStream_t s, Timer* tm) {
-    const uint64_t amps = batch << n, pairs = amps >> 1;
-    const uint64_t idx0 = traj0 << (n - 1);
-    MapArgs m{};
-    m.codes = codes;
-    m.touched = touched;
-    m.amps = amps;
-    m.cstride = pairs / 16;
-    m.blk0 = idx0 >> kFlipBlockLog;
-    PullArgs a{};
+// The live (can-fire) channels of one noise step, keyed like the push kernels' passes.
+static void pull_channels(int n, const std::vector<NoiseChan>& chans, uint64_t seed, uint64_t counter0,
+                          MapArgs& m, PullArgs& a) {
     uint64_t counter = counter0;
     for (const NoiseChan& ch : chans) {
         check_channel(n, ch.type, ch.qubit, ch.p);
         const uint64_t key = noise_key(seed, counter++);
+        if (m.nch >= kMaxPullChannels && flip_probability(ch.p) > 0.0)
+            fail(QSIM_ERR_RUNTIME, "too many channels for the pulled noise path");
         if (!flip_channel(ch.type, ch.qubit, ch.p, key, m.ch[m.nch])) continue;
-        if (m.nch >= kMaxPullChannels) fail(QSIM_ERR_RUNTIME, "too many channels for the pulled noise path");
         a.q[m.nch] = ch.qubit;
         ++m.nch;
     }
     a.nch = m.nch;
-    if (m.nch) {
-        TimedLaunch tl(tm, "noise_map", 0.0, s);
-        const uint64_t regions = amps >> kRegionLog;
-        hipLaunchKernelGGL(k_noise_map, dim3((unsigned)((regions + kMapThreads - 1) / kMapThreads)),
-                           dim3(kMapThreads), 0, s, m);
-        QSIM_HIPCHK(hipGetLastError());
-    } else {  // no channel can fire: every amplitude untouched
+}
+
+void launch_noise_map(int n, uint64_t batch, uint64_t traj0, const std::vector<NoiseChan>& chans, uint64_t seed,
+                      uint64_t counter0, uint32_t* codes, uint32_t* touched, hipStream_t s, Timer* tm) {
+    const uint64_t amps = batch << n, pairs = amps >> 1;
+    MapArgs m{};
+    PullArgs a{};
+    m.codes = codes;
+    m.touched = touched;
+    m.amps = amps;
+    m.cstride = pairs / 16;
+    m.blk0 = (traj0 << (n - 1)) >> kFlipBlockLog;
+    pull_channels(n, chans, seed, counter0, m, a);
+    if (!m.nch) {  // no channel can fire: every amplitude untouched
         QSIM_HIPCHK(hipMemsetAsync(touched, 0, (amps / 32) * sizeof(uint32_t), s));
+        return;
     }
+    TimedLaunch tl(tm, "noise_map", 0.0, s);
+    const uint64_t regions = amps >> kRegionLog;
+    hipLaunchKernelGGL(k_noise_map, dim3((unsigned)((regions + kMapThreads - 1) / kMapThreads)), dim3(kMapThreads),
+                       0, s, m);
+    QSIM_HIPCHK(hipGetLastError());
+}
+
+void launch_pull_gate(const double2* src, double2* dst, int n, uint64_t batch, const std::vector<NoiseChan>& chans,
+                      const Op* op, const uint32_t* codes, const uint32_t* touched, hipStream_t s, Timer* tm) {
+    const uint64_t amps = batch << n, pairs = amps >> 1;
+    MapArgs m{};
+    PullArgs a{};
+    pull_channels(n, chans, 0, 0, m, a);  // (the live channels and their qubits; keys unused)
     a.src = src;
     a.dst = dst;
     a.codes = codes;
     a.touched = touched;
-    a.cstride = m.cstride;
+    a.cstride = pairs / 16;
     a.kind = op ? op->kind : -1;
     if (op) {
         a.sub = op->sub;
@@ -656,6 +669,13 @@ void launch_pull_noise_step(const double2* src, double2* dst, int n, uint64_t ba
     TimedLaunch tl(tm, "pull_gate", 32.0 * (double)amps, s);
     hipLaunchKernelGGL(k_pull_gate, dim3((unsigned)blocks), dim3(256), 0, s, a);
     QSIM_HIPCHK(hipGetLastError());
+}
+
+void launch_pull_noise_step(const double2* src, double2* dst, int n, uint64_t batch, uint64_t traj0,
+                            const std::vector<NoiseChan>& chans, uint64_t seed, uint64_t counter0,
+                            const Op* op, uint32_t* codes, uint32_t* touched, hipStream_t s, Timer* tm) {
+    launch_noise_map(n, batch, traj0, chans, seed, counter0, codes, touched, s, tm);
+    launch_pull_gate(src, dst, n, batch, chans, op, codes, touched, s, tm);
 }
 
 }  // namespace qsim_hip

@@ -146,7 +146,7 @@ def test_reference_noise_one_launch_equals_per_channel_16q(qsim, gpu_ready, monk
         s.setSeed(9)
         s.run(c)
         out.append(np.stack([s.getStateVector(t) for t in (0, 77, 255)]))
-    assert np.array_equal(out[0], out[1])
+    assert np.array_equal(out[0], out[1]) and np.array_equal(out[0], out[2])
     assert abs(np.sum(np.abs(out[0][1]) ** 2) - 1.0) < 1e-10
 
 
@@ -176,22 +176,26 @@ def test_pulled_noise_matches_oracle(qsim, oracle, gpu_ready, n, B, seed, traj0,
 
 
 def test_pulled_noise_equals_push_16q(qsim, gpu_ready, monkeypatch):
-    """BASELINE config-4 shape (16 qubits, depolarizing 0.01 on every qubit, W-HC): pulled and
-    pushed noise give bit-identical trajectories; also through a pinned device pointer."""
+    """BASELINE config-4 shape (16 qubits, depolarizing 0.01 on every qubit, W-HC): pulled noise
+    (its maps overlapped on a second stream or not) and pushed noise give bit-identical
+    trajectories; also through a pinned device pointer."""
     n, B = 16, 128
     c = qsim.createRandomHCCircuit(n, 30, 42)
     nm = qsim.NoiseModel()
     nm.addDepolarizingAll(n, 0.01)
     out = []
-    for pull in ("1", "0"):
+    # pulled with the next step's map built on a second stream (the default), pulled on one
+    # stream, pushed
+    for pull, overlap in (("1", "1"), ("1", "0"), ("0", "1")):
         monkeypatch.setenv("QSIM_NOISE_PULL", pull)
+        monkeypatch.setenv("QSIM_NOISE_MAP_OVERLAP", overlap)
         s = qsim.BatchedSimulator(n, B, nm, noise=qsim.BatchedNoise.Reference)
         s.setSeed(9)
         s.run(c)
         s.run(c)
         out.append(np.stack([s.getStateVector(t) for t in (0, 63, 127)]))
         s.close()
-    assert np.array_equal(out[0], out[1])
+    assert np.array_equal(out[0], out[1]) and np.array_equal(out[0], out[2])
     assert abs(np.sum(np.abs(out[0][1]) ** 2) - 1.0) < 1e-10
     # a raw pointer handed out: the pulled run copies its result back where it points
     monkeypatch.setenv("QSIM_NOISE_PULL", "1")
