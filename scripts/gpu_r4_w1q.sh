@@ -4,6 +4,7 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 O=$PWD/gpurun_out/${1:-w1q}
+export PYTHONPATH=$PWD/cuda-quantum-simulator_amd${PYTHONPATH:+:$PYTHONPATH}
 mkdir -p $O
 for mode in 0 1 2; do
   for u in 2 4 8; do
