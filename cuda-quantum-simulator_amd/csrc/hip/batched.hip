@@ -267,11 +267,10 @@ struct qsim_batch {
     // pinned: a raw pointer to d0 was handed out, so a run that ends in d1 copies back.
     double2* d0 = nullptr;
     double2* d1 = nullptr;
-    // Two sets (noise steps alternate), so the next step's map is built on map_stream while
-    // this step's pass runs: per-step flip codes (2 bits per pair per channel), touched bits.
-    uint32_t* d_codes = nullptr;
+    // Two sets of per-step code words (one per amplitude; noise steps alternate), so the next
+    // step's words are built on map_stream while this step's pass runs.
+    unsigned char* d_codes = nullptr;
     size_t codes_cap = 0;           // bytes of ONE set
-    uint32_t* d_touched = nullptr;
     hipStream_t map_stream = nullptr;
     hipEvent_t ev_map[2] = {}, ev_pull[2] = {}, ev_start = nullptr;
     bool pinned = false;
@@ -284,7 +283,6 @@ struct qsim_batch {
         if (d0) (void)hipFree(d0);
         if (d1) (void)hipFree(d1);
         if (d_codes) (void)hipFree(d_codes);
-        if (d_touched) (void)hipFree(d_touched);
         if (d_xz) (void)hipFree(d_xz);
         if (d_e) (void)hipFree(d_e);
         if (d_ch) (void)hipFree(d_ch);
@@ -331,9 +329,7 @@ bool ensure_pull_buffers(qsim_batch* b, size_t nch) {
     const uint64_t amps = (uint64_t)b->batch << b->n;
     const size_t state_b = amps * sizeof(double2);
     const size_t codes_b = pull_noise_codes_bytes(b->n, (uint64_t)b->batch, nch);
-    const size_t touched_b = amps / 8;
-    size_t need_b = (b->d1 ? 0 : state_b) + (codes_b > b->codes_cap ? 2 * codes_b : 0) +
-                    (b->d_touched ? 0 : 2 * touched_b);
+    size_t need_b = (b->d1 ? 0 : state_b) + (codes_b > b->codes_cap ? 2 * codes_b : 0);
     if (need_b == 0) return true;
     size_t free_b = 0, total_b = 0;
     if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) {
@@ -360,7 +356,6 @@ bool ensure_pull_buffers(qsim_batch* b, size_t nch) {
         if (!grab((void**)&b->d_codes, 2 * codes_b)) return false;
         b->codes_cap = codes_b;
     }
-    if (!b->d_touched && !grab((void**)&b->d_touched, 2 * touched_b)) return false;
     if (!b->map_stream) {
         QSIM_HIPCHK(hipStreamCreateWithFlags(&b->map_stream, hipStreamNonBlocking));
         for (hipEvent_t* e : {&b->ev_map[0], &b->ev_map[1], &b->ev_pull[0], &b->ev_pull[1], &b->ev_start})
@@ -567,17 +562,14 @@ int qsim_batch_run(qsim_batch* b, const qsim_gate* gates, size_t count,
                 const char* oe = std::getenv("QSIM_NOISE_MAP_OVERLAP");
                 const bool overlap = oe == nullptr || std::atoi(oe) != 0;
                 const size_t G = ops.size();
-                const size_t set_words = b->codes_cap / sizeof(uint32_t);
-                const size_t tw_words = ((uint64_t)b->batch << b->n) / 32;
-                auto codes_of = [&](size_t i) { return b->d_codes + (i & 1) * set_words; };
-                auto touched_of = [&](size_t i) { return b->d_touched + (i & 1) * tw_words; };
+                auto codes_of = [&](size_t i) { return (void*)(b->d_codes + (i & 1) * b->codes_cap); };
                 const uint64_t c0 = b->ncounter;
                 b->ncounter += (uint64_t)G * dep.size();  // (one pass counter per channel entry, as the push path)
                 hipStream_t ms = overlap ? b->map_stream : b->stream;
                 auto map = [&](size_t i) {
                     if (overlap && i >= 2) QSIM_HIPCHK(hipStreamWaitEvent(ms, b->ev_pull[i & 1], 0));
-                    launch_noise_map(b->n, (uint64_t)b->batch, b->traj0, dep, b->seed, c0 + i * dep.size(), codes_of(i),
-                                     touched_of(i), ms, &b->timer);
+                    launch_noise_map(b->n, (uint64_t)b->batch, b->traj0, dep, b->seed, c0 + i * dep.size(), codes_of(i), ms,
+                                     &b->timer);
                     if (overlap) QSIM_HIPCHK(hipEventRecord(b->ev_map[i & 1], ms));
                 };
                 if (overlap) {  // (the previous run's passes may still read both sets)
@@ -594,8 +586,8 @@ int qsim_batch_run(qsim_batch* b, const qsim_gate* gates, size_t count,
                     }
                     const Op* op = i + 1 < G && ops[i + 1].kind >= 0 ? &ops[i + 1] : nullptr;
                     double2* dst = b->d == b->d0 ? b->d1 : b->d0;
-                    launch_pull_gate(b->d, dst, b->n, (uint64_t)b->batch, dep, op, codes_of(i), touched_of(i),
-                                     b->stream, &b->timer);
+                    launch_pull_gate(b->d, dst, b->n, (uint64_t)b->batch, dep, op, codes_of(i), b->stream,
+                                     &b->timer);
                     b->d = dst;
                     if (overlap && i + 2 < G) {
                         QSIM_HIPCHK(hipEventRecord(b->ev_pull[i & 1], b->stream));

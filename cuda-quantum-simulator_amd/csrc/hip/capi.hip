@@ -211,13 +211,11 @@ struct qsim_state {
     // pulled noise (NoisySimulator flip channels, noise.hip): per-step flip codes and touched bits
     uint32_t* noise_codes = nullptr;
     size_t noise_codes_cap = 0;
-    uint32_t* noise_touched = nullptr;
     ~qsim_state() {
         if (stream) (void)hipStreamSynchronize(stream);
         if (base) (void)hipFree(base);
         if (alt_base) (void)hipFree(alt_base);
         if (noise_codes) (void)hipFree(noise_codes);
-        if (noise_touched) (void)hipFree(noise_touched);
         if (d_partials) (void)hipFree(d_partials);
         if (d_result) (void)hipFree(d_result);
         if (stream) (void)hipStreamDestroy(stream);
@@ -285,7 +283,7 @@ static void release_alt(qsim_state* s) {
 
 // Buffers of the pulled noise path: the second state buffer, per-step flip codes, touched bits.
 static bool ensure_noise_buffers(qsim_state* s, size_t nch) {
-    const size_t codes_b = pull_noise_codes_bytes(s->n, 1, nch), touched_b = (sizeof(double2) << s->n) / 128;
+    const size_t codes_b = pull_noise_codes_bytes(s->n, 1, nch);
     if (!ensure_alt(s)) return false;
     auto grab = [&](uint32_t** p, size_t bytes) {
         if (hipMalloc((void**)p, bytes) != hipSuccess) {
@@ -305,7 +303,6 @@ static bool ensure_noise_buffers(qsim_state* s, size_t nch) {
         if (!grab(&s->noise_codes, codes_b)) return false;
         s->noise_codes_cap = codes_b;
     }
-    if (!s->noise_touched && !grab(&s->noise_touched, touched_b)) return false;
     return true;
 }
 
@@ -1346,7 +1343,7 @@ int qsim_state_memory_bytes(qsim_state* s, uint64_t* bytes) {
         QSIM_REQUIRE(bytes, QSIM_ERR_INVALID_ARGUMENT, "null out");
         const uint64_t amps = sizeof(double2) << s->n;
         *bytes = amps + (s->alt_base ? amps : 0) + 4096 * sizeof(double) + sizeof(double) + s->scratch.cap +
-                 s->ops.cap + s->stages.cap + s->noise_codes_cap + (s->noise_touched ? amps / 128 : 0);
+                 s->ops.cap + s->stages.cap + s->noise_codes_cap;
     });
 }
 
@@ -1420,8 +1417,8 @@ int qsim_noisy_run(qsim_state* s, const qsim_gate* gates, size_t count,
             uint64_t c_pending = 0;
             auto step = [&](const Op* op) {
                 double2* dst = s->alt;
-                launch_pull_noise_step(s->d, dst, s->n, 1, 0, chans, seed, c_pending, op, s->noise_codes,
-                                       s->noise_touched, s->stream, &s->timer);
+                launch_pull_noise_step(s->d, dst, s->n, 1, 0, chans, seed, c_pending, op, s->noise_codes, s->stream,
+                                       &s->timer);
                 s->alt = s->d;
                 s->d = dst;
             };

@@ -380,21 +380,20 @@ void launch_noise_after_gate(double2* st, int n, const std::vector<NoiseChan>& c
                              uint64_t& counter, hipStream_t s, Timer* tm, uint64_t batch, uint64_t traj0);
 // Pulled noise (noise.hip): the noise step after one gate (channels `chans`, passes counter0,
 // counter0 + 1, ...; the push kernels' draws) applied by the NEXT gate's pass: dst = U (P src)
-// out of place, op == null: the identity (the last step of a run).  codes: >=
-// pull_noise_codes_bytes; touched: (batch << n) / 8 bytes.  Supported when n >= 9, every
-// channel flips (depolarizing / X / Y / Z) and at most 32 can fire.
+// out of place, op == null: the identity (the last step of a run).  words: >=
+// pull_noise_codes_bytes (one code word per amplitude).  Supported when n >= 9, every channel
+// flips (depolarizing / X / Y / Z) and at most 32 can fire.
 bool pull_noise_supported(int n, const std::vector<NoiseChan>& chans);
 size_t pull_noise_codes_bytes(int n, uint64_t batch, size_t nch);
 void launch_pull_noise_step(const double2* src, double2* dst, int n, uint64_t batch, uint64_t traj0,
                             const std::vector<NoiseChan>& chans, uint64_t seed, uint64_t counter0,
-                            const Op* op, uint32_t* codes, uint32_t* touched, hipStream_t s, Timer* tm);
-// Its two halves, for callers that build the next step's map on another stream while this
-// step's pass runs (the map reads no amplitudes): the codes / touched bits of one noise step, and
-// the pass that pulls through them.
+                            const Op* op, void* words, hipStream_t s, Timer* tm);
+// Its two halves, for callers that build the next step's words on another stream while this
+// step's pass runs (the map reads no amplitudes).
 void launch_noise_map(int n, uint64_t batch, uint64_t traj0, const std::vector<NoiseChan>& chans, uint64_t seed,
-                      uint64_t counter0, uint32_t* codes, uint32_t* touched, hipStream_t s, Timer* tm);
+                      uint64_t counter0, void* words, hipStream_t s, Timer* tm);
 void launch_pull_gate(const double2* src, double2* dst, int n, uint64_t batch, const std::vector<NoiseChan>& chans,
-                      const Op* op, const uint32_t* codes, const uint32_t* touched, hipStream_t s, Timer* tm);
+                      const Op* op, const void* words, hipStream_t s, Timer* tm);
 
 // Density matrices as 2n-index-bit states (density.hip).
 void dm_lower(int n, const qsim_gate* gates, size_t count, const qsim_noise_channel* ch,

@@ -392,34 +392,42 @@ void launch_noise(double2* st, int n, int type, int qubit, double p, uint64_t se
 // Pulled noise: the flips after gate g applied by the NEXT gate's pass (BatchedSimulator's
 // reference process, NoisySimulator's flip channels).
 //
-// The flips of one noise step (every channel entry after one gate) form a signed permutation P
-// of the amplitudes (X swaps a pair, Y swaps it with phases -i / +i, Z negates its |1> member).
-// Pushing P into the state costs random 16-B reads and writes over most of the lines (one noise
-// step ~ one streaming pass of line traffic).  Instead the next gate's kernel reads
-// its inputs through P: (P psi)[k] = phase * psi[pi^-1(k)], found by walking the channels from
-// the last to the first (each flip on the current index moves it along the channel's qubit), and
-// writes U (P psi) out of place — one streaming pass per gate step instead of two.
+// The flips of one noise step (every channel entry after one gate, applied in channel order) form
+// a signed permutation P of the amplitudes (X swaps a pair, Y swaps it with phases -i / +i, Z
+// negates its |1> member).  Pushing P into the state costs random 16-B reads and writes over most
+// of the lines (one noise step ~ one streaming pass of line traffic).  Instead the next
+// gate's kernel reads its inputs through P: (P psi)[k] = i^e psi[s(k)], found by walking the
+// channels from the last to the first (a flip of the pair holding the current index moves it
+// along the channel's qubit, or only adds a phase), and writes U (P psi) out of place — one
+// streaming pass per gate step instead of two.
 //
 // The draws are exactly the push kernels' (flip_block: blocks of 256 global pairs, geometric
 // walks from the same counter hash), so both paths produce the same states:
-//   k_noise_map   per step, one thread per 512-amplitude region: walks the blocks holding the
-//                 region's pairs for every channel and writes (a) the 2-bit flip code of every
-//                 pair (0 none, 1 X, 2 Y, 3 Z; each block written by exactly one thread, so no
-//                 memset) and (b) one "touched" bit per amplitude (some channel flipped a pair
-//                 holding it, by its own index: the pull of an untouched amplitude is itself).
-//   k_pull_gate   the gate (2x2 / diagonal / SWAP with controls, or the identity after the last
-//                 gate) over the pulled inputs, src -> dst.
-// Needs n >= 9 (blocks and regions inside one trajectory), every channel a flip channel, <= 32.
+//   k_noise_words  per step, one work-group per region of 2^12 amplitudes (the whole trajectory
+//                  below 12 qubits): walks every block of pairs with a member in the region, for
+//                  every channel at once (one walk per thread), and ORs each flip's 2-bit code
+//                  (1 X, 2 Y, 3 Z) into the CODE WORD of both members in LDS (field c: bits
+//                  2c, 2c + 1), then stores the region's words (4 B per amplitude up to 16
+//                  channels, 8 B up to 32), coalesced.  A zero word: no channel flips a pair
+//                  holding that amplitude.
+//   k_pull_gate    the gate (2x2 / diagonal / SWAP with controls, or the identity after the last
+//                  gate) over the pulled inputs, src -> dst.  Amplitude, word and partner loads are
+//                  issued together (the common case, a zero word, is a plain streaming pass); a
+//                  non-zero word is walked from its highest field down, one dependent word load
+//                  per move (X / Y), none for Z.
+// Needs n >= 9, every channel a flip channel, <= 32 that can fire.
 // ---------------------------------------------------------------------------------------
-constexpr int kRegionLog = 9;  // 512 amplitudes: 16 touched words, <= 2 blocks of pairs per channel
+constexpr int kRegionLogMax = 12;
+constexpr int kMinPullQubits = 9;
 constexpr int kMaxPullChannels = 32;
+constexpr int kWordThreads = 256;
 struct MapArgs {
-    uint32_t* codes;     // [nch][pairs / 16]
-    uint32_t* touched;   // [amps / 32]
+    void* words;
     uint64_t amps;       // batch << n (this object's)
-    uint64_t cstride;    // words per channel = pairs / 16
-    uint64_t blk0;       // global block of local pair 0 = idx0 >> 8
+    uint64_t idx0;       // global pair index of local pair 0
+    int n, rl;           // qubits per trajectory, region log (min(12, n))
     int nch;
+    int task_off[kMaxPullChannels + 1];  // walks per region before channel c (prefix sums)
     FlipChan ch[kMaxPullChannels];
 };
 
@@ -439,72 +447,50 @@ __device__ __forceinline__ void walk_block(uint64_t gb, const FlipChan& c, F&& f
     }
 }
 
-constexpr int kMapThreads = 128;
-__global__ __launch_bounds__(kMapThreads) void k_noise_map(MapArgs a) {
-    // LDS, word-major so consecutive threads hit consecutive banks: touched mask (16 words) and
-    // the codes of up to two blocks (32 words) of the current channel
-    __shared__ uint32_t tw[16][kMapThreads];
-    __shared__ uint32_t cw[32][kMapThreads];
+template <class W>
+__global__ __launch_bounds__(kWordThreads) void k_noise_words(MapArgs a) {
+    __shared__ W w[1 << kRegionLogMax];
     const int t = threadIdx.x;
-    const uint64_t r = (uint64_t)blockIdx.x * kMapThreads + t;
-    const bool live = (r << kRegionLog) < a.amps;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) tw[i][t] = 0u;
-    if (live) {
-        const uint64_t k0 = r << kRegionLog;
-        for (int c = 0; c < a.nch; ++c) {
-            const FlipChan ch = a.ch[c];
-            const int q = ch.target;
-            if (q >= kRegionLog) {
-                // every amplitude of the region has bit q = side; its pairs: 512 consecutive
-                const int side = (int)((k0 >> q) & 1ull);
-                const uint64_t l0 = ((k0 >> (q + 1)) << q) | (k0 & ((1ull << q) - 1ull));
-                const uint64_t lb = l0 >> kFlipBlockLog;
-#pragma unroll
-                for (int i = 0; i < 32; ++i) cw[i][t] = 0u;
-                for (int h = 0; h < 2; ++h) {
-                    walk_block(a.blk0 + lb + (uint64_t)h, ch, [&](uint32_t l, uint32_t code) {
-                        const uint32_t o = (uint32_t)h * 256u + l;  // region offset (side fixed)
-                        tw[o >> 5][t] |= 1u << (o & 31u);
-                        cw[o >> 4][t] |= code << (2u * (o & 15u));
-                    });
-                }
-                if (side == 0) {  // the block's other region (side 1) walks it too, writes nothing
-                    uint4* dst = reinterpret_cast<uint4*>(a.codes + (uint64_t)c * a.cstride + (lb << 4));
-#pragma unroll
-                    for (int i = 0; i < 8; ++i)
-                        dst[i] = make_uint4(cw[4 * i][t], cw[4 * i + 1][t], cw[4 * i + 2][t], cw[4 * i + 3][t]);
-                }
-            } else {
-                // both members of the region's pairs lie in it: one block of 256 pairs
-                const uint64_t lb = r;
-#pragma unroll
-                for (int i = 0; i < 16; ++i) cw[i][t] = 0u;
-                walk_block(a.blk0 + lb, ch, [&](uint32_t l, uint32_t code) {
-                    const uint32_t lo = l & ((1u << q) - 1u);
-                    const uint32_t o0 = ((l ^ lo) << 1) | lo, o1 = o0 | (1u << q);
-                    tw[o0 >> 5][t] |= 1u << (o0 & 31u);
-                    tw[o1 >> 5][t] |= 1u << (o1 & 31u);
-                    cw[l >> 4][t] |= code << (2u * (l & 15u));
-                });
-                uint4* dst = reinterpret_cast<uint4*>(a.codes + (uint64_t)c * a.cstride + (lb << 4));
-#pragma unroll
-                for (int i = 0; i < 4; ++i)
-                    dst[i] = make_uint4(cw[4 * i][t], cw[4 * i + 1][t], cw[4 * i + 2][t], cw[4 * i + 3][t]);
-            }
+    const int R = 1 << a.rl;
+    for (int i = t; i < R; i += kWordThreads) w[i] = 0;
+    __syncthreads();
+    const uint64_t K0 = (uint64_t)blockIdx.x << a.rl;  // the region's first amplitude (this object)
+    const uint64_t traj = K0 >> a.n, r0 = K0 & ((1ull << a.n) - 1ull);
+    for (int task = t; task < a.task_off[a.nch]; task += kWordThreads) {
+        int c = 0;
+        while (task >= a.task_off[c + 1]) ++c;
+        const int j = task - a.task_off[c];
+        const FlipChan& ch = a.ch[c];
+        const int q = ch.target;
+        const W sh = (W)(2 * c);
+        uint64_t lbase;  // the first pair (this object's pair index) with a member in the region
+        if (q < a.rl) {  // both members in the region: 2^(rl-1) pairs
+            lbase = (traj << (a.n - 1)) + (r0 >> 1);
+        } else {         // one member in the region (bit q fixed): 2^rl consecutive pairs
+            lbase = (traj << (a.n - 1)) + (((r0 >> (q + 1)) << q) | (r0 & ((1ull << q) - 1ull)));
         }
-        uint4* td = reinterpret_cast<uint4*>(a.touched + (r << 4));
-#pragma unroll
-        for (int i = 0; i < 4; ++i) td[i] = make_uint4(tw[4 * i][t], tw[4 * i + 1][t], tw[4 * i + 2][t], tw[4 * i + 3][t]);
+        const uint64_t gb = ((a.idx0 + lbase) >> kFlipBlockLog) + (uint64_t)j;
+        walk_block(gb, ch, [&](uint32_t l, uint32_t code) {
+            const uint32_t lp = (uint32_t)j * (uint32_t)kFlipBlock + l;  // region-local pair
+            if (q < a.rl) {
+                const uint32_t lo = lp & ((1u << q) - 1u);
+                const uint32_t a0 = ((lp ^ lo) << 1) | lo;
+                atomicOr(&w[a0], (W)code << sh);
+                atomicOr(&w[a0 | (1u << q)], (W)code << sh);
+            } else {
+                atomicOr(&w[lp], (W)code << sh);
+            }
+        });
     }
+    __syncthreads();
+    W* out = static_cast<W*>(a.words) + K0;
+    for (int i = t; i < R; i += kWordThreads) out[i] = w[i];
 }
 
 struct PullArgs {
     const double2* src;
     double2* dst;
-    const uint32_t* codes;
-    const uint32_t* touched;
-    uint64_t cstride;
+    const void* words;
     uint64_t items;      // pairs (2x2 / diagonal) or amplitudes (SWAP / identity)
     int nch;
     int q[kMaxPullChannels];
@@ -514,46 +500,32 @@ struct PullArgs {
     double2 m[4];
 };
 
-// (P psi)[k]: untouched amplitudes are themselves; otherwise walk the channels last to first.
-// The code words of channels [0, hi] are fetched for the current index at once (independent
-// loads: one memory latency, not one per channel); only a flip that moves the index (X / Y)
-// starts another such round for the channels below it.
-__device__ __forceinline__ double2 pulled(const PullArgs& a, uint64_t k) {
-    if (!((a.touched[k >> 5] >> (k & 31ull)) & 1u)) return a.src[k];
+// (P psi)[k] for a non-zero code word w of k: the fields from the highest down; a move (X / Y)
+// re-reads the word at the new index, restricted to the channels below the one that moved it.
+template <class W>
+__device__ __forceinline__ double2 pull_walk(const PullArgs& a, const int* sq, const W* words, uint64_t k, W w,
+                                             double2 v) {
     int e = 0;  // phase i^e
-    int hi = a.nch - 1;
-    while (hi >= 0) {
-        uint32_t cw[kMaxPullChannels];
-#pragma unroll
-        for (int c = 0; c < kMaxPullChannels; ++c) {
-            if (c <= hi) {
-                const int q = a.q[c];
-                const uint64_t l = ((k >> (q + 1)) << q) | (k & ((1ull << q) - 1ull));
-                cw[c] = a.codes[(uint64_t)c * a.cstride + (l >> 4)] >> (2u * (uint32_t)(l & 15ull));
-            }
+    bool moved = false;
+    int hi = a.nch;  // fields [0, hi) still to apply
+    while (true) {
+        const W m = hi >= (int)(4 * sizeof(W)) ? w : (w & (((W)1 << (2 * hi)) - 1));
+        if (!m) break;
+        const int c = (int)(8 * sizeof(W) - 1 - (sizeof(W) == 8 ? __clzll((long long)m) : __clz((int)m))) >> 1;
+        const int code = (int)((w >> (2 * c)) & 3);
+        const int q = sq[c];
+        const int bit = (int)((k >> q) & 1ull);
+        hi = c;
+        if (code == 3) {  // Z: |1> <- -v[k1] (the index stays)
+            if (bit) e += 2;
+            continue;
         }
-        int next = -1;
-#pragma unroll
-        for (int c = kMaxPullChannels - 1; c >= 0; --c) {
-            if (c > hi || next >= 0) continue;
-            const uint32_t code = cw[c] & 3u;
-            if (!code) continue;
-            const int q = a.q[c];
-            const int bit = (int)((k >> q) & 1ull);
-            if (code == 1) {  // X: v[k ^ 2^q]
-                k ^= 1ull << q;
-                next = c - 1;
-            } else if (code == 2) {  // Y: |0> <- -i v[k1], |1> <- +i v[k0]
-                e += bit ? 1 : 3;
-                k ^= 1ull << q;
-                next = c - 1;
-            } else if (bit) {  // Z: |1> <- -v[k1] (the index stays)
-                e += 2;
-            }
-        }
-        hi = next;  // (-1: done; else the channels below a move, fetched for the new index)
+        if (code == 2) e += bit ? 1 : 3;  // Y: |0> <- -i v[k1], |1> <- +i v[k0]
+        k ^= 1ull << q;                  // X / Y: the partner's amplitude
+        moved = true;
+        w = words[k];
     }
-    const double2 v = a.src[k];
+    if (moved) v = a.src[k];
     switch (e & 3) {
         case 1: return make_double2(-v.y, v.x);
         case 2: return make_double2(-v.x, -v.y);
@@ -562,13 +534,21 @@ __device__ __forceinline__ double2 pulled(const PullArgs& a, uint64_t k) {
     }
 }
 
+template <class W>
 __global__ __launch_bounds__(256) void k_pull_gate(PullArgs a) {
+    __shared__ int sq[kMaxPullChannels];
+    if (threadIdx.x < kMaxPullChannels) sq[threadIdx.x] = a.q[threadIdx.x];
+    __syncthreads();
+    const W* words = static_cast<const W*>(a.words);
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.items; i += stride) {
         if (a.kind == K_M1 || a.kind == K_DIAG) {
             const uint64_t lo = i & ((1ull << a.t0) - 1ull);
             const uint64_t j0 = ((i ^ lo) << 1) | lo, j1 = j0 | (1ull << a.t0);
-            double2 x0 = pulled(a, j0), x1 = pulled(a, j1);
+            const W w0 = words[j0], w1 = words[j1];
+            double2 x0 = a.src[j0], x1 = a.src[j1];
+            if (w0) x0 = pull_walk(a, sq, words, j0, w0, x0);
+            if (w1) x1 = pull_walk(a, sq, words, j1, w1, x1);
             if ((j0 & a.cmask) == a.cmask) {
                 if (a.kind == K_M1) {
                     m1_pair(a.sub, a.m[0], a.m[1], a.m[2], a.m[3], x0, x1);
@@ -585,7 +565,10 @@ __global__ __launch_bounds__(256) void k_pull_gate(PullArgs a) {
                 const uint64_t b0 = (i >> a.t0) & 1ull, b1 = (i >> a.t1) & 1ull;
                 if (b0 != b1) s = i ^ ((1ull << a.t0) | (1ull << a.t1));
             }
-            a.dst[i] = pulled(a, s);
+            const W w = words[s];
+            double2 x = a.src[s];
+            if (w) x = pull_walk(a, sq, words, s, w, x);
+            a.dst[i] = x;
         }
     }
 }
@@ -593,7 +576,7 @@ __global__ __launch_bounds__(256) void k_pull_gate(PullArgs a) {
 bool pull_noise_supported(int n, const std::vector<NoiseChan>& chans) {
     const char* e = std::getenv("QSIM_NOISE_PULL");  // (read per run: tests switch it)
     const bool on = e == nullptr || std::atoi(e) != 0;
-    if (!on || n < kRegionLog || chans.empty()) return false;
+    if (!on || n < kMinPullQubits || chans.empty()) return false;
     int live = 0;
     for (const NoiseChan& c : chans) {
         if (!(c.type == 0 || c.type >= 3)) return false;  // damping channels stream every pair
@@ -602,8 +585,9 @@ bool pull_noise_supported(int n, const std::vector<NoiseChan>& chans) {
     return live <= kMaxPullChannels;
 }
 
+// Bytes of one step's code words: 4 per amplitude up to 16 channel entries, else 8.
 size_t pull_noise_codes_bytes(int n, uint64_t batch, size_t nch) {
-    return std::max<size_t>(1, nch) * ((batch << (n - 1)) / 16) * sizeof(uint32_t);
+    return (batch << n) * (nch <= 16 ? sizeof(uint32_t) : sizeof(uint64_t));
 }
 
 // The live (can-fire) channels of one noise step, keyed like the push kernels' passes.
@@ -623,38 +607,40 @@ static void pull_channels(int n, const std::vector<NoiseChan>& chans, uint64_t s
 }
 
 void launch_noise_map(int n, uint64_t batch, uint64_t traj0, const std::vector<NoiseChan>& chans, uint64_t seed,
-                      uint64_t counter0, uint32_t* codes, uint32_t* touched, hipStream_t s, Timer* tm) {
-    const uint64_t amps = batch << n, pairs = amps >> 1;
+                      uint64_t counter0, void* words, hipStream_t s, Timer* tm) {
+    if (n < kMinPullQubits) fail(QSIM_ERR_RUNTIME, "pulled noise needs >= 9 qubits");
+    const uint64_t amps = batch << n;
     MapArgs m{};
     PullArgs a{};
-    m.codes = codes;
-    m.touched = touched;
+    m.words = words;
     m.amps = amps;
-    m.cstride = pairs / 16;
-    m.blk0 = (traj0 << (n - 1)) >> kFlipBlockLog;
+    m.idx0 = traj0 << (n - 1);
+    m.n = n;
+    m.rl = std::min(n, kRegionLogMax);
     pull_channels(n, chans, seed, counter0, m, a);
-    if (!m.nch) {  // no channel can fire: every amplitude untouched
-        QSIM_HIPCHK(hipMemsetAsync(touched, 0, (amps / 32) * sizeof(uint32_t), s));
+    const size_t wb = chans.size() <= 16 ? sizeof(uint32_t) : sizeof(uint64_t);
+    if (!m.nch) {  // no channel can fire: every word zero
+        QSIM_HIPCHK(hipMemsetAsync(words, 0, amps * wb, s));
         return;
     }
+    for (int c = 0; c < m.nch; ++c)
+        m.task_off[c + 1] = m.task_off[c] + (1 << (m.ch[c].target < m.rl ? m.rl - 9 : m.rl - 8));
     TimedLaunch tl(tm, "noise_map", 0.0, s);
-    const uint64_t regions = amps >> kRegionLog;
-    hipLaunchKernelGGL(k_noise_map, dim3((unsigned)((regions + kMapThreads - 1) / kMapThreads)), dim3(kMapThreads),
-                       0, s, m);
+    const dim3 grid((unsigned)(amps >> m.rl));
+    if (wb == sizeof(uint32_t)) hipLaunchKernelGGL(k_noise_words<uint32_t>, grid, dim3(kWordThreads), 0, s, m);
+    else hipLaunchKernelGGL(k_noise_words<unsigned long long>, grid, dim3(kWordThreads), 0, s, m);
     QSIM_HIPCHK(hipGetLastError());
 }
 
 void launch_pull_gate(const double2* src, double2* dst, int n, uint64_t batch, const std::vector<NoiseChan>& chans,
-                      const Op* op, const uint32_t* codes, const uint32_t* touched, hipStream_t s, Timer* tm) {
+                      const Op* op, const void* words, hipStream_t s, Timer* tm) {
     const uint64_t amps = batch << n, pairs = amps >> 1;
     MapArgs m{};
     PullArgs a{};
     pull_channels(n, chans, 0, 0, m, a);  // (the live channels and their qubits; keys unused)
     a.src = src;
     a.dst = dst;
-    a.codes = codes;
-    a.touched = touched;
-    a.cstride = pairs / 16;
+    a.words = words;
     a.kind = op ? op->kind : -1;
     if (op) {
         a.sub = op->sub;
@@ -667,15 +653,16 @@ void launch_pull_gate(const double2* src, double2* dst, int n, uint64_t batch, c
     a.items = (a.kind == K_M1 || a.kind == K_DIAG) ? pairs : amps;
     const uint64_t blocks = std::min<uint64_t>((a.items + 255) / 256, 256ull * 64);
     TimedLaunch tl(tm, "pull_gate", 32.0 * (double)amps, s);
-    hipLaunchKernelGGL(k_pull_gate, dim3((unsigned)blocks), dim3(256), 0, s, a);
+    if (chans.size() <= 16) hipLaunchKernelGGL(k_pull_gate<uint32_t>, dim3((unsigned)blocks), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL(k_pull_gate<unsigned long long>, dim3((unsigned)blocks), dim3(256), 0, s, a);
     QSIM_HIPCHK(hipGetLastError());
 }
 
 void launch_pull_noise_step(const double2* src, double2* dst, int n, uint64_t batch, uint64_t traj0,
                             const std::vector<NoiseChan>& chans, uint64_t seed, uint64_t counter0,
-                            const Op* op, uint32_t* codes, uint32_t* touched, hipStream_t s, Timer* tm) {
-    launch_noise_map(n, batch, traj0, chans, seed, counter0, codes, touched, s, tm);
-    launch_pull_gate(src, dst, n, batch, chans, op, codes, touched, s, tm);
+                            const Op* op, void* words, hipStream_t s, Timer* tm) {
+    launch_noise_map(n, batch, traj0, chans, seed, counter0, words, s, tm);
+    launch_pull_gate(src, dst, n, batch, chans, op, words, s, tm);
 }
 
 }  // namespace qsim_hip
