@@ -534,41 +534,74 @@ __device__ __forceinline__ double2 pull_walk(const PullArgs& a, const int* sq, c
     }
 }
 
-template <class W>
+// U items per thread, all of their word and amplitude loads issued before any is used.
+//   PAIR (2x2 with target >= 6): item = pair; both members' runs are contiguous across lanes.
+//   else item = amplitude: a 2x2 on a target below 6 takes the partner from the lane 2^t0 away
+//   (a wave holds both members), diagonals act per amplitude, SWAP / identity read their source.
+constexpr int kPullU = 4;
+template <class W, bool PAIR>
 __global__ __launch_bounds__(256) void k_pull_gate(PullArgs a) {
     __shared__ int sq[kMaxPullChannels];
     if (threadIdx.x < kMaxPullChannels) sq[threadIdx.x] = a.q[threadIdx.x];
     __syncthreads();
     const W* words = static_cast<const W*>(a.words);
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.items; i += stride) {
-        if (a.kind == K_M1 || a.kind == K_DIAG) {
+    const uint64_t base = ((uint64_t)blockIdx.x * kPullU) << 8;
+    if (base >= a.items) return;  // (items is a multiple of 256: whole waves in or out)
+    if constexpr (PAIR) {
+        uint64_t j0[kPullU];
+        W w0[kPullU], w1[kPullU];
+        double2 x0[kPullU], x1[kPullU];
+#pragma unroll
+        for (int u = 0; u < kPullU; ++u) {
+            const uint64_t i = base + ((uint64_t)u << 8) + threadIdx.x;
             const uint64_t lo = i & ((1ull << a.t0) - 1ull);
-            const uint64_t j0 = ((i ^ lo) << 1) | lo, j1 = j0 | (1ull << a.t0);
-            const W w0 = words[j0], w1 = words[j1];
-            double2 x0 = a.src[j0], x1 = a.src[j1];
-            if (w0) x0 = pull_walk(a, sq, words, j0, w0, x0);
-            if (w1) x1 = pull_walk(a, sq, words, j1, w1, x1);
-            if ((j0 & a.cmask) == a.cmask) {
-                if (a.kind == K_M1) {
-                    m1_pair(a.sub, a.m[0], a.m[1], a.m[2], a.m[3], x0, x1);
-                } else {
-                    x0 = diag_apply(a.sub, a.d0_one, a.m[0], a.m[1], 0, x0);
-                    x1 = diag_apply(a.sub, a.d0_one, a.m[0], a.m[1], 1, x1);
-                }
+            j0[u] = ((i ^ lo) << 1) | lo;
+            const uint64_t j1 = j0[u] | (1ull << a.t0);
+            w0[u] = words[j0[u]];
+            w1[u] = words[j1];
+            x0[u] = ld<true>(a.src + j0[u]);
+            x1[u] = ld<true>(a.src + j1);
+        }
+#pragma unroll
+        for (int u = 0; u < kPullU; ++u) {
+            if (w0[u]) x0[u] = pull_walk(a, sq, words, j0[u], w0[u], x0[u]);
+            if (w1[u]) x1[u] = pull_walk(a, sq, words, j0[u] | (1ull << a.t0), w1[u], x1[u]);
+            if ((j0[u] & a.cmask) == a.cmask) m1_pair(a.sub, a.m[0], a.m[1], a.m[2], a.m[3], x0[u], x1[u]);
+            st<true>(a.dst + j0[u], x0[u]);
+            st<true>(a.dst + (j0[u] | (1ull << a.t0)), x1[u]);
+        }
+    } else {
+        uint64_t sk[kPullU];
+        W w[kPullU];
+        double2 x[kPullU];
+#pragma unroll
+        for (int u = 0; u < kPullU; ++u) {
+            const uint64_t k = base + ((uint64_t)u << 8) + threadIdx.x;
+            uint64_t s = k;
+            if (a.kind == K_SWAP && (k & a.cmask) == a.cmask) {
+                const uint64_t b0 = (k >> a.t0) & 1ull, b1 = (k >> a.t1) & 1ull;
+                if (b0 != b1) s = k ^ ((1ull << a.t0) | (1ull << a.t1));
             }
-            a.dst[j0] = x0;
-            a.dst[j1] = x1;
-        } else {
-            uint64_t s = i;
-            if (a.kind == K_SWAP && (i & a.cmask) == a.cmask) {
-                const uint64_t b0 = (i >> a.t0) & 1ull, b1 = (i >> a.t1) & 1ull;
-                if (b0 != b1) s = i ^ ((1ull << a.t0) | (1ull << a.t1));
+            sk[u] = s;
+            w[u] = words[s];
+            x[u] = ld<true>(a.src + s);
+        }
+#pragma unroll
+        for (int u = 0; u < kPullU; ++u) {
+            const uint64_t k = base + ((uint64_t)u << 8) + threadIdx.x;
+            if (w[u]) x[u] = pull_walk(a, sq, words, sk[u], w[u], x[u]);
+            double2 y = x[u];
+            const bool on = (k & a.cmask) == a.cmask;
+            const int bit = (int)((k >> a.t0) & 1ull);
+            if (a.kind == K_M1) {  // (target < 6: the partner is lane ^ 2^t0 of this wave)
+                double2 p;
+                p.x = __shfl_xor(y.x, 1 << a.t0);
+                p.y = __shfl_xor(y.y, 1 << a.t0);
+                if (on) y = m1_half(a.sub, a.m[0], a.m[1], a.m[2], a.m[3], bit, y, p);
+            } else if (a.kind == K_DIAG) {
+                if (on) y = diag_apply(a.sub, a.d0_one, a.m[0], a.m[1], bit, y);
             }
-            const W w = words[s];
-            double2 x = a.src[s];
-            if (w) x = pull_walk(a, sq, words, s, w, x);
-            a.dst[i] = x;
+            st<true>(a.dst + k, y);
         }
     }
 }
@@ -650,11 +683,15 @@ void launch_pull_gate(const double2* src, double2* dst, int n, uint64_t batch, c
         a.cmask = op->cmask;
         for (int i = 0; i < 4; ++i) a.m[i] = make_double2(op->m[2 * i], op->m[2 * i + 1]);
     }
-    a.items = (a.kind == K_M1 || a.kind == K_DIAG) ? pairs : amps;
-    const uint64_t blocks = std::min<uint64_t>((a.items + 255) / 256, 256ull * 64);
+    const bool pair = a.kind == K_M1 && a.t0 >= 6;
+    a.items = pair ? pairs : amps;  // (multiples of 256: n >= 9)
+    const dim3 grid((unsigned)((a.items + 256 * kPullU - 1) / (256 * kPullU)));
     TimedLaunch tl(tm, "pull_gate", 32.0 * (double)amps, s);
-    if (chans.size() <= 16) hipLaunchKernelGGL(k_pull_gate<uint32_t>, dim3((unsigned)blocks), dim3(256), 0, s, a);
-    else hipLaunchKernelGGL(k_pull_gate<unsigned long long>, dim3((unsigned)blocks), dim3(256), 0, s, a);
+    const bool w32 = chans.size() <= 16;
+    if (pair && w32) hipLaunchKernelGGL((k_pull_gate<uint32_t, true>), grid, dim3(256), 0, s, a);
+    else if (w32) hipLaunchKernelGGL((k_pull_gate<uint32_t, false>), grid, dim3(256), 0, s, a);
+    else if (pair) hipLaunchKernelGGL((k_pull_gate<unsigned long long, true>), grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((k_pull_gate<unsigned long long, false>), grid, dim3(256), 0, s, a);
     QSIM_HIPCHK(hipGetLastError());
 }
 
