@@ -538,8 +538,7 @@ __device__ __forceinline__ double2 pull_walk(const PullArgs& a, const int* sq, c
 //   PAIR (2x2 with target >= 6): item = pair; both members' runs are contiguous across lanes.
 //   else item = amplitude: a 2x2 on a target below 6 takes the partner from the lane 2^t0 away
 //   (a wave holds both members), diagonals act per amplitude, SWAP / identity read their source.
-constexpr int kPullU = 4;
-template <class W, bool PAIR>
+template <class W, bool PAIR, int kPullU, bool NT>
 __global__ __launch_bounds__(256) void k_pull_gate(PullArgs a) {
     __shared__ int sq[kMaxPullChannels];
     if (threadIdx.x < kMaxPullChannels) sq[threadIdx.x] = a.q[threadIdx.x];
@@ -559,16 +558,16 @@ __global__ __launch_bounds__(256) void k_pull_gate(PullArgs a) {
             const uint64_t j1 = j0[u] | (1ull << a.t0);
             w0[u] = words[j0[u]];
             w1[u] = words[j1];
-            x0[u] = ld<true>(a.src + j0[u]);
-            x1[u] = ld<true>(a.src + j1);
+            x0[u] = ld<NT>(a.src + j0[u]);
+            x1[u] = ld<NT>(a.src + j1);
         }
 #pragma unroll
         for (int u = 0; u < kPullU; ++u) {
             if (w0[u]) x0[u] = pull_walk(a, sq, words, j0[u], w0[u], x0[u]);
             if (w1[u]) x1[u] = pull_walk(a, sq, words, j0[u] | (1ull << a.t0), w1[u], x1[u]);
             if ((j0[u] & a.cmask) == a.cmask) m1_pair(a.sub, a.m[0], a.m[1], a.m[2], a.m[3], x0[u], x1[u]);
-            st<true>(a.dst + j0[u], x0[u]);
-            st<true>(a.dst + (j0[u] | (1ull << a.t0)), x1[u]);
+            st<NT>(a.dst + j0[u], x0[u]);
+            st<NT>(a.dst + (j0[u] | (1ull << a.t0)), x1[u]);
         }
     } else {
         uint64_t sk[kPullU];
@@ -584,7 +583,7 @@ __global__ __launch_bounds__(256) void k_pull_gate(PullArgs a) {
             }
             sk[u] = s;
             w[u] = words[s];
-            x[u] = ld<true>(a.src + s);
+            x[u] = ld<NT>(a.src + s);
         }
 #pragma unroll
         for (int u = 0; u < kPullU; ++u) {
@@ -601,7 +600,7 @@ __global__ __launch_bounds__(256) void k_pull_gate(PullArgs a) {
             } else if (a.kind == K_DIAG) {
                 if (on) y = diag_apply(a.sub, a.d0_one, a.m[0], a.m[1], bit, y);
             }
-            st<true>(a.dst + k, y);
+            st<NT>(a.dst + k, y);
         }
     }
 }
@@ -685,13 +684,36 @@ void launch_pull_gate(const double2* src, double2* dst, int n, uint64_t batch, c
     }
     const bool pair = a.kind == K_M1 && a.t0 >= 6;
     a.items = pair ? pairs : amps;  // (multiples of 256: n >= 9)
-    const dim3 grid((unsigned)((a.items + 256 * kPullU - 1) / (256 * kPullU)));
+    // QSIM_PULL_U (items per thread, 2 / 4 / 8, default 4), QSIM_PULL_NT (non-temporal amplitude
+    // traffic, default 1): read per launch (measurement sweeps)
+    const char* ue = std::getenv("QSIM_PULL_U");
+    const char* ne = std::getenv("QSIM_PULL_NT");
+    const int U = ue ? std::atoi(ue) : 4;
+    const bool nt = ne == nullptr || std::atoi(ne) != 0;
+    const int Uc = U <= 2 ? 2 : (U >= 8 ? 8 : 4);
+    const dim3 grid((unsigned)((a.items + 256 * Uc - 1) / (256 * Uc)));
     TimedLaunch tl(tm, "pull_gate", 32.0 * (double)amps, s);
     const bool w32 = chans.size() <= 16;
-    if (pair && w32) hipLaunchKernelGGL((k_pull_gate<uint32_t, true>), grid, dim3(256), 0, s, a);
-    else if (w32) hipLaunchKernelGGL((k_pull_gate<uint32_t, false>), grid, dim3(256), 0, s, a);
-    else if (pair) hipLaunchKernelGGL((k_pull_gate<unsigned long long, true>), grid, dim3(256), 0, s, a);
-    else hipLaunchKernelGGL((k_pull_gate<unsigned long long, false>), grid, dim3(256), 0, s, a);
+#define QSIM_PULL_LAUNCH(W_, UU, NTT)                                                                      \
+    do {                                                                                                 \
+        if (pair) hipLaunchKernelGGL((k_pull_gate<W_, true, UU, NTT>), grid, dim3(256), 0, s, a);       \
+        else hipLaunchKernelGGL((k_pull_gate<W_, false, UU, NTT>), grid, dim3(256), 0, s, a);           \
+    } while (0)
+#define QSIM_PULL_LAUNCH_U(W_, NTT)                  \
+    do {                                           \
+        if (Uc == 2) QSIM_PULL_LAUNCH(W_, 2, NTT);  \
+        else if (Uc == 8) QSIM_PULL_LAUNCH(W_, 8, NTT); \
+        else QSIM_PULL_LAUNCH(W_, 4, NTT);         \
+    } while (0)
+    if (w32) {
+        if (nt) QSIM_PULL_LAUNCH_U(uint32_t, true);
+        else QSIM_PULL_LAUNCH_U(uint32_t, false);
+    } else {
+        if (nt) QSIM_PULL_LAUNCH_U(unsigned long long, true);
+        else QSIM_PULL_LAUNCH_U(unsigned long long, false);
+    }
+#undef QSIM_PULL_LAUNCH_U
+#undef QSIM_PULL_LAUNCH
     QSIM_HIPCHK(hipGetLastError());
 }
 
