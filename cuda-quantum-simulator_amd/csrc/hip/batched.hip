@@ -553,7 +553,7 @@ int qsim_batch_run(qsim_batch* b, const qsim_gate* gates, size_t count,
             std::vector<NoiseChan> dep;
             for (size_t i = 0; i < n_channels; ++i)
                 if (channels[i].type == 0) dep.push_back(NoiseChan{0, channels[i].qubit, channels[i].probability});
-            if (pull_noise_supported(b->n, dep) && ensure_pull_buffers(b, dep.size())) {
+            if (pull_noise_supported(b->n, dep, false) && ensure_pull_buffers(b, dep.size())) {
                 // Pulled: the noise after gate i is applied by gate i+1's pass (out of place),
                 // the noise after the last gate by one identity pass; same draws, same states.
                 // The map of noise step i (codes set i & 1) is built on map_stream while the pass

@@ -1409,7 +1409,7 @@ int qsim_noisy_run(qsim_state* s, const qsim_gate* gates, size_t count,
         std::vector<NoiseChan> chans;
         for (size_t c = 0; c < n_channels; ++c)
             chans.push_back(NoiseChan{channels[c].type, channels[c].qubit, channels[c].probability});
-        if (pull_noise_supported(s->n, chans) && ensure_noise_buffers(s, chans.size())) {
+        if (pull_noise_supported(s->n, chans, true) && ensure_noise_buffers(s, chans.size())) {
             // Flip channels only: the noise after gate i is applied by gate i+1's pass (out of
             // place), the noise after the last gate by one identity pass (noise.hip); the same
             // draws as the per-channel passes below, so the same state.

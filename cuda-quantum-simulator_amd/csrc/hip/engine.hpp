@@ -382,8 +382,9 @@ void launch_noise_after_gate(double2* st, int n, const std::vector<NoiseChan>& c
 // counter0 + 1, ...; the push kernels' draws) applied by the NEXT gate's pass: dst = U (P src)
 // out of place, op == null: the identity (the last step of a run).  words: >=
 // pull_noise_codes_bytes (one code word per amplitude).  Supported when n >= 9, every channel
-// flips (depolarizing / X / Y / Z) and at most 32 can fire.
-bool pull_noise_supported(int n, const std::vector<NoiseChan>& chans);
+// flips (depolarizing / X / Y / Z) and at most 32 can fire; QSIM_NOISE_PULL=0 / 1 overrides the
+// caller's default (NoisySimulator: on; BatchedSimulator: off — measured).
+bool pull_noise_supported(int n, const std::vector<NoiseChan>& chans, bool default_on);
 size_t pull_noise_codes_bytes(int n, uint64_t batch, size_t nch);
 void launch_pull_noise_step(const double2* src, double2* dst, int n, uint64_t batch, uint64_t traj0,
                             const std::vector<NoiseChan>& chans, uint64_t seed, uint64_t counter0,

@@ -605,9 +605,9 @@ __global__ __launch_bounds__(256) void k_pull_gate(PullArgs a) {
     }
 }
 
-bool pull_noise_supported(int n, const std::vector<NoiseChan>& chans) {
+bool pull_noise_supported(int n, const std::vector<NoiseChan>& chans, bool default_on) {
     const char* e = std::getenv("QSIM_NOISE_PULL");  // (read per run: tests switch it)
-    const bool on = e == nullptr || std::atoi(e) != 0;
+    const bool on = e == nullptr ? default_on : std::atoi(e) != 0;
     if (!on || n < kMinPullQubits || chans.empty()) return false;
     int live = 0;
     for (const NoiseChan& c : chans) {

@@ -115,7 +115,7 @@ def test_reference_noise_one_launch_per_gate(qsim, oracle, gpu_ready, monkeypatc
     """All Depolarizing passes after a gate in ONE launch (k_noise_units: a work-group per unit
     of whole trajectories, channels in order between work-group barriers), forced here at oracle
     sizes (QSIM_NOISE_UNIT_MIN=1), also on a trajectory shard whose pairs start mid-block.
-    (The push kernels: the pulled path, default from 9 qubits, is switched off here.)"""
+    (The push kernels, the batched default; pinned here in case the default changes.)"""
     monkeypatch.setenv("QSIM_NOISE_UNIT_MIN", "1")
     monkeypatch.setenv("QSIM_NOISE_PULL", "0")
     c = _circuit(qsim, n, 12, seed)
@@ -150,14 +150,16 @@ def test_reference_noise_one_launch_equals_per_channel_16q(qsim, gpu_ready, monk
     assert abs(np.sum(np.abs(out[0][1]) ** 2) - 1.0) < 1e-10
 
 
-# ---- pulled noise (noise.hip: k_noise_map + k_pull_gate, the default from 9 qubits) ----------
+# ---- pulled noise (noise.hip: k_noise_words + k_pull_gate; opt-in for the batched ensemble,
+# QSIM_NOISE_PULL=1 — measured no faster there; NoisySimulator's default) -----------
 # The flips after gate i are applied by gate i+1's pass, reading its inputs through the noise
 # permutation out of place; the flips after the last gate by one identity pass.  Same draws as
 # the push kernels, so the states are the push path's and the oracle's.
 
 @pytest.mark.parametrize("n,B,seed,traj0,refgates", [(9, 6, 5, 2, False), (10, 4, 8, 0, True),
                                                      (12, 3, 6, 5, False), (14, 2, 11, 1, False)])
-def test_pulled_noise_matches_oracle(qsim, oracle, gpu_ready, n, B, seed, traj0, refgates):
+def test_pulled_noise_matches_oracle(qsim, oracle, gpu_ready, monkeypatch, n, B, seed, traj0, refgates):
+    monkeypatch.setenv("QSIM_NOISE_PULL", "1")  # (the batched default is the push kernels)
     c = _circuit(qsim, n, 14, seed)
     nm = qsim.NoiseModel()
     nm.addDepolarizingAll(n, 0.2)
