@@ -509,6 +509,10 @@ int qsim_batch_run(qsim_batch* b, const qsim_gate* gates, size_t count,
                     return lops;
                 };
                 const int kind = 1 + (flags & QSIM_BATCH_REFERENCE_GATESET ? 1 : 0);
+                // (chosen under the tile-control rule the frame path plans with, and memoised
+                // under it)
+                std::unique_ptr<CtrlOutOff> ctrl_off;
+                if (frame_path) ctrl_off = std::make_unique<CtrlOutOff>();
                 if (!layout_memo_get(b->n, kind, gates, count * sizeof(qsim_gate), b->perm)) {
                     b->perm = choose_layout(b->n, lower_under, relabel_tries()).perm;
                     layout_memo_put(b->n, kind, gates, count * sizeof(qsim_gate), b->perm);

@@ -450,12 +450,15 @@ static void add_fix(GArgs& a, int pos) {
 // Launch-shape knobs (defaults from MI355X sweeps, DESIGN.md §per-gate kernels); overridable by
 // QSIM_SLICE_U / QSIM_LANE_U / QSIM_DIAG_U (wave-items in flight per lane) and QSIM_NT (0/1:
 // non-temporal HBM loads/stores) for tuning runs.
-// Far-partner slice targets (QSIM_SLICE_FAR_LO..HI, default 20..25: the pair's two 1 KiB runs
-// 16-512 MiB apart) stream slower with one wave-item in flight per lane (0.68-0.72 of 8 TB/s at
-// 28 qubits vs 0.74-0.84 for the others); they get QSIM_SLICE_U_FAR items.
+// Far-partner slice targets (QSIM_SLICE_FAR_LO..HI, default 14 and up: the pair's two 1 KiB
+// runs >= 256 KiB apart) stream slower (0.70-0.73 of 8 TB/s at 28 qubits vs 0.74-0.84 for the
+// others); on states of >= QSIM_SLICE_FAR_MIN_QUBITS (24) they run QSIM_SLICE_FAR_MODE 2 (each
+// wave takes QSIM_SLICE_U_FAR = 2 consecutive items, the |0> runs' loads before the |1> runs').
+// Round-4 sweep (profiles/r04/w1q/): mode 2 / 2 items gives min 0.711, mean 0.721 over targets
+// 14-27 (mode 0 with 1-4 items: 0.68-0.71 minima).
 struct Tune {
     int slice_u = 1, lane_u = 2, diag_u = 2;
-    int slice_u_far = 4, far_lo = 20, far_hi = 25, far_mode = 0;
+    int slice_u_far = 2, far_lo = 14, far_hi = 63, far_mode = 2, far_min_n = 24;
     bool nt = true;
     Tune() {
         auto env = [](const char* k, int d) {
@@ -467,6 +470,7 @@ struct Tune {
         far_lo = env("QSIM_SLICE_FAR_LO", far_lo);
         far_hi = env("QSIM_SLICE_FAR_HI", far_hi);
         far_mode = env("QSIM_SLICE_FAR_MODE", far_mode);
+        far_min_n = env("QSIM_SLICE_FAR_MIN_QUBITS", far_min_n);
         lane_u = env("QSIM_LANE_U", lane_u);
         diag_u = env("QSIM_DIAG_U", diag_u);
         nt = env("QSIM_NT", nt ? 1 : 0) != 0;
@@ -553,7 +557,7 @@ void launch_op(double2* st, int n, uint64_t batch, const Op& op, hipStream_t s, 
                 add_fix(a, op.t0);
                 finish();
                 TimedLaunch tl(tm, "m1_slice", bytes, s, true);
-                const bool far = op.t0 >= T.far_lo && op.t0 <= T.far_hi;
+                const bool far = op.t0 >= T.far_lo && op.t0 <= T.far_hi && n >= T.far_min_n;
                 if (far && T.far_mode == 1) {
                     QSIM_GO_U(k_m1_slice_g, T.slice_u_far, QSIM_U248);
                 } else if (far && T.far_mode == 2) {

@@ -18,6 +18,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <functional>
+#include <memory>
 #include <mutex>
 #include <random>
 #include <thread>
@@ -251,6 +252,7 @@ LayoutChoice choose_layout(int n, const std::function<std::vector<Op>(const std:
                            int tries, size_t want_alts) {
     const int h = tile_height_default();  // the calling thread's height, for the worker threads too
     const double t13 = layout_t13();      // and its 13-qubit tile cost factor
+    const bool ctrl_out = tile_ctrl_out();  // (CtrlOutOff is per thread: carried into the workers)
     struct Cand {
         std::vector<int> pi;
         size_t passes = 0;
@@ -282,6 +284,8 @@ LayoutChoice choose_layout(int n, const std::function<std::vector<Op>(const std:
         for (size_t k = 0; k < cand.size(); ++k)
             th.emplace_back([&, k] {
                 const LayoutT13Scope sc(t13);
+                std::unique_ptr<CtrlOutOff> off;  // (the caller's tile-control rule, per thread)
+                if (!ctrl_out) off = std::make_unique<CtrlOutOff>();
                 plan_cand(cand[k]);
             });
         for (auto& t : th) t.join();
@@ -303,6 +307,8 @@ LayoutChoice choose_layout(int n, const std::function<std::vector<Op>(const std:
         for (size_t i = 0; i < pool.size(); ++i)
             th.emplace_back([&, i] {
                 const LayoutT13Scope sc(t13);
+                std::unique_ptr<CtrlOutOff> off;
+                if (!ctrl_out) off = std::make_unique<CtrlOutOff>();
                 const Cand& c = cand[pool[i]];
                 double b = 0.0, a = 0.0;
                 std::vector<int> sigma;

@@ -252,3 +252,20 @@ def test_relabeled_batch_equals_per_gate(qsim, gpu_ready, n, B):
         np.testing.assert_array_equal(fused.sampleWith(u), ref.sampleWith(u))
     finally:
         set_relabel(1, 26)
+
+
+def test_config4_physical_batch_plans_three_passes(qsim, gpu_ready):
+    """BASELINE config 4 (16q x 1024, W-HC seed 42) under the physical process: the relabeled
+    fused plan is 3 passes.  The labels are chosen under the frame path's tile-control rule
+    (every control a tile qubit) in every planning thread (round-4 regression: the relabel
+    workers planned with tile-constant controls, the frame path without, and ran 4 passes)."""
+    n, B = 16, 1024
+    c = qsim.createRandomHCCircuit(n, 100, 42)
+    nm = qsim.NoiseModel()
+    nm.addDepolarizingAll(n, 0.01)
+    s = qsim.BatchedSimulator(n, B, nm, noise=qsim.BatchedNoise.Physical)
+    s.setSeed(42)
+    s.run(c)
+    s.run(c)
+    assert s.lastRunInfo()[0] == 3
+    s.close()
