@@ -208,11 +208,18 @@ struct qsim_state {
     double2* alt = nullptr;
     double2* base_d = nullptr;  // the amplitudes' address inside `base` (d == base_d or alt_base)
     bool pinned = false;
-    // pulled noise (NoisySimulator flip channels, noise.hip): per-step flip codes and touched bits
-    uint32_t* noise_codes = nullptr;
-    size_t noise_codes_cap = 0;
+    // pulled noise (NoisySimulator flip channels, noise.hip): two sets of per-step code words
+    // (steps alternate), so the next step's words are built on noise_stream during this pass
+    unsigned char* noise_codes = nullptr;
+    size_t noise_codes_cap = 0;  // bytes of ONE set
+    hipStream_t noise_stream = nullptr;
+    hipEvent_t nev_map[2] = {}, nev_pull[2] = {}, nev_start = nullptr;
     ~qsim_state() {
         if (stream) (void)hipStreamSynchronize(stream);
+        if (noise_stream) (void)hipStreamSynchronize(noise_stream);
+        for (hipEvent_t e : {nev_map[0], nev_map[1], nev_pull[0], nev_pull[1], nev_start})
+            if (e) (void)hipEventDestroy(e);
+        if (noise_stream) (void)hipStreamDestroy(noise_stream);
         if (base) (void)hipFree(base);
         if (alt_base) (void)hipFree(alt_base);
         if (noise_codes) (void)hipFree(noise_codes);
@@ -281,11 +288,11 @@ static void release_alt(qsim_state* s) {
     s->alt = nullptr;
 }
 
-// Buffers of the pulled noise path: the second state buffer, per-step flip codes, touched bits.
+// Buffers of the pulled noise path: the second state buffer, two sets of per-step code words.
 static bool ensure_noise_buffers(qsim_state* s, size_t nch) {
     const size_t codes_b = pull_noise_codes_bytes(s->n, 1, nch);
     if (!ensure_alt(s)) return false;
-    auto grab = [&](uint32_t** p, size_t bytes) {
+    auto grab = [&](unsigned char** p, size_t bytes) {
         if (hipMalloc((void**)p, bytes) != hipSuccess) {
             (void)hipGetLastError();
             *p = nullptr;
@@ -300,8 +307,13 @@ static bool ensure_noise_buffers(qsim_state* s, size_t nch) {
             s->noise_codes = nullptr;
             s->noise_codes_cap = 0;
         }
-        if (!grab(&s->noise_codes, codes_b)) return false;
+        if (!grab(&s->noise_codes, 2 * codes_b)) return false;
         s->noise_codes_cap = codes_b;
+    }
+    if (!s->noise_stream) {
+        QSIM_HIPCHK(hipStreamCreateWithFlags(&s->noise_stream, hipStreamNonBlocking));
+        for (hipEvent_t* e : {&s->nev_map[0], &s->nev_map[1], &s->nev_pull[0], &s->nev_pull[1], &s->nev_start})
+            QSIM_HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
     }
     return true;
 }
@@ -1343,7 +1355,7 @@ int qsim_state_memory_bytes(qsim_state* s, uint64_t* bytes) {
         QSIM_REQUIRE(bytes, QSIM_ERR_INVALID_ARGUMENT, "null out");
         const uint64_t amps = sizeof(double2) << s->n;
         *bytes = amps + (s->alt_base ? amps : 0) + 4096 * sizeof(double) + sizeof(double) + s->scratch.cap +
-                 s->ops.cap + s->stages.cap + s->noise_codes_cap;
+                 s->ops.cap + s->stages.cap + 2 * s->noise_codes_cap;
     });
 }
 
@@ -1413,23 +1425,40 @@ int qsim_noisy_run(qsim_state* s, const qsim_gate* gates, size_t count,
             // Flip channels only: the noise after gate i is applied by gate i+1's pass (out of
             // place), the noise after the last gate by one identity pass (noise.hip); the same
             // draws as the per-channel passes below, so the same state.
-            bool pending = false;
-            uint64_t c_pending = 0;
-            auto step = [&](const Op* op) {
+            // The words of step i (set i & 1) are built on noise_stream while the pass of step
+            // i - 1 runs; the pass of step i waits for them, the words of step i + 2 for that pass
+            // (QSIM_NOISE_MAP_OVERLAP=0: one stream).
+            const char* oe = std::getenv("QSIM_NOISE_MAP_OVERLAP");
+            const bool overlap = oe == nullptr || std::atoi(oe) != 0;
+            const size_t G = ops.size();
+            const uint64_t c0 = *counter;
+            *counter += (uint64_t)G * n_channels;
+            auto words = [&](size_t i) { return (void*)(s->noise_codes + (i & 1) * s->noise_codes_cap); };
+            hipStream_t ms = overlap ? s->noise_stream : s->stream;
+            auto map = [&](size_t i) {
+                if (overlap && i >= 2) QSIM_HIPCHK(hipStreamWaitEvent(ms, s->nev_pull[i & 1], 0));
+                launch_noise_map(s->n, 1, 0, chans, seed, c0 + i * n_channels, words(i), ms, &s->timer);
+                if (overlap) QSIM_HIPCHK(hipEventRecord(s->nev_map[i & 1], ms));
+            };
+            if (overlap) {  // (the previous run's passes may still read both sets)
+                QSIM_HIPCHK(hipEventRecord(s->nev_start, s->stream));
+                QSIM_HIPCHK(hipStreamWaitEvent(ms, s->nev_start, 0));
+                for (size_t i = 0; i < std::min<size_t>(G, 2); ++i) map(i);
+            }
+            if (G) launch_op(s->d, s->n, 1, ops[0], s->stream, &s->timer);
+            for (size_t i = 0; i < G; ++i) {
+                if (overlap) QSIM_HIPCHK(hipStreamWaitEvent(s->stream, s->nev_map[i & 1], 0));
+                else map(i);
                 double2* dst = s->alt;
-                launch_pull_noise_step(s->d, dst, s->n, 1, 0, chans, seed, c_pending, op, s->noise_codes, s->stream,
-                                       &s->timer);
+                launch_pull_gate(s->d, dst, s->n, 1, chans, i + 1 < G ? &ops[i + 1] : nullptr, words(i), s->stream,
+                                 &s->timer);
                 s->alt = s->d;
                 s->d = dst;
-            };
-            for (const Op& op : ops) {
-                if (!pending) launch_op(s->d, s->n, 1, op, s->stream, &s->timer);
-                else step(&op);
-                pending = true;
-                c_pending = *counter;
-                *counter += n_channels;
+                if (overlap && i + 2 < G) {
+                    QSIM_HIPCHK(hipEventRecord(s->nev_pull[i & 1], s->stream));
+                    map(i + 2);
+                }
             }
-            if (pending) step(nullptr);
             if (s->pinned && s->d != s->base_d) {  // keep the amplitudes where the handed-out pointer points
                 QSIM_HIPCHK(hipMemcpyAsync(s->base_d, s->d, sizeof(double2) << s->n, hipMemcpyDeviceToDevice,
                                            s->stream));

@@ -147,11 +147,15 @@ def test_noise_free_run_is_fused_and_exact(qsim, oracle, gpu_ready):
         sim.applyNoiseToQubit(qsim.NoiseType.BitFlip, n, 0.5)
 
 
-@pytest.mark.parametrize("n,seed,types", [(10, 4, (0, 3, 4, 5)), (12, 5, (0, 0, 5, 3)), (11, 6, (0, 1, 3))])
-def test_pulled_flip_noise_matches_oracle(qsim, oracle, gpu_ready, n, seed, types):
+@pytest.mark.parametrize("overlap", ["1", "0"])
+@pytest.mark.parametrize("n,seed,types", [(10, 4, (0, 3, 4, 5)), (12, 5, (0, 0, 5, 3)), (11, 6, (0, 1, 3)),
+                                          (9, 7, (0,) * 20)])
+def test_pulled_flip_noise_matches_oracle(qsim, oracle, gpu_ready, monkeypatch, n, seed, types, overlap):
     """From 9 qubits, flip-only noise models run pulled (the noise after gate i applied by gate
-    i+1's pass, out of place; noise.hip) — exactly the oracle's per-pair passes.  A damping
-    channel in the model keeps the per-channel passes (third case)."""
+    i+1's pass, out of place; noise.hip) — exactly the oracle's per-pair passes, with the next
+    step's code words built on a second stream or not, and with > 16 channel entries (64-bit
+    words, fourth case).  A damping channel in the model keeps the per-channel passes (third)."""
+    monkeypatch.setenv("QSIM_NOISE_MAP_OVERLAP", overlap)
     rng = np.random.default_rng(seed)
     c = qsim.createRandomCircuit(n, 16, seed)
     channels = [(int(t), int(rng.integers(0, n)), float(rng.uniform(0.1, 0.5))) for t in types]
