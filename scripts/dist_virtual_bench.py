@@ -39,7 +39,8 @@ for _ in range(steps):
 d.synchronize()
 wall = time.perf_counter() - t0
 st = d.profileStats()
-out = {"n": n, "world": world, "steps": steps, "wall_ms_per_run_all_shards": wall / steps * 1e3}
+out = {"n": n, "world": world, "steps": steps, "wall_ms_per_run_all_shards": wall / steps * 1e3,
+       "fused_remaps_last_run": d.fusedRemaps()}
 for s in st:
     out[s["name"]] = {"ms_per_run": s["ms"] / steps, "launches_per_run": s["launches"] / steps,
                       "per_rank_ms_per_run": s["ms"] / steps / world,
