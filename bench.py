@@ -136,6 +136,15 @@ def cpu_baseline(circuit, n, budget, q=None, args=None):
             full20 = {"value": round(len(g20) / m, 2), "unit": "gates/s", "cores": 1, "kind": "port",
                       "sample": f"W-HC depth {args.depth} seed {args.seed} at 20 qubits, median of "
                                 f"{len(runs)} whole runs ({', '.join(f'{r:.3f}' for r in runs)} s)"}
+    pre28 = None
+    if q is not None and args is not None and args.workload == "hc" and budget > 0:
+        # BASELINE.md §3 plan: the same circuit family at 28 qubits (config 3), a prefix of it
+        c28 = q.createRandomHCCircuit(28, args.depth, args.seed)
+        d28, s28 = orc.time_prefix(28, orc.gates_of(c28), min(budget, 8.0))
+        if d28 and s28 > 0:
+            pre28 = {"value": round(d28 / s28, 3), "unit": "gates/s", "cores": 1, "kind": "port",
+                     "sample": f"prefix-extrapolated: first {d28} gates of W-HC depth {args.depth} seed "
+                               f"{args.seed} at 28 qubits, one run, single thread, {s28:.1f} s"}
     cpu_model = "unknown"
     try:
         with open("/proc/cpuinfo") as f:
@@ -146,7 +155,7 @@ def cpu_baseline(circuit, n, budget, q=None, args=None):
     except OSError:
         pass
     return {"value": done / secs if secs > 0 else None, "unit": "gates/s", "cores": 1,
-            "kind": "port", "w_hc_20q": full20,
+            "kind": "port", "w_hc_20q": full20, "w_hc_28q": pre28,
             "sample": f"prefix-extrapolated: first {done} gates of the same circuit at n={n}, one "
                       f"run, single thread, {secs:.1f} s ({cpu_model}; host has {os.cpu_count()} "
                       f"logical CPUs); value = prefix gates / prefix time"}
