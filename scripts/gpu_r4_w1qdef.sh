@@ -19,4 +19,5 @@ run old QSIM_SLICE_FAR_MODE=0 QSIM_SLICE_U_FAR=4 QSIM_SLICE_FAR_LO=20 QSIM_SLICE
 run m2u2_20_27 QSIM_SLICE_FAR_MODE=2 QSIM_SLICE_U_FAR=2 QSIM_SLICE_FAR_LO=20 QSIM_SLICE_FAR_HI=27 || exit 1
 run m2u2_20_25 QSIM_SLICE_FAR_MODE=2 QSIM_SLICE_U_FAR=2 QSIM_SLICE_FAR_LO=20 QSIM_SLICE_FAR_HI=25 || exit 1
 run m2u4_20_27 QSIM_SLICE_FAR_MODE=2 QSIM_SLICE_U_FAR=4 QSIM_SLICE_FAR_LO=20 QSIM_SLICE_FAR_HI=27 || exit 1
+run m2u2_20_27_nt0 QSIM_NT=0 QSIM_SLICE_FAR_MODE=2 QSIM_SLICE_U_FAR=2 QSIM_SLICE_FAR_LO=20 QSIM_SLICE_FAR_HI=27 || exit 1
 run new_default || exit 1
