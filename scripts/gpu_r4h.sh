@@ -11,3 +11,4 @@ bash scripts/gpu_r4_w1qdef.sh $O/w1qdef || exit 1
 bash scripts/gpu_r4_noisy.sh $O/noisy || exit 1
 timeout -k 10 400 python -u scripts/dist_virtual_bench.py 30 8 4 > gpurun_out/$O/dist_virtual_30q8.json 2> gpurun_out/$O/dist_virtual.err || { tail -5 gpurun_out/$O/dist_virtual.err; exit 1; }
 head -c 1500 gpurun_out/$O/dist_virtual_30q8.json
+bash scripts/gpu_r4_dmpmc.sh $O/dmpmc
