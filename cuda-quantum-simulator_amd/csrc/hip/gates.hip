@@ -450,15 +450,16 @@ static void add_fix(GArgs& a, int pos) {
 // Launch-shape knobs (defaults from MI355X sweeps, DESIGN.md §per-gate kernels); overridable by
 // QSIM_SLICE_U / QSIM_LANE_U / QSIM_DIAG_U (wave-items in flight per lane) and QSIM_NT (0/1:
 // non-temporal HBM loads/stores) for tuning runs.
-// Far-partner slice targets (QSIM_SLICE_FAR_LO..HI, default 14 and up: the pair's two 1 KiB
-// runs >= 256 KiB apart) stream slower (0.70-0.73 of 8 TB/s at 28 qubits vs 0.74-0.84 for the
+// Far-partner slice targets (QSIM_SLICE_FAR_LO..HI, default 20..25: the pair's two 1 KiB runs
+// 16-512 MiB apart) stream slower (0.70-0.72 of 8 TB/s at 28 qubits vs 0.74-0.84 for the
 // others); on states of >= QSIM_SLICE_FAR_MIN_QUBITS (24) they run QSIM_SLICE_FAR_MODE 2 (each
 // wave takes QSIM_SLICE_U_FAR = 2 consecutive items, the |0> runs' loads before the |1> runs').
-// Round-4 sweep (profiles/r04/w1q/): mode 2 / 2 items gives min 0.711, mean 0.721 over targets
-// 14-27 (mode 0 with 1-4 items: 0.68-0.71 minima).
+// Round-4 measurements (profiles/r04/w1q/): W-1Q 28q mean 0.7652 with this choice, 0.7613 with
+// round 3's (mode 0, 4 items), 0.7519 with the far range widened to targets >= 14; no variant
+// lifts targets 20-25 above 0.72.
 struct Tune {
     int slice_u = 1, lane_u = 2, diag_u = 2;
-    int slice_u_far = 2, far_lo = 14, far_hi = 63, far_mode = 2, far_min_n = 24;
+    int slice_u_far = 2, far_lo = 20, far_hi = 25, far_mode = 2, far_min_n = 24;
     bool nt = true;
     Tune() {
         auto env = [](const char* k, int d) {
