@@ -545,13 +545,18 @@ __global__ __launch_bounds__(256) void k_pull_gate(PullArgs a) {
     __syncthreads();
     const W* words = static_cast<const W*>(a.words);
     const uint64_t base = ((uint64_t)blockIdx.x * kPullU) << 8;
-    if (base >= a.items) return;  // (items is a multiple of 256: whole waves in or out)
+    // items is a multiple of 256, so each item group u (256 consecutive items) is wholly in or
+    // wholly out of range for the whole work-group; groups past the end do nothing (a 9- or
+    // 10-qubit state has fewer items than one work-group's kPullU groups)
+    const int nu = (int)std::min<uint64_t>((uint64_t)kPullU, (a.items - std::min(a.items, base)) >> 8);
+    if (nu == 0) return;
     if constexpr (PAIR) {
         uint64_t j0[kPullU];
         W w0[kPullU], w1[kPullU];
         double2 x0[kPullU], x1[kPullU];
 #pragma unroll
         for (int u = 0; u < kPullU; ++u) {
+            if (u >= nu) break;
             const uint64_t i = base + ((uint64_t)u << 8) + threadIdx.x;
             const uint64_t lo = i & ((1ull << a.t0) - 1ull);
             j0[u] = ((i ^ lo) << 1) | lo;
@@ -563,6 +568,7 @@ __global__ __launch_bounds__(256) void k_pull_gate(PullArgs a) {
         }
 #pragma unroll
         for (int u = 0; u < kPullU; ++u) {
+            if (u >= nu) break;
             if (w0[u]) x0[u] = pull_walk(a, sq, words, j0[u], w0[u], x0[u]);
             if (w1[u]) x1[u] = pull_walk(a, sq, words, j0[u] | (1ull << a.t0), w1[u], x1[u]);
             if ((j0[u] & a.cmask) == a.cmask) m1_pair(a.sub, a.m[0], a.m[1], a.m[2], a.m[3], x0[u], x1[u]);
@@ -575,6 +581,7 @@ __global__ __launch_bounds__(256) void k_pull_gate(PullArgs a) {
         double2 x[kPullU];
 #pragma unroll
         for (int u = 0; u < kPullU; ++u) {
+            if (u >= nu) break;
             const uint64_t k = base + ((uint64_t)u << 8) + threadIdx.x;
             uint64_t s = k;
             if (a.kind == K_SWAP && (k & a.cmask) == a.cmask) {
@@ -587,6 +594,7 @@ __global__ __launch_bounds__(256) void k_pull_gate(PullArgs a) {
         }
 #pragma unroll
         for (int u = 0; u < kPullU; ++u) {
+            if (u >= nu) break;
             const uint64_t k = base + ((uint64_t)u << 8) + threadIdx.x;
             if (w[u]) x[u] = pull_walk(a, sq, words, sk[u], w[u], x[u]);
             double2 y = x[u];
@@ -684,6 +692,8 @@ void launch_pull_gate(const double2* src, double2* dst, int n, uint64_t batch, c
     }
     const bool pair = a.kind == K_M1 && a.t0 >= 6;
     a.items = pair ? pairs : amps;  // (multiples of 256: n >= 9)
+    if (n < kMinPullQubits || a.items % 256 != 0) fail(QSIM_ERR_RUNTIME, "pulled noise pass: bad shape");
+    if (!pair && a.kind == K_M1 && a.t0 >= 6) fail(QSIM_ERR_RUNTIME, "pulled noise pass: lane partner");
     // QSIM_PULL_U (items per thread, 2 / 4 / 8, default 4), QSIM_PULL_NT (non-temporal amplitude
     // traffic, default 1): read per launch (measurement sweeps)
     const char* ue = std::getenv("QSIM_PULL_U");
