@@ -602,7 +602,13 @@ int qsim_batch_run(qsim_batch* b, const qsim_gate* gates, size_t count,
                 return;
             }
             for (const Op& op : ops) {
-                if (op.kind >= 0) launch_op(b->d, b->n, (uint64_t)b->batch, op, b->stream, &b->timer);
+                const Op* o = op.kind >= 0 ? &op : nullptr;
+                if (gate_noise_tile_supported(b->n, o)) {  // (noise.hip: gate + in-tile channels in LDS)
+                    launch_gate_noise_step(b->d, b->n, (uint64_t)b->batch, b->traj0, o, dep, b->seed, b->ncounter,
+                                           b->stream, &b->timer);
+                    continue;
+                }
+                if (o) launch_op(b->d, b->n, (uint64_t)b->batch, op, b->stream, &b->timer);
                 launch_noise_after_gate(b->d, b->n, dep, b->seed, b->ncounter, b->stream, &b->timer,
                                         (uint64_t)b->batch, b->traj0);
             }

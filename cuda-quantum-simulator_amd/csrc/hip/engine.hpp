@@ -378,6 +378,13 @@ struct NoiseChan {
 };
 void launch_noise_after_gate(double2* st, int n, const std::vector<NoiseChan>& chans, uint64_t seed,
                              uint64_t& counter, hipStream_t s, Timer* tm, uint64_t batch, uint64_t traj0);
+// Gate + in-tile noise (noise.hip): the gate and the prefix of `chans` whose qubits lie in its
+// 4096-amplitude tile in one LDS pass, the rest by the push kernel; counter advances by
+// chans.size().  Same states as launch_op + launch_noise_after_gate.  op == null: no gate.
+bool gate_noise_tile_supported(int n, const Op* op);
+void launch_gate_noise_step(double2* st, int n, uint64_t batch, uint64_t traj0, const Op* op,
+                            const std::vector<NoiseChan>& chans, uint64_t seed, uint64_t& counter, hipStream_t s,
+                            Timer* tm);
 // Pulled noise (noise.hip): the noise step after one gate (channels `chans`, passes counter0,
 // counter0 + 1, ...; the push kernels' draws) applied by the NEXT gate's pass: dst = U (P src)
 // out of place, op == null: the identity (the last step of a run).  words: >=

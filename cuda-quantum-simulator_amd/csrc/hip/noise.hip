@@ -389,6 +389,236 @@ void launch_noise(double2* st, int n, int type, int qubit, double p, uint64_t se
 
 
 // ---------------------------------------------------------------------------------------
+// Gate + in-tile noise (BatchedSimulator's reference process, the push path's fast form).
+//
+// One gate step = the gate, then every channel entry in order.  A work-group owns a TILE of
+// 4096 amplitudes of one trajectory — qubits 0..10 plus one more, u (the gate's target when it is
+// >= 11, else 11) — holds it in LDS, applies the gate, then the longest PREFIX of the channel list
+// whose qubits lie in the tile: every such channel's flips are pairs inside the tile, so the
+// work-group walks their blocks (the push kernels' draws: blocks of 256 global pairs, geometric
+// gaps from the same counter hash), records each flip's 2-bit code per pair in LDS, and applies
+// the channels one after the other with a barrier between them.  The tile goes back in place
+// (it is this work-group's alone), and the remaining channels (the suffix) run as the one-launch
+// push kernel.  Same operations in the same order on every amplitude as gate kernel + push, so the
+// same states bit for bit; one streaming pass carries the gate and most of the noise.
+// (Needs n >= 12; W-BATCH's depolarizing-on-all-qubits list puts 11 or 12 of its 16 channels in
+// the prefix.)
+// ---------------------------------------------------------------------------------------
+constexpr int kGnTile = 12;
+constexpr int kGnMaxPrefix = 12;
+struct GnArgs {
+    double2* st;
+    int n;
+    int u;                 // the tile's 12th qubit (>= 11)
+    uint64_t idx0;         // global pair index of this object's pair 0
+    int kind;              // K_M1, K_DIAG, K_SWAP, or -1: no gate
+    int sub, t0, t1, d0_one;
+    uint32_t cm_in;        // controls inside the tile, as tile-local bits
+    uint64_t cm_out;       // controls outside the tile (trajectory-local index bits)
+    double2 m[4];
+    int np;                // prefix channels
+    FlipChan ch[kGnMaxPrefix];
+};
+__device__ __forceinline__ int gn_local_pos(int q, int u) { return q <= 10 ? q : (q == u ? 11 : -1); }
+
+__global__ __launch_bounds__(256) void k_gate_noise_tile(GnArgs a) {
+    __shared__ double2 v[1 << kGnTile];
+    __shared__ uint32_t codes[kGnMaxPrefix][2048 / 16];
+    const int t = threadIdx.x;
+    // this work-group's tile: trajectory traj, the n - 12 non-tile bits from the block index
+    const int nfree = a.n - kGnTile;
+    const uint64_t traj = (uint64_t)blockIdx.x >> nfree;
+    const uint64_t m = (uint64_t)blockIdx.x & ((1ull << nfree) - 1ull);
+    // non-tile local bits: 11 .. n-1 except u, ascending
+    uint64_t loc = 0;
+    {
+        int j = 0;
+        for (int b = 11; b < a.n; ++b) {
+            if (b == a.u) continue;
+            loc |= ((m >> j) & 1ull) << b;
+            ++j;
+        }
+    }
+    const uint64_t gbase = (traj << a.n) | loc;  // tile-local j -> gbase | (j & 2047) | (j >> 11) << u
+    auto gidx = [&](int j) { return gbase | (uint64_t)(j & 2047) | ((uint64_t)(j >> 11) << a.u); };
+#pragma unroll 4
+    for (int r = 0; r < 16; ++r) {
+        const int j = r * 256 + t;
+        v[j] = ld<true>(a.st + gidx(j));
+    }
+    for (int i = t; i < a.np * (2048 / 16); i += 256) codes[i / 128][i % 128] = 0u;
+    __syncthreads();
+    // the gate
+    const bool on_out = (loc & a.cm_out) == a.cm_out;
+    if (a.kind >= 0 && on_out) {
+        const int p0 = gn_local_pos(a.t0, a.u);
+        if (a.kind == K_M1) {
+            for (int i = t; i < 2048; i += 256) {
+                const int lo = i & ((1 << p0) - 1);
+                const int j0 = ((i ^ lo) << 1) | lo, j1 = j0 | (1 << p0);
+                if (((uint32_t)j0 & a.cm_in) != a.cm_in) continue;
+                double2 x0 = v[j0], x1 = v[j1];
+                m1_pair(a.sub, a.m[0], a.m[1], a.m[2], a.m[3], x0, x1);
+                v[j0] = x0;
+                v[j1] = x1;
+            }
+        } else if (a.kind == K_DIAG) {
+            for (int j = t; j < 4096; j += 256) {
+                if (((uint32_t)j & a.cm_in) != a.cm_in) continue;
+                v[j] = diag_apply(a.sub, a.d0_one, a.m[0], a.m[1], (j >> p0) & 1, v[j]);
+            }
+        } else {  // SWAP (both qubits in the tile)
+            const int p1 = gn_local_pos(a.t1, a.u);
+            for (int j = t; j < 4096; j += 256) {
+                if (((j >> p0) & 1) == 0 && ((j >> p1) & 1) == 1 && ((uint32_t)j & a.cm_in) == a.cm_in) {
+                    const int k = j ^ ((1 << p0) | (1 << p1));
+                    const double2 x = v[j];
+                    v[j] = v[k];
+                    v[k] = x;
+                }
+            }
+        }
+    }
+    // the prefix channels' flips: 8 blocks of 256 pairs each, one walk per thread
+    if (t < a.np * 8) {
+        const int c = t >> 3, jb = t & 7;
+        const FlipChan& ch = a.ch[c];
+        const int q = ch.target;
+        const uint64_t tl = gbase & ((1ull << a.n) - 1ull);  // trajectory-local base
+        // pair index (within the trajectory) of the tile's first pair of this channel
+        const uint64_t prb = ((tl >> (q + 1)) << q) | (tl & ((1ull << q) - 1ull));
+        uint64_t pr0;  // first pair of this walk's run
+        int run_base;  // tile pair-local index of that pair
+        if (q == a.u) {
+            pr0 = prb + (uint64_t)jb * 256;
+            run_base = jb * 256;
+        } else {  // two runs of 1024 pairs, bit u of the index -> pair bit u - 1
+            const int y = jb >> 2;
+            pr0 = prb + ((uint64_t)y << (a.u - 1)) + (uint64_t)(jb & 3) * 256;
+            run_base = (y << 10) + (jb & 3) * 256;
+        }
+        const uint64_t gb = (a.idx0 + (traj << (a.n - 1)) + pr0) >> kFlipBlockLog;
+        FlipCursor cur{nz_mix(ch.key ^ nz_mix(gb ^ kBlockSalt)), 0, -1, false};
+        uint64_t g = 0, h = 0;
+        const uint64_t lo = gb << kFlipBlockLog, hi = lo + kFlipBlock;
+        while (next_flip(cur, gb, lo, hi, ch, g, h)) {
+            int code = ch.type == 3 ? 1 : (ch.type == 4 ? 3 : 2);
+            if (ch.type == 0) {
+                const float r2 = nz_uniform(nz_mix(h ^ 0x5bd1e9955bd1e995ull));
+                code = r2 < 1.0f / 3.0f ? 1 : (r2 < 2.0f / 3.0f ? 2 : 3);
+            }
+            const int x = run_base + (int)(g - lo);
+            atomicOr(&codes[c][x >> 4], (uint32_t)code << (2 * (x & 15)));
+        }
+    }
+    __syncthreads();
+    for (int c = 0; c < a.np; ++c) {
+        const int q = a.ch[c].target;
+        const int pq = gn_local_pos(q, a.u);
+        for (int x = t; x < 2048; x += 256) {
+            const uint32_t code = (codes[c][x >> 4] >> (2 * (x & 15))) & 3u;
+            if (!code) continue;
+            int j0;
+            if (pq == 11) {
+                j0 = x;
+            } else {
+                const int xl = x & 1023, y = x >> 10;
+                const int lo = xl & ((1 << pq) - 1);
+                j0 = (((xl ^ lo) << 1) | lo) | (y << 11);
+            }
+            const int j1 = j0 | (1 << pq);
+            if (code == 3) {
+                const double2 w = v[j1];
+                v[j1] = make_double2(-w.x, -w.y);
+            } else {
+                const double2 a0 = v[j0], a1 = v[j1];
+                if (code == 1) {
+                    v[j0] = a1;
+                    v[j1] = a0;
+                } else {
+                    v[j0] = make_double2(a1.y, -a1.x);
+                    v[j1] = make_double2(-a0.y, a0.x);
+                }
+            }
+        }
+        __syncthreads();
+    }
+#pragma unroll 4
+    for (int r = 0; r < 16; ++r) {
+        const int j = r * 256 + t;
+        st<true>(a.st + gidx(j), v[j]);
+    }
+}
+
+bool gate_noise_tile_supported(int n, const Op* op) {
+    const char* e = std::getenv("QSIM_NOISE_TILE");  // (read per run: tests switch it)
+    if (e && std::atoi(e) == 0) return false;
+    if (n < kGnTile) return false;
+    if (!op) return true;
+    if (op->kind == K_SWAP) {
+        const int hi0 = op->t0 >= 11, hi1 = op->t1 >= 11;
+        if (hi0 && hi1) return false;  // (two qubits above 10: not one tile)
+    }
+    return true;
+}
+
+void launch_gate_noise_step(double2* st, int n, uint64_t batch, uint64_t traj0, const Op* op,
+                            const std::vector<NoiseChan>& chans, uint64_t seed, uint64_t& counter, hipStream_t s,
+                            Timer* tm) {
+    GnArgs a{};
+    a.st = st;
+    a.n = n;
+    a.idx0 = traj0 << (n - 1);
+    int u = 11;
+    if (op) {
+        if (op->t0 >= 11) u = op->t0;
+        if (op->kind == K_SWAP && op->t1 >= 11) u = op->t1;
+    }
+    a.u = u;
+    a.kind = op ? op->kind : -1;
+    if (op) {
+        a.sub = op->sub;
+        a.t0 = op->t0;
+        a.t1 = op->t1;
+        a.d0_one = op->d0_one ? 1 : 0;
+        for (int q = 0; q < n; ++q) {
+            if (!((op->cmask >> q) & 1ull)) continue;
+            const int p = q <= 10 ? q : (q == u ? 11 : -1);
+            if (p >= 0) a.cm_in |= 1u << p;
+            else a.cm_out |= 1ull << q;
+        }
+        for (int i = 0; i < 4; ++i) a.m[i] = make_double2(op->m[2 * i], op->m[2 * i + 1]);
+    }
+    // the prefix: channel entries in order whose qubit is in the tile (a channel that cannot fire
+    // is skipped but still uses its counter, as the push kernels do)
+    uint64_t c = counter;
+    size_t used = 0;
+    for (; used < chans.size(); ++used) {
+        const NoiseChan& ch = chans[used];
+        check_channel(n, ch.type, ch.qubit, ch.p);
+        const bool in = ch.qubit <= 10 || ch.qubit == u;
+        if (!in || !(ch.type == 0 || ch.type >= 3)) break;
+        if (flip_probability(ch.p) > 0.0) {
+            if (a.np == kGnMaxPrefix) break;  // (the rest goes to the push kernel)
+            flip_channel(ch.type, ch.qubit, ch.p, noise_key(seed, c), a.ch[a.np]);
+            ++a.np;
+        }
+        ++c;
+    }
+    {
+        TimedLaunch tl(tm, "gate_noise", 32.0 * (double)(batch << n), s);
+        const uint64_t blocks = (batch << n) >> kGnTile;
+        hipLaunchKernelGGL(k_gate_noise_tile, dim3((unsigned)blocks), dim3(256), 0, s, a);
+        QSIM_HIPCHK(hipGetLastError());
+    }
+    counter = c;
+    if (used < chans.size()) {
+        const std::vector<NoiseChan> rest(chans.begin() + (long)used, chans.end());
+        launch_noise_after_gate(st, n, rest, seed, counter, s, tm, batch, traj0);
+    }
+}
+
+// ---------------------------------------------------------------------------------------
 // Pulled noise: the flips after gate g applied by the NEXT gate's pass (BatchedSimulator's
 // reference process, NoisySimulator's flip channels).
 //

@@ -242,3 +242,49 @@ def test_one_launch_noise_accesses_stay_in_unit(qsim, oracle, gpu_ready, monkeyp
     whole, _ = oracle.batched_reference_run(n, traj0 + B, oracle.gates_of(c), entries, seed)
     for t in range(B):
         np.testing.assert_allclose(s.getStateVector(t), whole[traj0 + t], atol=1e-12, rtol=0)
+
+
+# ---- gate + in-tile noise (noise.hip: k_gate_noise_tile, the push path from 12 qubits) --------
+# The gate and the channels whose qubits lie in its 4096-amplitude tile (qubits 0..10 and one
+# more) in one LDS pass, the remaining channels by the one-launch push kernel: the same
+# operations in the same order, so the same states as gate kernel + push.
+
+@pytest.mark.parametrize("n,B,seed,traj0,refgates", [(12, 3, 21, 0, False), (13, 2, 22, 3, True),
+                                                     (14, 2, 23, 1, False)])
+def test_gate_noise_tile_matches_oracle(qsim, oracle, gpu_ready, monkeypatch, n, B, seed, traj0, refgates):
+    monkeypatch.setenv("QSIM_NOISE_TILE", "1")
+    c = _circuit(qsim, n, 14, seed)
+    nm = qsim.NoiseModel()
+    nm.addDepolarizingAll(n, 0.2)
+    nm.addDepolarizing([0, 11], 0.3)  # (repeated qubits: a longer prefix than the tile's qubits)
+    s = qsim.BatchedSimulator(n, B, nm, noise=qsim.BatchedNoise.Reference,
+                              gate_set=qsim.BatchedGateSet.Reference if refgates else qsim.BatchedGateSet.Full)
+    s.setSeed(seed)
+    s.setTrajectoryOffset(traj0)
+    entries = [(0, q, 0.2) for q in range(n)] + [(0, 0, 0.3), (0, 11, 0.3)]
+    whole, counter = None, 0
+    for _ in range(2):
+        s.run(c)
+        whole, counter = oracle.batched_reference_run(n, traj0 + B, oracle.gates_of(c), entries, seed,
+                                                      refgates, states=whole, counter=counter)
+    for t in range(B):
+        np.testing.assert_allclose(s.getStateVector(t), whole[traj0 + t], atol=1e-12, rtol=0)
+
+
+def test_gate_noise_tile_equals_push_16q(qsim, gpu_ready, monkeypatch):
+    """Config-4 shape (16 qubits, depolarizing 0.01 on every qubit, W-HC and the mixed gate
+    set): the tile kernel and gate kernel + push give bit-identical trajectories."""
+    n, B = 16, 64
+    nm = qsim.NoiseModel()
+    nm.addDepolarizingAll(n, 0.01)
+    for c in (qsim.createRandomHCCircuit(n, 30, 42), _circuit(qsim, n, 30, 5)):
+        out = []
+        for tile in ("1", "0"):
+            monkeypatch.setenv("QSIM_NOISE_TILE", tile)
+            s = qsim.BatchedSimulator(n, B, nm, noise=qsim.BatchedNoise.Reference)
+            s.setSeed(9)
+            s.run(c)
+            s.run(c)
+            out.append(np.stack([s.getStateVector(t) for t in (0, 31, 63)]))
+            s.close()
+        assert np.array_equal(out[0], out[1])
