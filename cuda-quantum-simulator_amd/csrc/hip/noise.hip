@@ -552,7 +552,7 @@ __global__ __launch_bounds__(256) void k_gate_noise_tile(GnArgs a) {
 
 bool gate_noise_tile_supported(int n, const Op* op) {
     const char* e = std::getenv("QSIM_NOISE_TILE");  // (read per run: tests switch it)
-    if (e && std::atoi(e) == 0) return false;
+    if (!(e && std::atoi(e) != 0)) return false;      // (opt-in until measured on the device)
     if (n < kGnTile) return false;
     if (!op) return true;
     if (op->kind == K_SWAP) {
