@@ -593,7 +593,9 @@ void launch_gate_noise_step(double2* st, int n, uint64_t batch, uint64_t traj0, 
     // is skipped but still uses its counter, as the push kernels do)
     uint64_t c = counter;
     size_t used = 0;
-    for (; used < chans.size(); ++used) {
+    const char* pe = std::getenv("QSIM_NOISE_TILE_PREFIX");  // (measurement: cap on the prefix)
+    const size_t cap = pe ? (size_t)std::max(0, std::atoi(pe)) : chans.size();
+    for (; used < chans.size() && used < cap; ++used) {
         const NoiseChan& ch = chans[used];
         check_channel(n, ch.type, ch.qubit, ch.p);
         const bool in = ch.qubit <= 10 || ch.qubit == u;
