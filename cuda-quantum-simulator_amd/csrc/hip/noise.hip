@@ -406,6 +406,7 @@ void launch_noise(double2* st, int n, int type, int qubit, double p, uint64_t se
 // ---------------------------------------------------------------------------------------
 constexpr int kGnTile = 12;
 constexpr int kGnMaxPrefix = 12;
+constexpr int kGnListCap = 128;  // flips per channel per tile kept as a list (p = 0.01: ~20)
 struct GnArgs {
     double2* st;
     int n;
@@ -423,7 +424,9 @@ __device__ __forceinline__ int gn_local_pos(int q, int u) { return q <= 10 ? q :
 
 __global__ __launch_bounds__(256) void k_gate_noise_tile(GnArgs a) {
     __shared__ double2 v[1 << kGnTile];
-    __shared__ uint32_t codes[kGnMaxPrefix][2048 / 16];
+    __shared__ uint32_t codes[kGnMaxPrefix][2048 / 16];  // 2-bit code per pair (list overflow)
+    __shared__ uint16_t list[kGnMaxPrefix][kGnListCap];   // flips: pair << 2 | code
+    __shared__ uint32_t count[kGnMaxPrefix];
     const int t = threadIdx.x;
     // this work-group's tile: trajectory traj, the n - 12 non-tile bits from the block index
     const int nfree = a.n - kGnTile;
@@ -447,6 +450,7 @@ __global__ __launch_bounds__(256) void k_gate_noise_tile(GnArgs a) {
         v[j] = ld<true>(a.st + gidx(j));
     }
     for (int i = t; i < a.np * (2048 / 16); i += 256) codes[i / 128][i % 128] = 0u;
+    if (t < kGnMaxPrefix) count[t] = 0u;
     __syncthreads();
     // the gate
     const bool on_out = (loc & a.cm_out) == a.cm_out;
@@ -509,15 +513,28 @@ __global__ __launch_bounds__(256) void k_gate_noise_tile(GnArgs a) {
             }
             const int x = run_base + (int)(g - lo);
             atomicOr(&codes[c][x >> 4], (uint32_t)code << (2 * (x & 15)));
+            const uint32_t e = atomicAdd(&count[c], 1u);
+            if (e < (uint32_t)kGnListCap) list[c][e] = (uint16_t)((x << 2) | code);
         }
     }
     __syncthreads();
     for (int c = 0; c < a.np; ++c) {
         const int q = a.ch[c].target;
         const int pq = gn_local_pos(q, a.u);
-        for (int x = t; x < 2048; x += 256) {
-            const uint32_t code = (codes[c][x >> 4] >> (2 * (x & 15))) & 3u;
-            if (!code) continue;
+        const uint32_t nf = count[c];
+        const bool listed = nf <= (uint32_t)kGnListCap;  // (else scan the code bitmap)
+        const int lim = listed ? (int)nf : 2048;
+        for (int e = t; e < lim; e += 256) {
+            int x;
+            uint32_t code;
+            if (listed) {
+                x = list[c][e] >> 2;
+                code = list[c][e] & 3u;
+            } else {
+                x = e;
+                code = (codes[c][x >> 4] >> (2 * (x & 15))) & 3u;
+                if (!code) continue;
+            }
             int j0;
             if (pq == 11) {
                 j0 = x;
