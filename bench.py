@@ -39,6 +39,32 @@ METRIC = "gates/s + achieved HBM GB/s (% peak), 100-gate H+CNOT circuit @ n qubi
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
 
+PROFILE_REGION = ["none"]
+
+
+class region:
+    """roctxProfilerResume(0) / roctxProfilerPause(0) around a timed region when --profile-region
+    names it (rocprofv3 --selected-regions records nothing outside); a no-op otherwise (the roctx
+    library is loaded only then)."""
+    _lib = None
+
+    def __init__(self, name):
+        self.on = PROFILE_REGION[0] == name
+
+    def __enter__(self):
+        if self.on:
+            if region._lib is None:
+                import ctypes
+                region._lib = ctypes.CDLL("librocprofiler-sdk-roctx.so.1")
+            region._lib.roctxProfilerResume(0)
+        return self
+
+    def __exit__(self, *exc):
+        if self.on:
+            region._lib.roctxProfilerPause(0)
+        return False
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -82,7 +108,13 @@ def parse():
                         "per rank and step, barriers and max-over-ranks timing (CPU tests)")
     p.add_argument("--pmc-json", default=None,
                    help="per-launch HBM traffic measured by rocprofv3 --pmc (see profiles/)")
+    p.add_argument("--profile-region", default="none",
+                   choices=["none", "hc", "1q28", "batch16ref", "noisy26", "dm14"],
+                   help="bracket that timed region (only) with roctxProfilerResume / Pause, for "
+                        "rocprofv3 --selected-regions: the profile then holds exactly the launches "
+                        "the line's roofline averages (scripts/roofline_check.py recomputes it)")
     a = p.parse_args()
+    PROFILE_REGION[0] = a.profile_region
     if a.qubits is None:
         a.qubits = {"batch": 16, "dm": 14, "noisy": 26}.get(a.workload, 30)
     return a
@@ -183,20 +215,23 @@ def run_single(args):
     sim.synchronize()
     sim.state.profileReset()
     sim.synchronize()
-    # Per-launch HIP events cost ~5 us per launch (a 20-qubit pass is ~15 us), so only the last
-    # tenth of the timed steps (at least one) carries them; the kernel averages come from those.
+    # Per-launch HIP events cost ~5 us per launch: negligible against a pass of >= 24 qubits
+    # (0.08 ms and up), so there every timed step carries them and the roofline averages exactly
+    # the launches a --profile-region hc profile records; below 24 qubits (a 20-qubit pass is
+    # ~15 us) only the last tenth of the timed steps (at least one) does.
     # Every step is synchronised and timed on its own (the median of >= 10 steps);
     # at 30 qubits a step is ~25 ms, the per-step synchronisation ~20 us.
-    prof_from = args.steps - max(1, args.steps // 10)
+    prof_from = 0 if n >= 24 else args.steps - max(1, args.steps // 10)
     step_s = []
     t0 = time.perf_counter()
-    for i in range(args.steps):
-        if i == prof_from:
-            sim.state.profile(True)
-        ts = time.perf_counter()
-        sim.run(circuit)
-        sim.synchronize()
-        step_s.append(time.perf_counter() - ts)
+    with region("hc"):
+        for i in range(args.steps):
+            if i == prof_from:
+                sim.state.profile(True)
+            ts = time.perf_counter()
+            sim.run(circuit)
+            sim.synchronize()
+            step_s.append(time.perf_counter() - ts)
     t1 = time.perf_counter()
     stats = sim.state.profileStats()
     sim.state.profile(False)
@@ -473,8 +508,9 @@ def measure_dm(q, n, steps, warmup, jit, seed, depth, p_noise):
         sim.reset()
         sv.synchronize()
         t0 = time.perf_counter()
-        sim.run(c)
-        sv.synchronize()
+        with region("dm14" if n == 14 else "-"):
+            sim.run(c)
+            sv.synchronize()
         ts.append(time.perf_counter() - t0)
     stats = sv.profileStats()
     sv.profile(False)
@@ -509,8 +545,9 @@ def measure_noisy(q, n, steps, warmup, seed, depth, p_noise):
         sim.reset()
         sim.synchronize()
         t0 = time.perf_counter()
-        sim.run(c)
-        sim.synchronize()
+        with region("noisy26" if n == 26 else "-"):
+            sim.run(c)
+            sim.synchronize()
         ts.append(time.perf_counter() - t0)
     stats = sv.profileStats()
     sv.profile(False)
@@ -538,9 +575,10 @@ def roofline_1q28(q, steps=3):
     sim.state.profile(True)
     sim.state.profileReset()
     t0 = time.perf_counter()
-    for _ in range(steps):
-        sim.run(c)
-    sim.synchronize()
+    with region("1q28"):
+        for _ in range(steps):
+            sim.run(c)
+        sim.synchronize()
     wall = time.perf_counter() - t0
     stats = sim.state.profileStats()
     sim.state.profile(False)
@@ -588,9 +626,10 @@ def measure_batch(q, n, B, steps, warmup, jit, seed, depth, p_noise, process, pm
     sim.synchronize()
     sim.profile(True)
     t0 = time.perf_counter()
-    for _ in range(steps):
-        sim.run(circuit)
-    sim.synchronize()
+    with region("batch16ref" if process == "reference" and n == 16 and B == 1024 else "-"):
+        for _ in range(steps):
+            sim.run(circuit)
+        sim.synchronize()
     wall = time.perf_counter() - t0
     stats = sim.profileStats()
     sim.profile(False)

@@ -318,6 +318,30 @@ static bool ensure_noise_buffers(qsim_state* s, size_t nch) {
     return true;
 }
 
+// After a pulled noisy run: free the second buffer (unless a relayout plan owns it) and the
+// code words when the device no longer has room for another 2^n buffer beside a margin.
+static void trim_noise_buffers(qsim_state* s) {
+    static const int keep = [] {  // QSIM_NOISE_KEEP_BUFFERS: 1 always keep, 0 always free (tests)
+        const char* e = std::getenv("QSIM_NOISE_KEEP_BUFFERS");
+        return e ? std::atoi(e) : -1;
+    }();
+    if (keep == 1) return;
+    if (keep != 0) {
+        size_t free_b = 0, total_b = 0;
+        if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) {
+            (void)hipGetLastError();
+            free_b = 0;
+        }
+        if (free_b >= (sizeof(double2) << s->n) + kAltMarginBytes) return;
+    }
+    QSIM_HIPCHK(hipStreamSynchronize(s->stream));
+    if (s->noise_stream) QSIM_HIPCHK(hipStreamSynchronize(s->noise_stream));
+    if (s->noise_codes) (void)hipFree(s->noise_codes);
+    s->noise_codes = nullptr;
+    s->noise_codes_cap = 0;
+    if (!s->relayout) release_alt(s);
+}
+
 // One fused plan on the state: relayout passes alternate between the state's two buffers.
 static void launch_plan(qsim_state* s, const Plan& plan, Timer* tm, const JitModule* jm) {
     FusedRange range;
@@ -946,7 +970,12 @@ int qsim_run(qsim_state* s, const qsim_gate* gates, size_t count, int flags) {
         };
         // First run on a basis state: choose the qubit labels (and, with cross-height calibration,
         // the tile height) for fewer passes and faster pass layouts (relabel.hip: choose_layout).
-        if ((flags & QSIM_RUN_FUSED) && s->basis && s->perm.empty() && count > 0 &&
+        // A state whose raw device pointer was handed out (devicePtr) is never relabeled: the
+        // pointer must always see the canonical amplitudes (reference include/StateVector.cuh:
+        // devicePtr() is the state itself), and a relabeled run would leave them qubit-permuted
+        // there until the next index-based reader.  So pinned states run the identity layout in
+        // place (no relayout plan, no second buffer, no copy-back).
+        if ((flags & QSIM_RUN_FUSED) && !s->pinned && s->basis && s->perm.empty() && count > 0 &&
             (relabel_enabled(s->n) || (relayout_enabled(s->n) && relabel_mode_on() && !tile_height_is_set()))) {
             choose_first_layout(s, gates, count);
             if (!s->perm.empty() && s->basis_idx) {  // relabel the basis state itself
@@ -1421,6 +1450,9 @@ int qsim_noisy_run(qsim_state* s, const qsim_gate* gates, size_t count,
         std::vector<NoiseChan> chans;
         for (size_t c = 0; c < n_channels; ++c)
             chans.push_back(NoiseChan{channels[c].type, channels[c].qubit, channels[c].probability});
+        // where the amplitudes are now: a pinned state's handed-out pointer (prep() leaves the
+        // amplitudes of a pinned state in the buffer that was handed out, which may be either one)
+        double2* const home = s->d;
         if (pull_noise_supported(s->n, chans, true) && ensure_noise_buffers(s, chans.size())) {
             // Flip channels only: the noise after gate i is applied by gate i+1's pass (out of
             // place), the noise after the last gate by one identity pass (noise.hip); the same
@@ -1459,13 +1491,18 @@ int qsim_noisy_run(qsim_state* s, const qsim_gate* gates, size_t count,
                     map(i + 2);
                 }
             }
-            if (s->pinned && s->d != s->base_d) {  // keep the amplitudes where the handed-out pointer points
-                QSIM_HIPCHK(hipMemcpyAsync(s->base_d, s->d, sizeof(double2) << s->n, hipMemcpyDeviceToDevice,
+            if (s->pinned && s->d != home) {  // keep the amplitudes where the handed-out pointer points
+                QSIM_HIPCHK(hipMemcpyAsync(home, s->d, sizeof(double2) << s->n, hipMemcpyDeviceToDevice,
                                            s->stream));
                 s->alt = s->d;
-                s->d = s->base_d;
+                s->d = home;
             }
-            return;  // (the second buffer stays for the next run: qsim_state_memory_bytes counts it)
+            // The second buffer and the code words stay for the next run (qsim_state_memory_bytes
+            // counts them) only while the device keeps room for another state of this size beside
+            // them; otherwise they are freed now, so a later StateVector does not fail where the
+            // reference's single-buffer one would not.
+            trim_noise_buffers(s);
+            return;
         }
         for (const Op& op : ops) {
             launch_op(s->d, s->n, 1, op, s->stream, &s->timer);

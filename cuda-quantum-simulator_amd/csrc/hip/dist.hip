@@ -61,6 +61,12 @@ struct DStep {
 
 constexpr int kMaxPivots = 4;
 constexpr int kMaxParts = 1 << kMaxPivots;  // part-exchanges of one overlapped remap
+// QSIM_DIST_CARRY=1 (experimental, off by default; read per call so tests can switch it): a run's
+// last step is left pending and merged into the next run's first step (qsim_dist_run).
+bool carry_enabled() {
+    const char* e = std::getenv("QSIM_DIST_CARRY");
+    return e != nullptr && std::atoi(e) != 0;
+}
 static bool pass_avoids(const FusedPass& p, uint64_t pmask) {
     if (p.single >= 0 || p.h < 4) return false;
     for (int i = 0; i < 6 + p.h - p.r0; ++i)
@@ -500,11 +506,7 @@ static std::vector<DStep> plan_dist(const qsim_gate* gates, size_t count, int n,
     // the next run's first ops step (rank 0's lowering, from this run's end map: the same on every
     // rank), for scoring the last remap's pivots by the passes it can carry
     std::vector<Op> next_ops;
-    static const bool carry_on = [] {  // (off by default: see qsim_dist_run)
-        const char* e = std::getenv("QSIM_DIST_CARRY");
-        return e != nullptr && std::atoi(e) != 0;
-    }();
-    if (carry_on && overlap && L >= 8) {
+    if (carry_enabled() && overlap && L >= 8) {
         std::vector<int> pn = perm;
         const std::vector<DStep> nxt = plan_dist_core(gates, count, n, g, 0, pn);
         if (!nxt.empty() && nxt[0].kind == 0) next_ops = nxt[0].ops;
@@ -1073,8 +1075,17 @@ void exchange(qsim_dist* d, const DStep& ex, const std::vector<char>& fused) {
 // each part waiting for its local work (event pev[j], recorded on the compute stream after the
 // role-1 step's part) and signalling pev[3 kMaxParts + j] when unpacked (the role-2 step's part waits for
 // it).  Part j uses part j of the send / receive buffers, so all parts can be in flight.
+// Part count of an overlapped remap with pivot mask pmask; the event array pev holds kMaxParts
+// slots per kind, so a larger count is a planner bug, reported instead of overrunning it (round 4:
+// a segfault when the pivot limit rose to 4 while pev still had 8 slots per kind).
+int part_count(uint64_t pmask) {
+    const int m = __builtin_popcountll(pmask);
+    if (m > kMaxPivots) fail(QSIM_ERR_RUNTIME, "overlapped remap with " + std::to_string(m) + " pivots (at most " +
+                                                   std::to_string(kMaxPivots) + ")");
+    return 1 << m;
+}
 void exchange_parts(qsim_dist* d, const DStep& ex, const std::vector<char>& fused) {
-    const int K = 1 << __builtin_popcountll(ex.pmask);
+    const int K = part_count(ex.pmask);
     const uint64_t part_amps = 1ull << (d->L - __builtin_popcountll(ex.pmask));
     const uint64_t chunk = part_amps >> ex.k;
     const double bytes = 2.0 * 16.0 * (double)(part_amps - chunk) * (double)d->shards.size();
@@ -1219,15 +1230,20 @@ Op map_op_positions(Op op, const std::vector<int>& sg) {
 // the slab layout, B's planned on positions sigma(p) (the receive buffer's layout) with its last
 // pass storing back to the standard positions.  The slab layout is the unfused exchange's, so
 // shards decide independently.
+// The variants are built the first time a run of this plan may use them (fused mode, fused pack
+// on); whether a run uses them is decided per run from its own flags (fused_now), so a per-gate
+// run of a cached plan never runs them and a fused run after a per-gate one still gets them.
+bool fused_now(int flags) {
+    return (flags & QSIM_RUN_FUSED) && fused_pack_enabled();
+}
 void decide_fused(qsim_dist* d, qsim_dist::RunPlan& rp, int flags) {
-    if (rp.fused_decided) return;
-    rp.fused_decided = true;
     const size_t S = d->shards.size();
     rp.fpack.resize(S);
     rp.funpack.resize(S);
+    if (rp.fused_decided || !fused_now(flags)) return;
+    rp.fused_decided = true;
     const std::vector<DStep>& st0 = rp.steps[0];
-    if (!(flags & QSIM_RUN_FUSED) || !fused_pack_enabled() || st0.size() < 3 || st0[0].kind != 0 ||
-        st0[1].kind != 1 || st0[2].kind != 0 || (st0[2].role & 1))
+    if (st0.size() < 3 || st0[0].kind != 0 || st0[1].kind != 1 || st0[2].kind != 0 || (st0[2].role & 1))
         return;
     const DStep& ex = st0[1];
     if (ex.pmask & 0x3full) return;  // (pivots are >= 6 by construction)
@@ -1312,6 +1328,7 @@ qsim_dist::RunPlan& run_plan(qsim_dist* d, const qsim_gate* gates, size_t count,
 void flush_carry(qsim_dist* d) {
     qsim_dist::Carry& c = d->carry;
     if (!c.active) return;
+    if (c.parts > kMaxParts) fail(QSIM_ERR_RUNTIME, "carried remap with too many parts");
     for (int h = 0; h < c.parts; ++h) {
         QSIM_HIPCHK(hipStreamWaitEvent(d->stream, d->pev[3 * kMaxParts + h], 0));
         for (size_t i = 0; i < d->shards.size(); ++i)
@@ -1534,10 +1551,7 @@ int qsim_dist_run(qsim_dist* d, const qsim_gate* gates, size_t count, int flags)
         }
         d->fresh = false;
         d->sent_bytes = 0.0;
-        static const bool carry_on = [] {  // QSIM_DIST_CARRY=1: carry the last step into the next run
-            const char* e = std::getenv("QSIM_DIST_CARRY");
-            return e != nullptr && std::atoi(e) != 0;
-        }();
+        const bool carry_on = carry_enabled();
         if (!(flags & QSIM_RUN_FUSED) || !carry_on) flush_carry(d);
         const uint64_t carry_in = d->carry.active ? d->carry.pmask : 0ull;
         qsim_dist::RunPlan& rp = run_plan(d, gates, count, carry_in);
@@ -1552,7 +1566,7 @@ int qsim_dist_run(qsim_dist* d, const qsim_gate* gates, size_t count, int flags)
         d->fused_remaps = 0;
         decide_fused(d, rp, flags);
         std::vector<char> fused(S, 0);  // per shard: the first exchange runs fused
-        for (size_t i = 0; i < S; ++i) fused[i] = rp.fpack[i] && rp.fpack[i]->ok;
+        for (size_t i = 0; i < S; ++i) fused[i] = fused_now(flags) && rp.fpack[i] && rp.fpack[i]->ok;
         const std::vector<char> unfused(S, 0);
         static const bool dbg = std::getenv("QSIM_DIST_DEBUG") != nullptr;
         if (dbg) {  // the exchange skeleton this run executes (kind, k, pivot mask, role)
@@ -1567,6 +1581,7 @@ int qsim_dist_run(qsim_dist* d, const qsim_gate* gates, size_t count, int flags)
         int pending = merge ? d->carry.parts : 0;  // parts of an overlapped remap still to be waited for
         if (merge) ++d->carried;
         auto wait_pending = [&]() {
+            if (pending > kMaxParts) fail(QSIM_ERR_RUNTIME, "pending remap with too many parts");
             for (int h = 0; h < pending; ++h) QSIM_HIPCHK(hipStreamWaitEvent(d->stream, d->pev[3 * kMaxParts + h], 0));
             pending = 0;
         };
@@ -1583,7 +1598,7 @@ int qsim_dist_run(qsim_dist* d, const qsim_gate* gates, size_t count, int flags)
                 if (s0.pmask) {
                     // the ops step before (role bit 1) recorded pev[j] after its tail part j;
                     // otherwise every part is ready now
-                    const int K = 1 << __builtin_popcountll(s0.pmask);
+                    const int K = part_count(s0.pmask);
                     wait_pending();
                     if (k == 0 || !(plans[0][k - 1].role & 1))
                         for (int h = 0; h < K; ++h) QSIM_HIPCHK(hipEventRecord(d->pev[h], d->stream));
@@ -1645,6 +1660,7 @@ int qsim_dist_run(qsim_dist* d, const qsim_gate* gates, size_t count, int flags)
             }
             if (head) {
                 const bool carried = k == 0 && merge;
+                if (pending > kMaxParts) fail(QSIM_ERR_RUNTIME, "pending remap with too many parts");
                 for (int h = 0; h < pending; ++h) {
                     QSIM_HIPCHK(hipStreamWaitEvent(d->stream, d->pev[3 * kMaxParts + h], 0));
                     if (carried) {  // part h of the previous run's last step, then part h of this one
@@ -1673,7 +1689,7 @@ int qsim_dist_run(qsim_dist* d, const qsim_gate* gates, size_t count, int flags)
                 else run_part(d, d->shards[i], plans[i][k].ops, runs[i], 0, 1);  // per-gate: the whole list
             }
             if (pa) {  // the exchange after waits for pev[h]
-                for (int h = 0; h < (1 << __builtin_popcountll(pa)); ++h) {
+                for (int h = 0, K = part_count(pa); h < K; ++h) {
                     for (size_t i = 0; i < S; ++i)
                         if (runs[i].plan)
                             run_part(d, d->shards[i], plans[i][k].ops, runs[i], runs[i].j2, runs[i].np, pa, h, homes[i],
@@ -1699,6 +1715,14 @@ int qsim_dist_fused_remaps(qsim_dist* d, int* remaps) {
         need(d);
         if (!remaps) fail(QSIM_ERR_INVALID_ARGUMENT, "null out");
         *remaps = d->fused_remaps;
+    });
+}
+
+int qsim_dist_carried_runs(qsim_dist* d, int* runs) {
+    return dguard([&] {
+        need(d);
+        if (!runs) fail(QSIM_ERR_INVALID_ARGUMENT, "null out");
+        *runs = d->carried;
     });
 }
 

@@ -196,6 +196,7 @@ _sig(hip, "qsim_dist_run", [_P, POINTER(qsim_gate), c_size_t, c_int])
 _sig(hip, "qsim_dist_sync", [_P])
 _sig(hip, "qsim_dist_overlapped", [_P, POINTER(c_int)])
 _sig(hip, "qsim_dist_fused_remaps", [_P, POINTER(c_int)])
+_sig(hip, "qsim_dist_carried_runs", [_P, POINTER(c_int)])
 _sig(hip, "qsim_dist_remap_bytes", [_P, POINTER(c_double)])
 _sig(hip, "qsim_dist_plan_memo_clear", [])
 _sig(hip, "qsim_dist_slab_map", [c_int, c_int, c_int, POINTER(qsim_dist_step), c_int, POINTER(c_int32),

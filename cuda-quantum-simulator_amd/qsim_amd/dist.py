@@ -116,6 +116,12 @@ class DistributedSimulator:
         v = _c.c_int(0)
         _lib.check(_lib.hip.qsim_dist_overlapped(self._h, _c.byref(v)))
         return v.value
+    def carriedRuns(self) -> int:
+        """Runs whose first step merged the previous run's carried last step (QSIM_DIST_CARRY=1,
+        experimental)."""
+        v = _c.c_int(0)
+        _lib.check(_lib.hip.qsim_dist_carried_runs(self._h, _c.byref(v)))
+        return v.value
     def fusedRemaps(self) -> int:
         """Exchanges of the last run whose pack / unpack ran inside the local passes (the pass
         before stored into the slab layout, the step after loaded from it), summed over shards."""

@@ -426,6 +426,9 @@ int qsim_dist_destroy(qsim_dist* d);
 int qsim_dist_run(qsim_dist* d, const qsim_gate* gates, size_t count, int flags);
 int qsim_dist_sync(qsim_dist* d);
 int qsim_dist_overlapped(qsim_dist* d, int* remaps); /* remaps of the last run that overlapped local work */
+/* Runs of this object whose first step merged the previous run's carried last step (the
+ * EXPERIMENTAL cross-run overlap, QSIM_DIST_CARRY=1, off by default; read per run). */
+int qsim_dist_carried_runs(qsim_dist* d, int* runs);
 int qsim_dist_remap_bytes(qsim_dist* d, double* sent); /* bytes this rank sent in its last run's remaps */
 int qsim_dist_reset(qsim_dist* d);                         /* |0..0>, identity qubit map */
 int qsim_dist_perm(qsim_dist* d, int32_t* perm);            /* logical -> physical, n entries */

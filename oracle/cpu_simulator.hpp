@@ -56,10 +56,17 @@ public:
             apply(static_cast<int>(g.type), g.qubits.data(), (int)g.qubits.size(), g.parameter);
     }
 
-    void apply(int type, const int* q, int nq, double theta) {
-        if (nq == 1) one(type, q[0], theta);
-        else if (nq == 2) two(type, q[0], q[1], theta);
-        else if (nq == 3 && mode_ == Mode::GpuSemantics && type == Toffoli) toffoli(q[0], q[1], q[2]);
+    void apply(int type, const int* q, int nq, double theta) { apply_range(type, q, nq, theta, 0, loop_size(nq)); }
+
+    // The gate's loop (pairs for one-qubit gates, indices otherwise) restricted to [begin, end).
+    // Every iteration writes only the amplitudes of its own pair (two- and three-qubit gates act
+    // from the pair's lower member only), so disjoint ranges may run on different threads and
+    // produce exactly the single-threaded result (same operations per amplitude).
+    size_t loop_size(int nq) const { return nq == 1 ? size_ >> 1 : size_; }
+    void apply_range(int type, const int* q, int nq, double theta, size_t begin, size_t end) {
+        if (nq == 1) one(type, q[0], theta, begin, end);
+        else if (nq == 2) two(type, q[0], q[1], theta, begin, end);
+        else if (nq == 3 && mode_ == Mode::GpuSemantics && type == Toffoli) toffoli(q[0], q[1], q[2], begin, end);
     }
 
     const std::vector<cplx>& getStateVector() const { return state_; }
@@ -101,11 +108,11 @@ private:
     Mode mode_;
     std::vector<cplx> state_;
 
-    void one(int type, int t, double theta) {
+    void one(int type, int t, double theta, size_t begin, size_t end) {
         const double r = 0.70710678118654752440;  // constants::INV_SQRT2
-        const size_t pairs = size_ >> 1, low = (size_t(1) << t) - 1;
+        const size_t low = (size_t(1) << t) - 1;
         const double c = std::cos(theta / 2.0), s = std::sin(theta / 2.0);
-        for (size_t p = 0; p < pairs; ++p) {
+        for (size_t p = begin; p < end; ++p) {
             const size_t i0 = (p & low) | ((p & ~low) << 1), i1 = i0 | (size_t(1) << t);
             const cplx a0 = state_[i0], a1 = state_[i1];
             switch (type) {
@@ -125,10 +132,10 @@ private:
         }
     }
 
-    void two(int type, int q1, int q2, double theta) {
+    void two(int type, int q1, int q2, double theta, size_t begin, size_t end) {
         const double c = std::cos(theta / 2.0), s = std::sin(theta / 2.0);
         const size_t m1 = size_t(1) << q1, m2 = size_t(1) << q2;
-        for (size_t i = 0; i < size_; ++i) {
+        for (size_t i = begin; i < end; ++i) {
             const bool b1 = i & m1, b2 = i & m2;
             switch (type) {
                 case CNOT:
@@ -156,9 +163,9 @@ private:
         }
     }
 
-    void toffoli(int c1, int c2, int t) {  // Gates.cu:392-410
+    void toffoli(int c1, int c2, int t, size_t begin, size_t end) {  // Gates.cu:392-410
         const size_t a = size_t(1) << c1, b = size_t(1) << c2, m = size_t(1) << t;
-        for (size_t i = 0; i < size_; ++i)
+        for (size_t i = begin; i < end; ++i)
             if ((i & a) && (i & b) && !(i & m)) std::swap(state_[i], state_[i ^ m]);
     }
 };

@@ -2,6 +2,7 @@
 // Test infrastructure only; see cpu_simulator.hpp.
 #include <chrono>
 #include <cstring>
+#include <thread>
 
 #include "cpu_simulator.hpp"
 #include "qsim_hip.h"
@@ -20,6 +21,29 @@ int qsim_oracle_run(int n, const qsim_gate* gates, size_t count, int strict_cpu,
     if (init_from_state) std::memcpy((void*)sim.mutableState().data(), state, N * 2 * sizeof(double));
     for (size_t i = 0; i < count; ++i)
         sim.apply(gates[i].type, gates[i].qubits, gates[i].nqubits, gates[i].parameter);
+    std::memcpy(state, sim.getStateVector().data(), N * 2 * sizeof(double));
+    return QSIM_OK;
+}
+
+// As qsim_oracle_run with each gate's loop split over `threads` threads (disjoint pair ranges,
+// joined before the next gate): the same result bit for bit, for the large-n parity tests.
+int qsim_oracle_run_mt(int n, const qsim_gate* gates, size_t count, int strict_cpu, int init_from_state,
+                       double* state, int threads) {
+    if (n < 1 || n > 30 || threads < 1) return QSIM_ERR_INVALID_ARGUMENT;
+    CPUSimulator sim(n, strict_cpu ? Mode::StrictCpu : Mode::GpuSemantics);
+    const size_t N = size_t(1) << n;
+    if (init_from_state) std::memcpy((void*)sim.mutableState().data(), state, N * 2 * sizeof(double));
+    for (size_t i = 0; i < count; ++i) {
+        const qsim_gate& g = gates[i];
+        const size_t L = sim.loop_size(g.nqubits);
+        const size_t T = std::min<size_t>((size_t)threads, std::max<size_t>(1, L >> 12));
+        std::vector<std::thread> th;
+        for (size_t t = 0; t < T; ++t)
+            th.emplace_back([&, t] {
+                sim.apply_range(g.type, g.qubits, g.nqubits, g.parameter, L * t / T, L * (t + 1) / T);
+            });
+        for (std::thread& x : th) x.join();
+    }
     std::memcpy(state, sim.getStateVector().data(), N * 2 * sizeof(double));
     return QSIM_OK;
 }

@@ -214,3 +214,36 @@ def test_fused_remap_equals_pack_unpack(qsim, oracle, gpu_ready, monkeypatch, n,
     ref = oracle.run_cpu(n, g + g)
     assert np.max(np.abs(out["1"] - ref)) < 1e-12
     assert np.max(np.abs(out["0"] - ref)) < 1e-12
+
+
+@pytest.mark.parametrize("world,n", [(8, 20), (4, 21)])
+def test_cross_run_carry_matches_oracle(qsim, oracle, gpu_ready, monkeypatch, world, n):
+    """the experimental cross-run carry (QSIM_DIST_CARRY=1: a run's last step is
+    left pending and merged into the next run's first step).  Three runs of one circuit, with
+    readers (probability, gather) and a reset in between — every state-touching entry must flush
+    the pending step first — against the oracle at 1e-12, and the merge must have happened."""
+    from qsim_amd.dist import DistributedSimulator
+    monkeypatch.setenv("QSIM_DIST_CARRY", "1")
+    c = qsim.createRandomHCCircuit(n, 100, 42)
+    g = oracle.gates_of(c)
+    d = DistributedSimulator.virtual(n, world)
+    merged = 0
+    for _ in range(3):
+        d.run(c)
+        merged += d.carriedRuns() > 0
+    np.testing.assert_allclose(d.getStateVector(), oracle.run_cpu(n, g * 3), atol=1e-12, rtol=0)
+    d.run(c)  # (carry pending again) then a reader
+    assert abs(d.getTotalProbability() - 1.0) < 1e-12
+    d.run(c)
+    ref5 = oracle.run_cpu(n, g * 5)
+    p = np.abs(ref5) ** 2
+    mask = ((np.arange(1 << n) >> (n - 1)) & 1) == 0
+    assert abs(d.probBitZero(n - 1) - p[mask].sum()) < 1e-12
+    np.testing.assert_allclose(d.getStateVector(), ref5, atol=1e-12, rtol=0)
+    d.run(c)
+    d.reset()  # flushes, then |0..0>
+    s = d.getStateVector()
+    assert abs(s[0] - 1) < 1e-15 and np.all(np.abs(s[1:]) == 0)
+    d.run(c)
+    np.testing.assert_allclose(d.getStateVector(), oracle.run_cpu(n, g), atol=1e-12, rtol=0)
+    assert d.carriedRuns() >= 1 or merged >= 1, "the carry never merged"

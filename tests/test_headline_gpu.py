@@ -14,7 +14,7 @@ relayouts (its kernels are oracle-checked gate by gate in test_parity_gpu.py):
   * after ONE run (the first run: calibration, then the chosen plan) and after TWO runs (the
     second starts from the layout the first ends in: the bench's timed steady state).
 Also: config 3 (28 qubits, its calibrated plan), W-HC seed 2 under its 5-pass relayout plan, a
-relayout run on a state whose raw device pointer was handed out (the copy-back branch), and the
+state whose raw device pointer was handed out (never relabeled: the pointer stays canonical), and the
 fallback when the relayout plan's second buffer does not fit in device memory.
 """
 import ctypes
@@ -111,25 +111,42 @@ def test_w_hc_30q_headline_path_round_trip(qsim, gpu_ready, jit2):
     assert abs(sim.state.getTotalProbability() - 1.0) < 1e-10
 
 
-def test_relayout_on_a_pinned_state_copies_back(qsim, oracle, gpu_ready):
-    """devicePtr() handed out before a relayout run: the result must be where the pointer points
-    (capi.hip launch_plan copies it back), and the raw kernel entry on that pointer acts on it."""
+def _read_device(ptr, n):
+    """The 2^n amplitudes at a raw device pointer (D2H through the loaded HIP runtime)."""
+    hip = _hip()
+    out = np.empty(1 << n, dtype=np.complex128)
+    assert hip.hipDeviceSynchronize() == 0
+    assert hip.hipMemcpy(out.ctypes.data, ctypes.c_void_p(ptr), out.nbytes, 2) == 0  # D2H
+    return out
+
+
+def test_pinned_state_is_never_relabeled(qsim, oracle, gpu_ready):
+    """a pointer from devicePtr() held across a basis-state fused run (relayout
+    forced, so an unpinned state would be relabeled) sees the canonical state without calling
+    devicePtr() again (reference include/StateVector.cuh:66-124: devicePtr() is the state), and the
+    raw kernel entry on it acts on the right qubit.  Pinned states run the identity layout in place
+    (capi.hip qsim_run), so no second buffer and no copy-back either."""
     from qsim_amd import _lib
     from qsim_amd.plan import set_jit, set_relayout
-    set_relayout(2, 20)  # forced relayout plan at 22 qubits
+    set_relayout(2, 20)  # forced relayout plan at 22 qubits (taken by an unpinned state)
     set_jit(0, -1)       # (the interpreter: no compile wait)
     n = 22
     c = qsim.createRandomHCCircuit(n, 100, 42)
+    ref = oracle.run_cpu(n, oracle.gates_of(c))
+    free = qsim.StateVector(n)  # control: the same run unpinned takes the relayout plan
+    free.run(c, qsim.RunMode.Fused)
+    assert free.layoutInfo()["relayout"] and free.layoutInfo()["relabeled"]
+    assert float(np.max(np.abs(free.toHost() - ref))) < 1e-12
+    free.close()
     sv = qsim.StateVector(n)
     ptr = sv.devicePtr()
-    sv.initializeZero()  # (a basis state again, pointer still out: its first run chooses relayout)
+    sv.initializeZero()  # (a basis state again, pointer still out)
     sv.run(c, qsim.RunMode.Fused)
-    assert sv.layoutInfo()["relayout"]
-    ref = oracle.run_cpu(n, oracle.gates_of(c))
-    assert sv.devicePtr() == ptr  # (restores the identity layout into the same buffer)
-    got = sv.toHost()
-    assert float(np.max(np.abs(got - ref))) < 1e-12
-    # the raw entry on the handed-out pointer, on the state's stream
+    info = sv.layoutInfo()
+    assert not info["relayout"] and not info["relabeled"], info
+    assert sv.getDeviceMemoryBytes() < 2 * (16 << n)  # one 2^n buffer
+    assert float(np.max(np.abs(_read_device(ptr, n) - ref))) < 1e-12  # no devicePtr() call before
+    # the raw entry on the held pointer, on the state's stream
     _lib.check(_lib.hip.qsim_apply_hadamard_optimized(ctypes.c_void_p(ptr), n, 17,
                                                       ctypes.c_void_p(sv.stream())))
     sv.synchronize()
@@ -137,17 +154,15 @@ def test_relayout_on_a_pinned_state_copies_back(qsim, oracle, gpu_ready):
     h.h(17)
     ref2 = oracle.run_cpu(n, oracle.gates_of(h), state=ref)
     assert float(np.max(np.abs(sv.toHost() - ref2))) < 1e-12
-    # a run from that (non-basis) state: identity labels, in place
+    # a run from that (non-basis) state, then back to |0..0> and the memoised decision: still in place
     sv.run(c, qsim.RunMode.Fused)
     ref3 = oracle.run_cpu(n, oracle.gates_of(c), state=ref2)
-    assert sv.devicePtr() == ptr
-    assert float(np.max(np.abs(sv.toHost() - ref3))) < 1e-12
-    # back to |0..0>: the memoised relayout plan, still pinned
+    assert float(np.max(np.abs(_read_device(ptr, n) - ref3))) < 1e-12
     sv.initializeZero()
     sv.run(c, qsim.RunMode.Fused)
-    assert sv.layoutInfo()["relayout"]
+    assert not sv.layoutInfo()["relabeled"]
+    assert float(np.max(np.abs(_read_device(ptr, n) - ref))) < 1e-12
     assert sv.devicePtr() == ptr
-    assert float(np.max(np.abs(sv.toHost() - ref))) < 1e-12
 
 
 def _hip():
@@ -155,6 +170,8 @@ def _hip():
     lib.hipMalloc.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t]
     lib.hipFree.argtypes = [ctypes.c_void_p]
     lib.hipMemGetInfo.argtypes = [ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(ctypes.c_size_t)]
+    lib.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    lib.hipDeviceSynchronize.argtypes = []
     return lib
 
 

@@ -167,3 +167,47 @@ def test_pulled_flip_noise_matches_oracle(qsim, oracle, gpu_ready, monkeypatch, 
     sim.run(c)
     want2, _ = oracle.noisy_run(n, oracle.gates_of(c), channels, 2000 + seed, ctr, want)
     np.testing.assert_allclose(sim.getStateVector(), want2, atol=1e-12, rtol=0)
+
+
+def _read_device(ptr, n):
+    """The 2^n complex amplitudes at a raw device pointer (hipMemcpy D2H via the loaded runtime)."""
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so.7")
+    hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    hip.hipDeviceSynchronize.argtypes = []
+    out = np.empty(1 << n, dtype=np.complex128)
+    assert hip.hipDeviceSynchronize() == 0
+    assert hip.hipMemcpy(out.ctypes.data, ctypes.c_void_p(ptr), out.nbytes, 2) == 0  # D2H
+    return out
+
+
+@pytest.mark.parametrize("keep", ["1", "0"])
+def test_pulled_noise_on_a_pinned_pointer(qsim, oracle, gpu_ready, monkeypatch, keep):
+    """an unpinned pulled run with an odd gate count leaves the amplitudes in
+    the second buffer; devicePtr() then hands that buffer out.  The next pulled runs must leave
+    their result where that pointer points (odd and even gate counts), never free it, and the
+    pointer must equal getStateVector and the oracle.  keep=0 frees the noise buffers after every
+    run (the low-memory branch), keep=1 keeps them."""
+    monkeypatch.setenv("QSIM_NOISE_KEEP_BUFFERS", keep)
+    n, seed = 12, 9
+    channels = [(0, q, 0.2) for q in range(n)]
+    c_odd = qsim.createRandomCircuit(n, 15, seed)
+    c_even = qsim.createRandomCircuit(n, 16, seed + 1)
+    assert len(c_odd.getGates()) % 2 == 1 and len(c_even.getGates()) % 2 == 0
+    sim = qsim.NoisySimulator(n, _model(qsim, channels))
+    sim.setSeed(77)
+    sim.run(c_odd)
+    want, ctr = oracle.noisy_run(n, oracle.gates_of(c_odd), channels, 77)
+    ptr = sim.state.devicePtr()
+    np.testing.assert_allclose(_read_device(ptr, n), want, atol=1e-12, rtol=0)
+    for c in (c_odd, c_even, c_odd):
+        sim.run(c)
+        want, ctr = oracle.noisy_run(n, oracle.gates_of(c), channels, 77, ctr, want)
+        np.testing.assert_allclose(_read_device(ptr, n), want, atol=1e-12, rtol=0)
+        np.testing.assert_allclose(sim.getStateVector(), want, atol=1e-12, rtol=0)
+    assert sim.state.devicePtr() == ptr
+    # a basis-state fused run (the path that used to release the second buffer) keeps the pointer
+    sim.state.initializeZero()
+    c = qsim.createRandomHCCircuit(n, 40, 3)
+    sim.state.run(c, qsim.RunMode.Fused)
+    np.testing.assert_allclose(_read_device(ptr, n), oracle.run_cpu(n, oracle.gates_of(c)), atol=1e-12, rtol=0)

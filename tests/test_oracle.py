@@ -106,3 +106,21 @@ def test_oracle_sampling_lower_bound(oracle):
     u = np.array([0.0, 0.25, 0.4999999, 0.5, 0.5000001, 0.99])
     out = oracle.sample_cpu(2, st, u)
     assert list(out) == [0, 0, 0, 0, 3, 3]
+
+
+@pytest.mark.parametrize("threads", [2, 7, 16])
+def test_threaded_oracle_is_bit_identical(oracle, threads):
+    """qsim_oracle_run_mt (each gate's loop split over threads, used by the 26-30 qubit GPU parity
+    tests) equals the single-threaded oracle bit for bit on every gate type, targets low and high."""
+    n = 17
+    rng = np.random.default_rng(threads)
+    gates = []
+    for _ in range(60):
+        t = int(rng.integers(0, 17))
+        ar = 1 if t <= 10 else (2 if t <= 15 else 3)
+        qs = [int(x) for x in rng.choice(n, size=ar, replace=False)]
+        gates.append((t, qs, float(rng.uniform(0, 2 * math.pi))))
+    start = oracle.run_cpu(n, [(3, [q], 0.0) for q in range(n)])
+    want = oracle.run_cpu(n, gates, state=start)
+    got = oracle.run_cpu_mt(n, gates, state=start, threads=threads)
+    assert np.array_equal(got, want)
