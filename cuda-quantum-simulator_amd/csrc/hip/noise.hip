@@ -389,24 +389,33 @@ void launch_noise(double2* st, int n, int type, int qubit, double p, uint64_t se
 
 
 // ---------------------------------------------------------------------------------------
-// Gate + in-tile noise (BatchedSimulator's reference process, the push path's fast form).
+// Gate + in-tile noise (BatchedSimulator's reference process: the default from 12 qubits).
 //
 // One gate step = the gate, then every channel entry in order.  A work-group owns a TILE of
 // 4096 amplitudes of one trajectory — qubits 0..10 plus one more, u (the gate's target when it is
-// >= 11, else 11) — holds it in LDS, applies the gate, then the longest PREFIX of the channel list
-// whose qubits lie in the tile: every such channel's flips are pairs inside the tile, so the
-// work-group walks their blocks (the push kernels' draws: blocks of 256 global pairs, geometric
-// gaps from the same counter hash), records each flip's 2-bit code per pair in LDS, and applies
-// the channels one after the other with a barrier between them.  The tile goes back in place
-// (it is this work-group's alone), and the remaining channels (the suffix) run as the one-launch
-// push kernel.  Same operations in the same order on every amplitude as gate kernel + push, so the
-// same states bit for bit; one streaming pass carries the gate and most of the noise.
-// (Needs n >= 12; W-BATCH's depolarizing-on-all-qubits list puts 11 or 12 of its 16 channels in
-// the prefix.)
+// >= 11, else 11) — and applies the gate and then the longest PREFIX of the channel list whose
+// qubits lie in the tile (every such channel's flips are pairs inside the tile).  The suffix (the
+// remaining channels) runs as the one-launch push kernel afterwards.
+//
+// The prefix's flips form a signed permutation P of the tile (X swaps a pair, Y swaps it with
+// phases -i / +i, Z negates its |1> member), so P is never applied channel by channel (round 4's
+// form: one LDS phase and barrier per channel, ~24 us per channel per launch).  Instead:
+//   1. the tile's 16 loads per thread are issued into registers;
+//   2. meanwhile the blocks of every prefix channel are walked (the push kernels' draws: blocks of
+//      256 global pairs, geometric gaps from the same counter hash), one walk per thread, and each
+//      flip's 2-bit code (1 X, 2 Y, 3 Z) is ORed into field c of the CODE WORD of both members of
+//      its pair (LDS, one 32-bit word per amplitude, 16 KiB);
+//   3. the registers go to LDS and the gate runs there;
+//   4. each output amplitude k is PULLED through P: walking its word's non-zero fields from the
+//      last channel down (X / Y move k to the pair partner and re-read the word there, keeping the
+//      fields below; Y and Z add a phase i^e), out[k] = i^e v[k'] — a zero word (~89 % of them at
+//      p = 0.01 on 12 channels) is a plain copy — and stored straight to HBM.
+// Exact: out[k] equals applying the channels in order (every step is a swap / sign change of
+// doubles), so the same states bit for bit as the gate kernel + push kernel.  Three barriers per
+// tile whatever the channel count; LDS 80 KiB (two work-groups per CU).
 // ---------------------------------------------------------------------------------------
 constexpr int kGnTile = 12;
-constexpr int kGnMaxPrefix = 12;
-constexpr int kGnListCap = 128;  // flips per channel per tile kept as a list (p = 0.01: ~20)
+constexpr int kGnMaxPrefix = 12;  // 2-bit fields of a 32-bit word (<= 16)
 struct GnArgs {
     double2* st;
     int n;
@@ -418,15 +427,14 @@ struct GnArgs {
     uint64_t cm_out;       // controls outside the tile (trajectory-local index bits)
     double2 m[4];
     int np;                // prefix channels
+    int pq[kGnMaxPrefix];  // tile-local position of each prefix channel's qubit
     FlipChan ch[kGnMaxPrefix];
 };
 __device__ __forceinline__ int gn_local_pos(int q, int u) { return q <= 10 ? q : (q == u ? 11 : -1); }
 
 __global__ __launch_bounds__(256) void k_gate_noise_tile(GnArgs a) {
     __shared__ double2 v[1 << kGnTile];
-    __shared__ uint32_t codes[kGnMaxPrefix][2048 / 16];  // 2-bit code per pair (list overflow)
-    __shared__ uint16_t list[kGnMaxPrefix][kGnListCap];   // flips: pair << 2 | code
-    __shared__ uint32_t count[kGnMaxPrefix];
+    __shared__ uint32_t words[1 << kGnTile];
     const int t = threadIdx.x;
     // this work-group's tile: trajectory traj, the n - 12 non-tile bits from the block index
     const int nfree = a.n - kGnTile;
@@ -444,17 +452,60 @@ __global__ __launch_bounds__(256) void k_gate_noise_tile(GnArgs a) {
     }
     const uint64_t gbase = (traj << a.n) | loc;  // tile-local j -> gbase | (j & 2047) | (j >> 11) << u
     auto gidx = [&](int j) { return gbase | (uint64_t)(j & 2047) | ((uint64_t)(j >> 11) << a.u); };
-#pragma unroll 4
-    for (int r = 0; r < 16; ++r) {
-        const int j = r * 256 + t;
-        v[j] = ld<true>(a.st + gidx(j));
-    }
-    for (int i = t; i < a.np * (2048 / 16); i += 256) codes[i / 128][i % 128] = 0u;
-    if (t < kGnMaxPrefix) count[t] = 0u;
+    // 1. the tile's loads, in flight during the walks
+    double2 r[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) r[k] = ld<true>(a.st + gidx(k * 256 + t));
+#pragma unroll
+    for (int k = 0; k < 16; ++k) words[k * 256 + t] = 0u;
     __syncthreads();
-    // the gate
+    // 2. the prefix channels' flips: 8 blocks of 256 pairs per channel, one walk per thread
+    if (t < a.np * 8) {
+        const int c = t >> 3, jb = t & 7;
+        const FlipChan& ch = a.ch[c];
+        const int q = ch.target, pq = a.pq[c];
+        const uint64_t tl = gbase & ((1ull << a.n) - 1ull);  // trajectory-local base
+        // pair index (within the trajectory) of the tile's first pair of this channel
+        const uint64_t prb = ((tl >> (q + 1)) << q) | (tl & ((1ull << q) - 1ull));
+        uint64_t pr0;  // first pair of this walk's run
+        int run_base;  // tile pair-local index of that pair
+        if (q == a.u) {
+            pr0 = prb + (uint64_t)jb * 256;
+            run_base = jb * 256;
+        } else {  // two runs of 1024 pairs, bit u of the index -> pair bit u - 1
+            const int y = jb >> 2;
+            pr0 = prb + ((uint64_t)y << (a.u - 1)) + (uint64_t)(jb & 3) * 256;
+            run_base = (y << 10) + (jb & 3) * 256;
+        }
+        const uint64_t gb = (a.idx0 + (traj << (a.n - 1)) + pr0) >> kFlipBlockLog;
+        FlipCursor cur{nz_mix(ch.key ^ nz_mix(gb ^ kBlockSalt)), 0, -1, false};
+        uint64_t g = 0, h = 0;
+        const uint64_t lo = gb << kFlipBlockLog, hi = lo + kFlipBlock;
+        while (next_flip(cur, gb, lo, hi, ch, g, h)) {
+            uint32_t code = ch.type == 3 ? 1u : (ch.type == 4 ? 3u : 2u);
+            if (ch.type == 0) {
+                const float r2 = nz_uniform(nz_mix(h ^ 0x5bd1e9955bd1e995ull));
+                code = r2 < 1.0f / 3.0f ? 1u : (r2 < 2.0f / 3.0f ? 2u : 3u);
+            }
+            const int x = run_base + (int)(g - lo);  // tile pair-local index
+            int j0;
+            if (pq == 11) {
+                j0 = x;
+            } else {
+                const int xl = x & 1023, y = x >> 10;
+                const int lo2 = xl & ((1 << pq) - 1);
+                j0 = (((xl ^ lo2) << 1) | lo2) | (y << 11);
+            }
+            atomicOr(&words[j0], code << (2 * c));
+            atomicOr(&words[j0 | (1 << pq)], code << (2 * c));
+        }
+    }
+    // 3. registers -> LDS, the gate
+#pragma unroll
+    for (int k = 0; k < 16; ++k) v[k * 256 + t] = r[k];
+    __syncthreads();
     const bool on_out = (loc & a.cm_out) == a.cm_out;
-    if (a.kind >= 0 && on_out) {
+    if (a.kind >= 0 && on_out) {  // (uniform per work-group)
         const int p0 = gn_local_pos(a.t0, a.u);
         if (a.kind == K_M1) {
             for (int i = t; i < 2048; i += 256) {
@@ -482,94 +533,42 @@ __global__ __launch_bounds__(256) void k_gate_noise_tile(GnArgs a) {
                 }
             }
         }
-    }
-    // the prefix channels' flips: 8 blocks of 256 pairs each, one walk per thread
-    if (t < a.np * 8) {
-        const int c = t >> 3, jb = t & 7;
-        const FlipChan& ch = a.ch[c];
-        const int q = ch.target;
-        const uint64_t tl = gbase & ((1ull << a.n) - 1ull);  // trajectory-local base
-        // pair index (within the trajectory) of the tile's first pair of this channel
-        const uint64_t prb = ((tl >> (q + 1)) << q) | (tl & ((1ull << q) - 1ull));
-        uint64_t pr0;  // first pair of this walk's run
-        int run_base;  // tile pair-local index of that pair
-        if (q == a.u) {
-            pr0 = prb + (uint64_t)jb * 256;
-            run_base = jb * 256;
-        } else {  // two runs of 1024 pairs, bit u of the index -> pair bit u - 1
-            const int y = jb >> 2;
-            pr0 = prb + ((uint64_t)y << (a.u - 1)) + (uint64_t)(jb & 3) * 256;
-            run_base = (y << 10) + (jb & 3) * 256;
-        }
-        const uint64_t gb = (a.idx0 + (traj << (a.n - 1)) + pr0) >> kFlipBlockLog;
-        FlipCursor cur{nz_mix(ch.key ^ nz_mix(gb ^ kBlockSalt)), 0, -1, false};
-        uint64_t g = 0, h = 0;
-        const uint64_t lo = gb << kFlipBlockLog, hi = lo + kFlipBlock;
-        while (next_flip(cur, gb, lo, hi, ch, g, h)) {
-            int code = ch.type == 3 ? 1 : (ch.type == 4 ? 3 : 2);
-            if (ch.type == 0) {
-                const float r2 = nz_uniform(nz_mix(h ^ 0x5bd1e9955bd1e995ull));
-                code = r2 < 1.0f / 3.0f ? 1 : (r2 < 2.0f / 3.0f ? 2 : 3);
-            }
-            const int x = run_base + (int)(g - lo);
-            atomicOr(&codes[c][x >> 4], (uint32_t)code << (2 * (x & 15)));
-            const uint32_t e = atomicAdd(&count[c], 1u);
-            if (e < (uint32_t)kGnListCap) list[c][e] = (uint16_t)((x << 2) | code);
-        }
-    }
-    __syncthreads();
-    for (int c = 0; c < a.np; ++c) {
-        const int q = a.ch[c].target;
-        const int pq = gn_local_pos(q, a.u);
-        const uint32_t nf = count[c];
-        const bool listed = nf <= (uint32_t)kGnListCap;  // (else scan the code bitmap)
-        const int lim = listed ? (int)nf : 2048;
-        for (int e = t; e < lim; e += 256) {
-            int x;
-            uint32_t code;
-            if (listed) {
-                x = list[c][e] >> 2;
-                code = list[c][e] & 3u;
-            } else {
-                x = e;
-                code = (codes[c][x >> 4] >> (2 * (x & 15))) & 3u;
-                if (!code) continue;
-            }
-            int j0;
-            if (pq == 11) {
-                j0 = x;
-            } else {
-                const int xl = x & 1023, y = x >> 10;
-                const int lo = xl & ((1 << pq) - 1);
-                j0 = (((xl ^ lo) << 1) | lo) | (y << 11);
-            }
-            const int j1 = j0 | (1 << pq);
-            if (code == 3) {
-                const double2 w = v[j1];
-                v[j1] = make_double2(-w.x, -w.y);
-            } else {
-                const double2 a0 = v[j0], a1 = v[j1];
-                if (code == 1) {
-                    v[j0] = a1;
-                    v[j1] = a0;
-                } else {
-                    v[j0] = make_double2(a1.y, -a1.x);
-                    v[j1] = make_double2(-a0.y, a0.x);
-                }
-            }
-        }
         __syncthreads();
     }
+    // 4. out[k] = (P v)[k], pulled through the code words, stored in place
 #pragma unroll 4
-    for (int r = 0; r < 16; ++r) {
-        const int j = r * 256 + t;
-        st<true>(a.st + gidx(j), v[j]);
+    for (int k0 = 0; k0 < 16; ++k0) {
+        const int k = k0 * 256 + t;
+        uint32_t w = words[k];
+        int j = k, e = 0;
+        while (w) {
+            const int c = (31 - __builtin_clz(w)) >> 1;  // the last channel that flips j's pair
+            const uint32_t code = (w >> (2 * c)) & 3u;
+            const int bit = (j >> a.pq[c]) & 1;
+            w &= (1u << (2 * c)) - 1u;  // the channels before it
+            if (code == 3u) {           // Z: -1 on the |1> member
+                e += 2 * bit;
+            } else {                    // X: partner; Y: partner with -i (|0> member) / +i (|1>)
+                if (code == 2u) e += bit ? 1 : 3;
+                j ^= 1 << a.pq[c];
+                w = words[j] & ((1u << (2 * c)) - 1u);
+            }
+        }
+        const double2 x = v[j];
+        double2 y;
+        switch (e & 3) {
+            case 0: y = x; break;
+            case 1: y = make_double2(-x.y, x.x); break;   // i
+            case 2: y = make_double2(-x.x, -x.y); break;  // -1
+            default: y = make_double2(x.y, -x.x); break;  // -i
+        }
+        st<true>(a.st + gidx(k), y);
     }
 }
 
 bool gate_noise_tile_supported(int n, const Op* op) {
-    const char* e = std::getenv("QSIM_NOISE_TILE");  // (read per run: tests switch it)
-    if (!(e && std::atoi(e) != 0)) return false;      // (opt-in until measured on the device)
+    const char* e = std::getenv("QSIM_NOISE_TILE");  // (read per run: tests switch it; 0 = push)
+    if (e && std::atoi(e) == 0) return false;
     if (n < kGnTile) return false;
     if (!op) return true;
     if (op->kind == K_SWAP) {
@@ -620,6 +619,7 @@ void launch_gate_noise_step(double2* st, int n, uint64_t batch, uint64_t traj0, 
         if (flip_probability(ch.p) > 0.0) {
             if (a.np == kGnMaxPrefix) break;  // (the rest goes to the push kernel)
             flip_channel(ch.type, ch.qubit, ch.p, noise_key(seed, c), a.ch[a.np]);
+            a.pq[a.np] = ch.qubit <= 10 ? ch.qubit : 11;
             ++a.np;
         }
         ++c;

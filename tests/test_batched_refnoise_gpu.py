@@ -115,9 +115,10 @@ def test_reference_noise_one_launch_per_gate(qsim, oracle, gpu_ready, monkeypatc
     """All Depolarizing passes after a gate in ONE launch (k_noise_units: a work-group per unit
     of whole trajectories, channels in order between work-group barriers), forced here at oracle
     sizes (QSIM_NOISE_UNIT_MIN=1), also on a trajectory shard whose pairs start mid-block.
-    (The push kernels, the batched default; pinned here in case the default changes.)"""
+    (The push kernels: the batched default below 12 qubits, the suffix kernel above.)"""
     monkeypatch.setenv("QSIM_NOISE_UNIT_MIN", "1")
     monkeypatch.setenv("QSIM_NOISE_PULL", "0")
+    monkeypatch.setenv("QSIM_NOISE_TILE", "0")  # (the push kernels alone, also at 12 qubits)
     c = _circuit(qsim, n, 12, seed)
     nm = qsim.NoiseModel()
     nm.addDepolarizingAll(n, 0.2)
@@ -140,6 +141,7 @@ def test_reference_noise_one_launch_equals_per_channel_16q(qsim, gpu_ready, monk
     nm.addDepolarizingAll(n, 0.01)
     out = []
     monkeypatch.setenv("QSIM_NOISE_PULL", "0")
+    monkeypatch.setenv("QSIM_NOISE_TILE", "0")
     for unit_min in ("128", str(1 << 40)):
         monkeypatch.setenv("QSIM_NOISE_UNIT_MIN", unit_min)
         s = qsim.BatchedSimulator(n, B, nm, noise=qsim.BatchedNoise.Reference)
@@ -244,10 +246,12 @@ def test_one_launch_noise_accesses_stay_in_unit(qsim, oracle, gpu_ready, monkeyp
         np.testing.assert_allclose(s.getStateVector(t), whole[traj0 + t], atol=1e-12, rtol=0)
 
 
-# ---- gate + in-tile noise (noise.hip: k_gate_noise_tile, the push path from 12 qubits) --------
+# ---- gate + in-tile noise (noise.hip: k_gate_noise_tile, the reference process's default from 12
+# qubits, round 5) -------------------------------------------------------------------------------
 # The gate and the channels whose qubits lie in its 4096-amplitude tile (qubits 0..10 and one
-# more) in one LDS pass, the remaining channels by the one-launch push kernel: the same
-# operations in the same order, so the same states as gate kernel + push.
+# more) in one LDS pass — the flips composed into per-amplitude code words and every output
+# amplitude pulled through them — the remaining channels by the one-launch push kernel: the
+# same result as applying the channels in order, so the same states as gate kernel + push.
 
 @pytest.mark.parametrize("n,B,seed,traj0,refgates", [(12, 3, 21, 0, False), (13, 2, 22, 3, True),
                                                      (14, 2, 23, 1, False)])
@@ -269,6 +273,26 @@ def test_gate_noise_tile_matches_oracle(qsim, oracle, gpu_ready, monkeypatch, n,
                                                       refgates, states=whole, counter=counter)
     for t in range(B):
         np.testing.assert_allclose(s.getStateVector(t), whole[traj0 + t], atol=1e-12, rtol=0)
+
+
+@pytest.mark.parametrize("p", [0.5, 0.05])
+def test_gate_noise_tile_dense_flips_match_oracle(qsim, oracle, gpu_ready, monkeypatch, p):
+    """Flip densities where most code words hold several fields (p = 0.5: a pair flips on most
+    channels, so the pulled walk moves through up to 12 partners), X / Y / Z channels mixed with
+    depolarizing ones on repeated qubits, controlled gates with controls in and out of the tile."""
+    monkeypatch.setenv("QSIM_NOISE_TILE", "1")
+    n, B, seed = 13, 2, 31
+    c = _circuit(qsim, n, 16, seed)
+    c.cnot(12, 3).toffoli(12, 1, 5).cz(2, 12).swap(4, 12)
+    nm = qsim.NoiseModel()
+    nm.addDepolarizingAll(n, p)
+    s = qsim.BatchedSimulator(n, B, nm, noise=qsim.BatchedNoise.Reference)
+    s.setSeed(seed)
+    entries = [(0, q, p) for q in range(n)]
+    whole, _ = oracle.batched_reference_run(n, B, oracle.gates_of(c), entries, seed)
+    s.run(c)
+    for t in range(B):
+        np.testing.assert_allclose(s.getStateVector(t), whole[t], atol=1e-12, rtol=0)
 
 
 def test_gate_noise_tile_equals_push_16q(qsim, gpu_ready, monkeypatch):
