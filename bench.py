@@ -43,12 +43,14 @@ PROFILE_REGION = ["none"]
 
 
 class region:
-    """roctxProfilerResume(0) / roctxProfilerPause(0) around a timed region when --profile-region
-    names it (rocprofv3 --selected-regions records nothing outside); a no-op otherwise (the roctx
-    library is loaded only then)."""
+    """A roctx range named "timed_<name>" (rocprofv3 --marker-trace: scripts/roofline_check.py
+    keeps the kernels that start inside it) and roctxProfilerResume(0) / roctxProfilerPause(0)
+    (rocprofv3 --selected-regions) around a timed region when --profile-region names it; a no-op
+    otherwise (the roctx library is loaded only then)."""
     _lib = None
 
     def __init__(self, name):
+        self.name = name
         self.on = PROFILE_REGION[0] == name
 
     def __enter__(self):
@@ -56,11 +58,14 @@ class region:
             if region._lib is None:
                 import ctypes
                 region._lib = ctypes.CDLL("librocprofiler-sdk-roctx.so.1")
+                region._lib.roctxRangePushA.argtypes = [ctypes.c_char_p]
             region._lib.roctxProfilerResume(0)
+            region._lib.roctxRangePushA(f"timed_{self.name}".encode())
         return self
 
     def __exit__(self, *exc):
         if self.on:
+            region._lib.roctxRangePop()
             region._lib.roctxProfilerPause(0)
         return False
 
@@ -752,7 +757,11 @@ def main():
         return
     if world > 1 or args.gpus > 1 or args.dry_run:
         from qsim_amd import dist_bench  # sharded strong-scaling path (RCCL over xGMI)
-        dist_bench.run(args, METRIC, HBM_PEAK_GBPS)
+        cpu_fn = None
+        if args.cpu_budget > 0:  # rank 0, after the timed region (dist_bench._cpu_baseline)
+            def cpu_fn(circuit, n, qmod):
+                return cpu_baseline(circuit, n, args.cpu_budget, qmod, args)
+        dist_bench.run(args, METRIC, HBM_PEAK_GBPS, cpu_fn)
     else:
         run_single(args)
 

@@ -404,7 +404,7 @@ void launch_noise(double2* st, int n, int type, int qubit, double p, uint64_t se
 //   2. meanwhile the blocks of every prefix channel are walked (the push kernels' draws: blocks of
 //      256 global pairs, geometric gaps from the same counter hash), one walk per thread, and each
 //      flip's 2-bit code (1 X, 2 Y, 3 Z) is ORed into field c of the CODE WORD of both members of
-//      its pair (LDS, one 32-bit word per amplitude, 16 KiB);
+//      its pair (LDS, 24 bits per amplitude, 12 KiB);
 //   3. the registers go to LDS and the gate runs there;
 //   4. each output amplitude k is PULLED through P: walking its word's non-zero fields from the
 //      last channel down (X / Y move k to the pair partner and re-read the word there, keeping the
@@ -412,7 +412,7 @@ void launch_noise(double2* st, int n, int type, int qubit, double p, uint64_t se
 //      p = 0.01 on 12 channels) is a plain copy — and stored straight to HBM.
 // Exact: out[k] equals applying the channels in order (every step is a swap / sign change of
 // doubles), so the same states bit for bit as the gate kernel + push kernel.  Three barriers per
-// tile whatever the channel count; LDS 80 KiB (two work-groups per CU).
+// tile whatever the channel count; LDS 76 KiB (two work-groups per CU).
 // ---------------------------------------------------------------------------------------
 constexpr int kGnTile = 12;
 constexpr int kGnMaxPrefix = 12;  // 2-bit fields of a 32-bit word (<= 16)
@@ -434,7 +434,16 @@ __device__ __forceinline__ int gn_local_pos(int q, int u) { return q <= 10 ? q :
 
 __global__ __launch_bounds__(256) void k_gate_noise_tile(GnArgs a) {
     __shared__ double2 v[1 << kGnTile];
-    __shared__ uint32_t words[1 << kGnTile];
+    // code words packed to 24 bits per amplitude (12 KiB, so two work-groups fit a CU's 160 KiB
+    // LDS with room to spare): fields of channels 0-7 in 16-bit halves of wlo, 8-11 in bytes of whi
+    __shared__ uint32_t wlo[1 << (kGnTile - 1)], whi[1 << (kGnTile - 2)];
+    auto word_or = [&](int j, int c, uint32_t code) {
+        if (c < 8) atomicOr(&wlo[j >> 1], code << (2 * c + 16 * (j & 1)));
+        else atomicOr(&whi[j >> 2], code << (2 * (c - 8) + 8 * (j & 3)));
+    };
+    auto word_at = [&](int j) {
+        return ((wlo[j >> 1] >> (16 * (j & 1))) & 0xffffu) | (((whi[j >> 2] >> (8 * (j & 3))) & 0xffu) << 16);
+    };
     const int t = threadIdx.x;
     // this work-group's tile: trajectory traj, the n - 12 non-tile bits from the block index
     const int nfree = a.n - kGnTile;
@@ -457,7 +466,9 @@ __global__ __launch_bounds__(256) void k_gate_noise_tile(GnArgs a) {
 #pragma unroll
     for (int k = 0; k < 16; ++k) r[k] = ld<true>(a.st + gidx(k * 256 + t));
 #pragma unroll
-    for (int k = 0; k < 16; ++k) words[k * 256 + t] = 0u;
+    for (int k = 0; k < 8; ++k) wlo[k * 256 + t] = 0u;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) whi[k * 256 + t] = 0u;
     __syncthreads();
     // 2. the prefix channels' flips: 8 blocks of 256 pairs per channel, one walk per thread
     if (t < a.np * 8) {
@@ -496,8 +507,8 @@ __global__ __launch_bounds__(256) void k_gate_noise_tile(GnArgs a) {
                 const int lo2 = xl & ((1 << pq) - 1);
                 j0 = (((xl ^ lo2) << 1) | lo2) | (y << 11);
             }
-            atomicOr(&words[j0], code << (2 * c));
-            atomicOr(&words[j0 | (1 << pq)], code << (2 * c));
+            word_or(j0, c, code);
+            word_or(j0 | (1 << pq), c, code);
         }
     }
     // 3. registers -> LDS, the gate
@@ -539,7 +550,7 @@ __global__ __launch_bounds__(256) void k_gate_noise_tile(GnArgs a) {
 #pragma unroll 4
     for (int k0 = 0; k0 < 16; ++k0) {
         const int k = k0 * 256 + t;
-        uint32_t w = words[k];
+        uint32_t w = word_at(k);
         int j = k, e = 0;
         while (w) {
             const int c = (31 - __builtin_clz(w)) >> 1;  // the last channel that flips j's pair
@@ -551,7 +562,7 @@ __global__ __launch_bounds__(256) void k_gate_noise_tile(GnArgs a) {
             } else {                    // X: partner; Y: partner with -i (|0> member) / +i (|1>)
                 if (code == 2u) e += bit ? 1 : 3;
                 j ^= 1 << a.pq[c];
-                w = words[j] & ((1u << (2 * c)) - 1u);
+                w = word_at(j) & ((1u << (2 * c)) - 1u);
             }
         }
         const double2 x = v[j];

@@ -39,21 +39,35 @@ def _circuit(args):
     return qc.createScalingBenchmarkCircuit(n), "W-REF benchmark_scaling.cu:69-76 (100 H + 20 CNOT)"
 
 
-def run_dry(args, metric: str) -> None:
+def _cpu_baseline(cpu_fn, circuit, n):
+    """Rank 0, after the timed region and its max-over-ranks reduction (so it cannot disturb the
+    measurement): bench.py's cpu_baseline leg (the oracle's single-thread restatement of the
+    reference CPUSimulator on a bounded prefix of the same circuit, plus its 20q / 28q entries)."""
+    if cpu_fn is None:
+        return None
+    from . import circuit as qc
+    return cpu_fn(circuit, n, qc)
+
+
+def run_dry(args, metric: str, peak_gbps: float = 8000.0, cpu_fn=None) -> None:
     from .dist import plan
     rank, world, _ = _rank_world(args)
     grp = FileGroup(rank, world)
     circuit, wl = _circuit(args)
     n = args.qubits
+    L = n - (world.bit_length() - 1)
     perm = list(range(n))
-    remaps = 0
+    remaps, sent = 0, 0.0
     for _ in range(args.warmup):
         steps, perm = plan(circuit, world, rank, perm)
     grp.barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         steps, perm = plan(circuit, world, rank, perm)
-        remaps += sum(1 for s in steps if s["kind"] == "exchange")
+        xs = [s for s in steps if s["kind"] == "exchange"]
+        remaps += len(xs)
+        # each exchange of k global qubits sends (1 - 2^-k) of this rank's 16 B x 2^L shard
+        sent += sum(16.0 * (1 << L) * (1.0 - 2.0 ** -s["k"]) for s in xs)
     t1 = time.perf_counter()
     grp.barrier()
     wall = max(grp.all_reduce_max(t1 - t0), 1e-9)
@@ -62,6 +76,14 @@ def run_dry(args, metric: str) -> None:
         raise RuntimeError("ranks planned different numbers of remaps")
     if rank == 0:
         gates = circuit.getGateCount()
+        # the line's full shape; what only the GPU run measures is null (dry_run: true)
+        roof = {"bound": "hbm", "kernel": "fused_tile", "achieved": None, "peak": peak_gbps, "unit": "GB/s",
+                "frac": None, "traffic": None, "alg_bytes_per_launch": 32.0 * (1 << L),
+                "avg_launch_ms": None, "launches": None}
+        comm = {"bytes_sent_per_step": sent / max(1, args.steps), "bytes_sent_last_run": None,
+                "transfer_ms_per_step": None, "transfer_parts_per_step": None, "sent_GBps": None,
+                "local_kernel_ms_per_step": None, "exposed_ms_per_step": None,
+                "overlapped_ms_per_step": None, "source": "host planner (bytes); times need the GPU run"}
         print(json.dumps({
             "metric": metric, "value": round(gates * args.steps / wall, 2), "unit": "gates/s",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -71,13 +93,16 @@ def run_dry(args, metric: str) -> None:
             "config": {"workload": wl, "qubits": n, "gates": gates,
                        "remaps_per_step": remaps / max(1, args.steps),
                        "parallelism": f"dry run: host planner on {world} ranks, no GPU"},
-            "roofline": None, "cpu_baseline": None}), flush=True)
+            "roofline": roof, "comm": comm,
+            "cpu_baseline": _cpu_baseline(cpu_fn, circuit, n)}), flush=True)
     grp.close()
 
 
-def run(args, metric: str, peak_gbps: float) -> None:
+def run(args, metric: str, peak_gbps: float, cpu_fn=None) -> None:
+    """cpu_fn(circuit, n, circuit_module) -> the cpu_baseline object (bench.py), timed on rank 0
+    after the timed region; None leaves it null."""
     if getattr(args, "dry_run", False):
-        run_dry(args, metric)
+        run_dry(args, metric, peak_gbps, cpu_fn)
         return
     from .dist import DistributedSimulator, unique_id
     rank, world, local = _rank_world(args)
@@ -144,8 +169,10 @@ def run(args, metric: str, peak_gbps: float) -> None:
             "comm": dict(comms[0], per_rank_transfer_ms=[c["transfer_ms_per_step"] for c in comms],
                          max_exposed_ms=max(c["exposed_ms_per_step"] for c in comms)),
         }
-        print(json.dumps(out), flush=True)
     sim.close()
+    if rank == 0:
+        out["cpu_baseline"] = _cpu_baseline(cpu_fn, circuit, n)
+        print(json.dumps(out), flush=True)
     grp.close()
 
 

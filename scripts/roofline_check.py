@@ -2,6 +2,7 @@
 """Recompute a bench line's roofline fraction from a rocprofv3 kernel trace of its timed region.
 
     python scripts/roofline_check.py <region> <bench.json> <kernel_trace.csv> [out.json]
+        [--markers=<marker_api_trace.csv>]
 
 <region> is one of bench.py's --profile-region names.  The trace comes from
     rocprofv3 --selected-regions --kernel-trace --stats --output-format csv -- \
@@ -45,7 +46,17 @@ def load_line(path):
     raise SystemExit(f"no JSON line in {path}")
 
 
-def durations(trace_csv, pattern):
+def marker_window(marker_csv, region):
+    """[start, end] of the roctx range "timed_<region>" (rocprofv3 --marker-trace csv)."""
+    with open(marker_csv, newline="") as f:
+        for row in csv.DictReader(f):
+            msg = row.get("Function") or row.get("Message") or row.get("Name") or ""
+            if msg == f"timed_{region}" or row.get("Message", "") == f"timed_{region}":
+                return int(row["Start_Timestamp"]), int(row["End_Timestamp"])
+    raise SystemExit(f"no range timed_{region} in {marker_csv}")
+
+
+def durations(trace_csv, pattern, window=None):
     rx = re.compile(pattern)
     out = {}
     with open(trace_csv, newline="") as f:
@@ -53,19 +64,25 @@ def durations(trace_csv, pattern):
             name = row.get("Kernel_Name") or row.get("KernelName") or row.get("Name")
             if name is None or not rx.match(name):
                 continue
-            d = int(row["End_Timestamp"]) - int(row["Start_Timestamp"])
-            out.setdefault(name, []).append(d)
+            t0, t1 = int(row["Start_Timestamp"]), int(row["End_Timestamp"])
+            if window and not (window[0] <= t0 <= window[1]):
+                continue
+            out.setdefault(name, []).append(t1 - t0)
     return out
 
 
 def main():
-    region, bench_json, trace = sys.argv[1:4]
+    args = [a for a in sys.argv[1:] if not a.startswith("--markers=")]
+    markers = [a.split("=", 1)[1] for a in sys.argv[1:] if a.startswith("--markers=")]
+    sys.argv = [sys.argv[0]] + args
+    region, bench_json, trace = args[:3]
+    window = marker_window(markers[0], region) if markers else None
     line = load_line(bench_json)
     get_roof, pattern = REGIONS[region]
     roof = get_roof(line)
     if pattern is None:
         pattern = ENGINE_NAMES[roof["kernel"]]
-    per_name = durations(trace, pattern)
+    per_name = durations(trace, pattern, window)
     allv = [d for v in per_name.values() for d in v]
     if not allv:
         raise SystemExit(f"no launches matching {pattern} in {trace}")
@@ -75,6 +92,8 @@ def main():
     frac_med = per / (med_ns * 1e-9) / 1e9 / PEAK
     res = {
         "region": region, "kernel_pattern": pattern, "launches": len(allv),
+        "selection": (f"kernels starting inside the roctx range timed_{region} (--marker-trace)" if window
+                      else "every launch in the trace (--selected-regions)"),
         "line_launches": roof.get("launches"),
         "rocprof_avg_ms": round(avg_ns / 1e6, 4), "rocprof_median_ms": round(med_ns / 1e6, 4),
         "line_avg_launch_ms": roof.get("avg_launch_ms"),

@@ -29,8 +29,8 @@ def _env():
 @pytest.mark.parametrize("world", [2, 4])
 def test_dry_run_launch_prints_one_json_line(world):
     r = subprocess.run([sys.executable, BENCH, "--gpus", str(world), "--dry-run", "--steps", "2",
-                        "--warmup", "1", "--qubits", "24"], capture_output=True, text=True,
-                       timeout=300, env=_env())
+                        "--warmup", "1", "--qubits", "24", "--cpu-budget", "1"], capture_output=True,
+                       text=True, timeout=300, env=_env())
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
     assert len(lines) == 1, r.stdout
@@ -38,6 +38,17 @@ def test_dry_run_launch_prints_one_json_line(world):
     assert out["n_gpus"] == world and out["dry_run"] is True
     assert out["steps"] == 2 and out["value"] > 0 and out["scaling"] == "strong"
     assert out["config"]["remaps_per_step"] >= 1  # W-HC at 24q needs at least one remap per run
+    # the N > 1 line's complete shape — roofline, comm and cpu_baseline (rank 0,
+    # after the timed region)
+    L = 24 - (world.bit_length() - 1)
+    roof = out["roofline"]
+    assert roof["bound"] == "hbm" and roof["peak"] == 8000.0 and roof["alg_bytes_per_launch"] == 32.0 * 2 ** L
+    for k in ("achieved", "frac", "traffic", "avg_launch_ms"):
+        assert k in roof
+    assert out["comm"]["bytes_sent_per_step"] >= 16 * 2 ** L * 0.5  # at least one remap of k >= 1
+    cb = out["cpu_baseline"]
+    assert cb["kind"] == "port" and cb["cores"] == 1 and cb["value"] > 0 and "prefix" in cb["sample"]
+    assert cb["w_hc_20q"]["value"] > 0
 
 
 def test_launcher_parent_does_not_load_the_engine():
