@@ -271,6 +271,10 @@ struct qsim_batch {
     // step's words are built on map_stream while this step's pass runs.
     unsigned char* d_codes = nullptr;
     size_t codes_cap = 0;           // bytes of ONE set
+    // Two sets of per-step flip lists of the in-tile noise kernel (noise.hip: k_gn_lists), built
+    // on map_stream one step ahead.
+    char* d_lists = nullptr;
+    size_t lists_cap = 0;           // bytes of ONE set
     hipStream_t map_stream = nullptr;
     hipEvent_t ev_map[2] = {}, ev_pull[2] = {}, ev_start = nullptr;
     bool pinned = false;
@@ -283,6 +287,7 @@ struct qsim_batch {
         if (d0) (void)hipFree(d0);
         if (d1) (void)hipFree(d1);
         if (d_codes) (void)hipFree(d_codes);
+        if (d_lists) (void)hipFree(d_lists);
         if (d_xz) (void)hipFree(d_xz);
         if (d_e) (void)hipFree(d_e);
         if (d_ch) (void)hipFree(d_ch);
@@ -323,6 +328,40 @@ void settle_in_d0(qsim_batch* b) {
                                hipMemcpyDeviceToDevice, b->stream));
     b->d = b->d0;
 }
+// map_stream and its events (the pulled path's word maps, the tile path's flip lists).
+void ensure_map_stream(qsim_batch* b) {
+    if (b->map_stream) return;
+    QSIM_HIPCHK(hipStreamCreateWithFlags(&b->map_stream, hipStreamNonBlocking));
+    for (hipEvent_t* e : {&b->ev_map[0], &b->ev_map[1], &b->ev_pull[0], &b->ev_pull[1], &b->ev_start})
+        QSIM_HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
+}
+// Two sets of flip lists of `bytes` each, when the device has room beside a margin (false: the
+// tile kernels walk the blocks themselves).
+bool ensure_list_buffers(qsim_batch* b, size_t bytes) {
+    if (bytes > b->lists_cap) {
+        if (b->d_lists) {
+            QSIM_HIPCHK(hipStreamSynchronize(b->stream));
+            if (b->map_stream) QSIM_HIPCHK(hipStreamSynchronize(b->map_stream));
+            (void)hipFree(b->d_lists);
+            b->d_lists = nullptr;
+            b->lists_cap = 0;
+        }
+        size_t free_b = 0, total_b = 0;
+        if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) {
+            (void)hipGetLastError();
+            return false;
+        }
+        if (free_b < 2 * bytes + (256ull << 20)) return false;
+        if (hipMalloc((void**)&b->d_lists, 2 * bytes) != hipSuccess) {
+            (void)hipGetLastError();
+            b->d_lists = nullptr;
+            return false;
+        }
+        b->lists_cap = bytes;
+    }
+    ensure_map_stream(b);
+    return true;
+}
 // Buffers of the pulled noise path (second ensemble buffer, flip codes, touched bits), allocated
 // when the device has room for them beside a margin; false: run the push kernels instead.
 bool ensure_pull_buffers(qsim_batch* b, size_t nch) {
@@ -356,11 +395,7 @@ bool ensure_pull_buffers(qsim_batch* b, size_t nch) {
         if (!grab((void**)&b->d_codes, 2 * codes_b)) return false;
         b->codes_cap = codes_b;
     }
-    if (!b->map_stream) {
-        QSIM_HIPCHK(hipStreamCreateWithFlags(&b->map_stream, hipStreamNonBlocking));
-        for (hipEvent_t* e : {&b->ev_map[0], &b->ev_map[1], &b->ev_pull[0], &b->ev_pull[1], &b->ev_start})
-            QSIM_HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
-    }
+    ensure_map_stream(b);
     return true;
 }
 // Apply the carried Pauli frames to the stored vectors (one pass), frames back to 1.
@@ -599,6 +634,29 @@ int qsim_batch_run(qsim_batch* b, const qsim_gate* gates, size_t count,
                     }
                 }
                 if (b->pinned) settle_in_d0(b);
+                return;
+            }
+            bool all_tile = !ops.empty();
+            for (const Op& op : ops) all_tile = all_tile && gate_noise_tile_supported(b->n, op.kind >= 0 ? &op : nullptr);
+            if (all_tile) {
+                // noise.hip: gate + in-tile channels in LDS per step, each step's flip lists built on
+                // map_stream during the step before (when the device has room for them)
+                const size_t lb = gate_noise_lists_bytes(b->n, (uint64_t)b->batch, dep);
+                GnLists L{};
+                const bool lists = lb && ensure_list_buffers(b, lb);
+                if (lists) {
+                    L.buf[0] = b->d_lists;
+                    L.buf[1] = b->d_lists + b->lists_cap;
+                    L.set_bytes = b->lists_cap;
+                    L.ms = b->map_stream;
+                    L.built[0] = b->ev_map[0];
+                    L.built[1] = b->ev_map[1];
+                    L.used[0] = b->ev_pull[0];
+                    L.used[1] = b->ev_pull[1];
+                    L.start = b->ev_start;
+                }
+                launch_gate_noise_run(b->d, b->n, (uint64_t)b->batch, b->traj0, ops, dep, b->seed, b->ncounter,
+                                      b->stream, &b->timer, lists ? &L : nullptr);
                 return;
             }
             for (const Op& op : ops) {

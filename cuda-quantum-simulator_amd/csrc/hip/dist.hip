@@ -53,6 +53,12 @@ struct DStep {
     // fused plan either way (no extra passes).  `pivot`: the lowest pivot (-1: none).
     int pivot = -1, role = 0;
     uint64_t pmask = 0;
+    // Coarse parts (round 5; exchange steps): a subset of pmask that the step before's passes just
+    // ahead of its per-part tail leave untouched.  Those passes (which do touch the other pivots)
+    // run per value of these bits, each coarse part followed at once by the tail of its fine parts,
+    // so the first part can leave after 1/2^|coarse| of them instead of after all of them.  Parts
+    // are exchanged in coarse-major order (part_order).  0: none.
+    uint64_t coarse = 0;
     // planning only: the circuit gates emitted into this step (rank-independent), their physical
     // qubit masks, and for each op the index of the gate (in this list) it came from
     std::vector<uint64_t> gmask;
@@ -61,11 +67,74 @@ struct DStep {
 
 constexpr int kMaxPivots = 4;
 constexpr int kMaxParts = 1 << kMaxPivots;  // part-exchanges of one overlapped remap
+// QSIM_DIST_COARSE=0: no coarse parts (DStep::coarse; read once)
+static bool coarse_enabled() {
+    static const bool v = [] {
+        const char* e = std::getenv("QSIM_DIST_COARSE");
+        return e == nullptr || std::atoi(e) != 0;
+    }();
+    return v;
+}
 // QSIM_DIST_CARRY=1 (experimental, off by default; read per call so tests can switch it): a run's
 // last step is left pending and merged into the next run's first step (qsim_dist_run).
 bool carry_enabled() {
     const char* e = std::getenv("QSIM_DIST_CARRY");
     return e != nullptr && std::atoi(e) != 0;
+}
+// The positions of `mask` that pass p's tile touches (all of them for a per-gate step or a tile
+// below 4 free bits: such passes never run as sub-space launches).
+static uint64_t pass_touches(const FusedPass& p, uint64_t mask) {
+    if (p.single >= 0 || p.h < 4) return mask;
+    uint64_t t = 0;
+    for (int i = 0; i < 6 + p.h - p.r0; ++i) t |= mask & (1ull << p.hpos[i]);
+    return t;
+}
+// Coarse split of the passes [lo, hi) of a plan just ahead of its per-part tail, for pivots `set`:
+// the count c of passes (ending at hi) and the coarse bits (pivots none of them touches) that
+// minimise the exposed work (hi - lo - c) + c / 2^|coarse| (in passes).  *cb = 0, 0: none.
+static int coarse_split(const Plan& pl, int lo, int hi, uint64_t set, uint64_t* cb) {
+    int best_c = 0;
+    uint64_t best_cb = 0, U = 0;
+    double best = (double)(hi - lo);
+    for (int c = 1; c <= hi - lo; ++c) {
+        U |= pass_touches(pl.passes[hi - c], set);
+        const uint64_t b = set & ~U;
+        if (!b) break;
+        const double e = (double)(hi - lo - c) + (double)c / (double)(1 << __builtin_popcountll(b));
+        if (e < best - 1e-9) {
+            best = e;
+            best_c = c;
+            best_cb = b;
+        }
+    }
+    *cb = best_cb;
+    return best_c;
+}
+// Exchange order of the K parts of an overlapped remap with pivots pmask and coarse bits cb:
+// coarse-major (part index bit j = the j-th pivot; the coarse pivots' bits vary slowest), so the
+// parts of the first coarse part, whose passes finish first, leave first.  Rank-independent.
+static void part_order(uint64_t pmask, uint64_t cb, int* order) {
+    const int m = __builtin_popcountll(pmask), K = 1 << m;
+    uint64_t ch = 0;  // coarse pivots as part-index bits
+    {
+        int j = 0;
+        for (uint64_t mm = pmask; mm; mm &= mm - 1, ++j)
+            if ((cb >> __builtin_ctzll(mm)) & 1ull) ch |= 1ull << j;
+    }
+    const uint64_t fh = (uint64_t)(K - 1) & ~ch;
+    const int Kc = 1 << __builtin_popcountll(ch), Kf = K / Kc;
+    int i = 0;
+    for (int cv = 0; cv < Kc; ++cv)
+        for (int f = 0; f < Kf; ++f) {
+            uint64_t h = 0;
+            int a = 0, b = 0;
+            for (int j = 0; j < m; ++j) {
+                if ((ch >> j) & 1ull) h |= (uint64_t)((cv >> a++) & 1) << j;
+                else h |= (uint64_t)((f >> b++) & 1) << j;
+            }
+            order[i++] = (int)h;
+        }
+    (void)fh;
 }
 static bool pass_avoids(const FusedPass& p, uint64_t pmask) {
     if (p.single >= 0 || p.h < 4) return false;
@@ -118,7 +187,11 @@ static void mark_overlap(std::vector<DStep>& steps, int L, int world, const std:
     if (!enabled || L < 8) return;
     if (carry && !steps.empty() && steps[0].kind == 0) steps[0].role |= 2;
     const int min_gates = 4;
-    const double R = 50.0 / std::max(2, world);
+    static const double r_scale = [] {  // QSIM_DIST_MODEL_R (experiments): R x world, default 50
+        const char* e = std::getenv("QSIM_DIST_MODEL_R");
+        return e ? std::atof(e) : 50.0;
+    }();
+    const double R = r_scale / std::max(2, world);
     for (size_t i = 1; i + 1 < steps.size(); ++i) {
         DStep& ex = steps[i];
         DStep& A = steps[i - 1];
@@ -145,8 +218,9 @@ static void mark_overlap(std::vector<DStep>& steps, int L, int world, const std:
         const DStep& rB = ref[i + 1];
         if (by_plan && !rA.ops.empty() && !rB.ops.empty() && !cand.empty()) {
             const uint64_t avoidA0 = (A.role & 2) ? (i >= 2 ? steps[i - 2].pmask : carry) : 0ull;
-            // T of a pivot set (pass counts in units of one pass); +inf when planning failed
-            auto model = [&](uint64_t set) {
+            // T of a pivot set (pass counts in units of one pass); +inf when planning failed;
+            // *cb_out: the coarse bits of that set (coarse_split)
+            auto model = [&](uint64_t set, uint64_t* cb_out = nullptr) {
                 const Plan pA = plan_fused(rA.ops, L, -1, set, avoidA0);
                 const Plan pB = plan_fused(rB.ops, L, -1, 0, set);
                 const int na = (int)pA.passes.size(), nb = (int)pB.passes.size();
@@ -171,7 +245,12 @@ static void mark_overlap(std::vector<DStep>& steps, int L, int world, const std:
                     const Plan pN = plan_fused(*next_ops, L, -1, set);
                     hn = !pN.passes.empty() && pass_avoids(pN.passes[0], set) ? 1 : 0;
                 }
-                return std::max(R + (na - t - ha) + (nb - h) + (t + h + hn) / K - hn, na + nb + R / K);
+                // the passes just ahead of the tail run per coarse part (coarse_split)
+                uint64_t cb = 0;
+                const int c = coarse_enabled() ? coarse_split(pA, ha, na - t, set, &cb) : 0;
+                if (cb_out) *cb_out = cb;
+                const double exposed = (double)(na - t - ha - c) + (c ? (double)c / (double)(1 << __builtin_popcountll(cb)) : 0.0);
+                return std::max(R + exposed + (nb - h) + (t + h + hn) / K - hn, na + nb + R / K);
             };
             auto score_all = [&](uint64_t base, const std::vector<int>& cs) {
                 std::vector<double> sc(cs.size(), 1e30);
@@ -186,7 +265,10 @@ static void mark_overlap(std::vector<DStep>& steps, int L, int world, const std:
                 for (auto& t : th) t.join();
                 return sc;
             };
-            // round 1: every single position; later rounds: the 8 best singles added to the set
+            // round 1: every single position; later rounds: a beam of the kBeam best sets, each
+            // grown by one of the kPool best singles (the greedy of round 4 kept one set: it missed
+            // sets whose first pass leaves a pivot untouched, i.e. coarse parts, round 5)
+            constexpr size_t kBeam = 4, kPool = 10;
             std::vector<double> sc1 = score_all(0, cand);
             std::vector<size_t> order(cand.size());
             for (size_t c = 0; c < order.size(); ++c) order[c] = c;
@@ -194,19 +276,53 @@ static void mark_overlap(std::vector<DStep>& steps, int L, int world, const std:
             double bestT = sc1[order[0]];
             uint64_t set = bestT < 1e29 ? 1ull << cand[order[0]] : 0ull;
             std::vector<int> pool;
-            for (size_t c = 1; c < order.size() && pool.size() < 8; ++c)
-                if (sc1[order[c]] < 1e29) pool.push_back(cand[order[c]]);
-            for (int m = 1; set && m < max_piv && !pool.empty(); ++m) {
-                const std::vector<double> sc = score_all(set, pool);
-                size_t bi = 0;
-                for (size_t c = 1; c < sc.size(); ++c)
-                    if (sc[c] < sc[bi]) bi = c;
-                if (!(sc[bi] < bestT - 1e-9)) break;
-                bestT = sc[bi];
-                set |= 1ull << pool[bi];
-                pool.erase(pool.begin() + (long)bi);
+            std::vector<std::pair<double, uint64_t>> beam;
+            for (size_t c = 0; c < order.size() && pool.size() < kPool; ++c)
+                if (sc1[order[c]] < 1e29) {
+                    pool.push_back(cand[order[c]]);
+                    if (beam.size() < kBeam) beam.push_back({sc1[order[c]], 1ull << cand[order[c]]});
+                }
+            for (int m = 1; set && m < max_piv && !beam.empty(); ++m) {
+                std::vector<uint64_t> sets;
+                for (const auto& b : beam)
+                    for (int q : pool) {
+                        const uint64_t s2 = b.second | (1ull << q);
+                        if (s2 != b.second && std::find(sets.begin(), sets.end(), s2) == sets.end()) sets.push_back(s2);
+                    }
+                std::vector<double> sc(sets.size(), 1e30);
+                {
+                    std::vector<std::thread> th;
+                    const size_t nt = std::min<size_t>(sets.size(), 16);
+                    for (size_t w = 0; w < nt; ++w)
+                        th.emplace_back([&, w] {
+                            for (size_t c = w; c < sets.size(); c += nt) try {
+                                    sc[c] = model(sets[c]);
+                                } catch (...) {
+                                }
+                        });
+                    for (auto& t : th) t.join();
+                }
+                std::vector<size_t> o2(sets.size());
+                for (size_t c = 0; c < o2.size(); ++c) o2[c] = c;
+                std::sort(o2.begin(), o2.end(), [&](size_t a, size_t b) {
+                    return sc[a] != sc[b] ? sc[a] < sc[b] : sets[a] < sets[b];  // (deterministic)
+                });
+                beam.clear();
+                for (size_t c = 0; c < o2.size() && beam.size() < kBeam; ++c)
+                    if (sc[o2[c]] < 1e29) beam.push_back({sc[o2[c]], sets[o2[c]]});
+                if (!beam.empty() && beam[0].first < bestT - 1e-9) {
+                    bestT = beam[0].first;
+                    set = beam[0].second;
+                }
             }
-            if (set) pmask = set;
+            if (set) {
+                pmask = set;
+                try {
+                    (void)model(set, &ex.coarse);
+                } catch (...) {
+                    ex.coarse = 0;
+                }
+            }
         }
         if (!pmask) continue;
         ex.pmask = pmask;
@@ -465,7 +581,8 @@ struct PivotMemo {
     uint64_t carry;
     std::vector<qsim_gate> gates;
     std::vector<int> perm;
-    std::vector<uint64_t> pmask;  // per step (0: none)
+    std::vector<uint64_t> pmask;   // per step (0: none)
+    std::vector<uint64_t> coarse;  // per step
     uint64_t used;
 };
 std::mutex g_pivot_mu;
@@ -496,6 +613,7 @@ static std::vector<DStep> plan_dist(const qsim_gate* gates, size_t count, int n,
                 for (size_t k = 0; k < steps.size(); ++k)
                     if (m.pmask[k]) {
                         steps[k].pmask = m.pmask[k];
+                        steps[k].coarse = m.coarse[k];
                         steps[k].pivot = __builtin_ctzll(m.pmask[k]);
                         steps[k - 1].role |= 1;
                         steps[k + 1].role |= 2;
@@ -519,8 +637,11 @@ static std::vector<DStep> plan_dist(const qsim_gate* gates, size_t count, int n,
         if (ref.size() != steps.size()) fail(QSIM_ERR_RUNTIME, "exchange skeleton mismatch");
         mark_overlap(steps, L, 1 << g, ref, carry, &next_ops);
     }
-    PivotMemo m{n, g, carry, std::vector<qsim_gate>(gates, gates + count), perm_in, {}, 0};
-    for (const DStep& st : steps) m.pmask.push_back(st.kind == 1 ? st.pmask : 0ull);
+    PivotMemo m{n, g, carry, std::vector<qsim_gate>(gates, gates + count), perm_in, {}, {}, 0};
+    for (const DStep& st : steps) {
+        m.pmask.push_back(st.kind == 1 ? st.pmask : 0ull);
+        m.coarse.push_back(st.kind == 1 ? st.coarse : 0ull);
+    }
     std::lock_guard<std::mutex> l(g_pivot_mu);
     m.used = ++g_pivot_clock;
     if (g_pivots.size() >= 16)
@@ -633,6 +754,7 @@ struct qsim_dist {
     // overlapped remap, per part h < kMaxParts: tail done (pev[h]), packed (kMaxParts + h), sent
     // (2 kMaxParts + h), unpacked (3 kMaxParts + h)
     hipEvent_t pev[4 * kMaxParts] = {};
+    int order[kMaxParts] = {};  // exchange order of the pending overlapped remap's parts (part_order)
     int overlapped = 0;                 // remaps of the last run that overlapped local work
     ncclComm_t comm = nullptr;
     bool aborted = false;  // the communicator was aborted after an RCCL / HIP error or a timeout
@@ -1089,7 +1211,9 @@ void exchange_parts(qsim_dist* d, const DStep& ex, const std::vector<char>& fuse
     const uint64_t part_amps = 1ull << (d->L - __builtin_popcountll(ex.pmask));
     const uint64_t chunk = part_amps >> ex.k;
     const double bytes = 2.0 * 16.0 * (double)(part_amps - chunk) * (double)d->shards.size();
-    for (int h = 0; h < K; ++h) {
+    part_order(ex.pmask, ex.coarse & ex.pmask, d->order);  // (the same on every rank: RCCL pairs posts in order)
+    for (int oi = 0; oi < K; ++oi) {
+        const int h = d->order[oi];
         TimedLaunch tl(&d->timer, "alltoall_remap", bytes, d->copy_stream);
         std::vector<XPlan> xs;
         for (Shard& sh : d->shards) xs.push_back(xplan(d, sh, ex, h));
@@ -1329,7 +1453,8 @@ void flush_carry(qsim_dist* d) {
     qsim_dist::Carry& c = d->carry;
     if (!c.active) return;
     if (c.parts > kMaxParts) fail(QSIM_ERR_RUNTIME, "carried remap with too many parts");
-    for (int h = 0; h < c.parts; ++h) {
+    for (int oi = 0; oi < c.parts; ++oi) {
+        const int h = d->order[oi];
         QSIM_HIPCHK(hipStreamWaitEvent(d->stream, d->pev[3 * kMaxParts + h], 0));
         for (size_t i = 0; i < d->shards.size(); ++i)
             if (c.runs[i].plan)
@@ -1582,7 +1707,8 @@ int qsim_dist_run(qsim_dist* d, const qsim_gate* gates, size_t count, int flags)
         if (merge) ++d->carried;
         auto wait_pending = [&]() {
             if (pending > kMaxParts) fail(QSIM_ERR_RUNTIME, "pending remap with too many parts");
-            for (int h = 0; h < pending; ++h) QSIM_HIPCHK(hipStreamWaitEvent(d->stream, d->pev[3 * kMaxParts + h], 0));
+            for (int oi = 0; oi < pending; ++oi)
+                QSIM_HIPCHK(hipStreamWaitEvent(d->stream, d->pev[3 * kMaxParts + d->order[oi]], 0));
             pending = 0;
         };
         // Every rank's plan has the same step skeleton (mark_overlap decides from
@@ -1661,7 +1787,8 @@ int qsim_dist_run(qsim_dist* d, const qsim_gate* gates, size_t count, int flags)
             if (head) {
                 const bool carried = k == 0 && merge;
                 if (pending > kMaxParts) fail(QSIM_ERR_RUNTIME, "pending remap with too many parts");
-                for (int h = 0; h < pending; ++h) {
+                for (int oi = 0; oi < pending; ++oi) {
+                    const int h = d->order[oi];
                     QSIM_HIPCHK(hipStreamWaitEvent(d->stream, d->pev[3 * kMaxParts + h], 0));
                     if (carried) {  // part h of the previous run's last step, then part h of this one
                         const qsim_dist::Carry& c = d->carry;
@@ -1681,20 +1808,43 @@ int qsim_dist_run(qsim_dist* d, const qsim_gate* gates, size_t count, int flags)
                     d->carry.rp = nullptr;
                 }
             }
+            // coarse parts (DStep::coarse, rank-independent): this shard's passes just ahead of its
+            // tail that avoid the coarse bits run per coarse part, each followed by the tails of its
+            // fine parts, in the exchange's part order
+            const uint64_t cb = pa ? (plans[0][k + 1].coarse & pa) : 0ull;
+            std::vector<size_t> jc(S, 0);
+            for (size_t i = 0; i < S; ++i) {
+                if (!runs[i].plan) continue;
+                jc[i] = runs[i].j2;
+                const size_t lo = head ? runs[i].j1 : 0;
+                if (cb)
+                    while (jc[i] > lo && pass_avoids(runs[i].plan->passes[jc[i] - 1], cb)) --jc[i];
+            }
             wait_pending();
             for (size_t i = 0; i < S; ++i) {
                 if (runs[i].plan)
-                    run_part(d, d->shards[i], plans[i][k].ops, runs[i], head ? runs[i].j1 : 0, runs[i].j2, 0, -1,
+                    run_part(d, d->shards[i], plans[i][k].ops, runs[i], head ? runs[i].j1 : 0, jc[i], 0, -1,
                              homes[i], alts[i]);
                 else run_part(d, d->shards[i], plans[i][k].ops, runs[i], 0, 1);  // per-gate: the whole list
             }
             if (pa) {  // the exchange after waits for pev[h]
-                for (int h = 0, K = part_count(pa); h < K; ++h) {
-                    for (size_t i = 0; i < S; ++i)
-                        if (runs[i].plan)
-                            run_part(d, d->shards[i], plans[i][k].ops, runs[i], runs[i].j2, runs[i].np, pa, h, homes[i],
-                                     alts[i]);
-                    QSIM_HIPCHK(hipEventRecord(d->pev[h], d->stream));
+                const int K = part_count(pa), Kc = 1 << __builtin_popcountll(cb), Kf = K / Kc;
+                int ord[kMaxParts];
+                part_order(pa, cb, ord);
+                for (int cv = 0; cv < Kc; ++cv) {
+                    if (cb)
+                        for (size_t i = 0; i < S; ++i)
+                            if (runs[i].plan)
+                                run_part(d, d->shards[i], plans[i][k].ops, runs[i], jc[i], runs[i].j2, cb, cv, homes[i],
+                                         alts[i]);
+                    for (int f = 0; f < Kf; ++f) {
+                        const int h = ord[cv * Kf + f];
+                        for (size_t i = 0; i < S; ++i)
+                            if (runs[i].plan)
+                                run_part(d, d->shards[i], plans[i][k].ops, runs[i], runs[i].j2, runs[i].np, pa, h,
+                                         homes[i], alts[i]);
+                        QSIM_HIPCHK(hipEventRecord(d->pev[h], d->stream));
+                    }
                 }
             }
         }
@@ -1908,6 +2058,7 @@ int qsim_dist_plan(int n, int world, int rank, const qsim_gate* gates, size_t co
                 }
                 o.pivot = s.pivot;
                 o.pmask = s.pmask;
+                o.coarse = s.coarse;
                 o.role = s.role;
             }
             for (const Op& op : s.ops) {
@@ -1933,9 +2084,8 @@ int qsim_dist_plan(int n, int world, int rank, const qsim_gate* gates, size_t co
     });
 }
 
-int qsim_dist_plan_passes_carry(int n, int world, int rank, const qsim_gate* gates, size_t count,
-                                int32_t* perm_inout, uint64_t* carry_inout, int32_t* passes, size_t cap,
-                                size_t* n_steps) {
+static int plan_passes_impl(int n, int world, int rank, const qsim_gate* gates, size_t count, int32_t* perm_inout,
+                            uint64_t* carry_inout, int32_t* passes, size_t cap, size_t* n_steps, int width) {
     return dguard([&] {
         const int g = log2_exact(world);
         check_sizes(n, g);
@@ -1947,7 +2097,7 @@ int qsim_dist_plan_passes_carry(int n, int world, int rank, const qsim_gate* gat
         const int L = n - g;
         uint64_t carry_out = 0;
         for (size_t k = 0; k < st.size(); ++k) {
-            int np = 0, head = 0, tail = 0;
+            int np = 0, head = 0, tail = 0, coarse = 0, coarse_bits = 0;
             if (st[k].kind == 0 && !st[k].ops.empty()) {  // as prepare_step plans it
                 const uint64_t pb = (st[k].role & 2) ? (k == 0 ? carry : st[k - 1].pmask) : 0ull;
                 const uint64_t pa = (st[k].role & 1) ? st[k + 1].pmask : 0ull;
@@ -1957,11 +2107,35 @@ int qsim_dist_plan_passes_carry(int n, int world, int rank, const qsim_gate* gat
                     while (head < np && pass_avoids(pl.passes[head], pb)) ++head;
                 if (pa)
                     while (tail < np - head && pass_avoids(pl.passes[np - 1 - tail], pa)) ++tail;
+                const uint64_t cb = pa ? (st[k + 1].coarse & pa) : 0ull;
+                if (cb) {  // as qsim_dist_run splits the step
+                    int jc = np - tail;
+                    while (jc > head && pass_avoids(pl.passes[jc - 1], cb)) --jc;
+                    coarse = np - tail - jc;
+                    coarse_bits = __builtin_popcountll(cb);
+                }
+                static const bool dbg = std::getenv("QSIM_DIST_DEBUG_PASSES") != nullptr;
+                if (dbg && pa) {  // the exchange-after pivots each pass touches
+                    std::string line = "[passes] step " + std::to_string(k) + " pa " + std::to_string(pa) + ":";
+                    for (int j = 0; j < np; ++j) {
+                        uint64_t tm = 0;
+                        const FusedPass& fp = pl.passes[j];
+                        if (fp.single >= 0 || fp.h < 4) tm = pa;
+                        else
+                            for (int i = 0; i < 6 + fp.h - fp.r0; ++i) tm |= pa & (1ull << fp.hpos[i]);
+                        line += " " + std::to_string(__builtin_popcountll(tm));
+                    }
+                    std::fprintf(stderr, "%s\n", line.c_str());
+                }
             }
             if (k < cap && passes) {
-                passes[3 * k] = st[k].kind == 1 ? -1 : np;
-                passes[3 * k + 1] = head;
-                passes[3 * k + 2] = tail;
+                passes[width * k] = st[k].kind == 1 ? -1 : np;
+                passes[width * k + 1] = head;
+                passes[width * k + 2] = tail;
+                if (width >= 5) {
+                    passes[width * k + 3] = coarse;
+                    passes[width * k + 4] = coarse_bits;
+                }
             }
             // a last step run wholly per part is carried into the next run (qsim_dist_run)
             if (k + 1 == st.size() && k > 0 && st[k].kind == 0 && (st[k].role & 2) && !(st[k].role & 1) && np > 0 &&
@@ -1973,6 +2147,18 @@ int qsim_dist_plan_passes_carry(int n, int world, int rank, const qsim_gate* gat
             for (int q = 0; q < n; ++q) perm_inout[q] = perm[q];
         if (carry_inout) *carry_inout = carry_out;
     });
+}
+
+int qsim_dist_plan_passes_carry(int n, int world, int rank, const qsim_gate* gates, size_t count,
+                                int32_t* perm_inout, uint64_t* carry_inout, int32_t* passes, size_t cap,
+                                size_t* n_steps) {
+    return plan_passes_impl(n, world, rank, gates, count, perm_inout, carry_inout, passes, cap, n_steps, 3);
+}
+
+int qsim_dist_plan_passes_coarse(int n, int world, int rank, const qsim_gate* gates, size_t count,
+                                 int32_t* perm_inout, uint64_t* carry_inout, int32_t* passes, size_t cap,
+                                 size_t* n_steps) {
+    return plan_passes_impl(n, world, rank, gates, count, perm_inout, carry_inout, passes, cap, n_steps, 5);
 }
 
 int qsim_dist_plan_passes(int n, int world, int rank, const qsim_gate* gates, size_t count,

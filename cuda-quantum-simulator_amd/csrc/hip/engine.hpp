@@ -385,6 +385,20 @@ bool gate_noise_tile_supported(int n, const Op* op);
 void launch_gate_noise_step(double2* st, int n, uint64_t batch, uint64_t traj0, const Op* op,
                             const std::vector<NoiseChan>& chans, uint64_t seed, uint64_t& counter, hipStream_t s,
                             Timer* tm);
+// A whole run of gate steps (ops[i].kind < 0: no gate) through the tile kernel, each step's
+// prefix flip lists built by k_gn_lists on L->ms (two sets, event-ordered) during the step before;
+// L == null or gate_noise_lists_bytes == 0: the tile kernels walk the blocks themselves.  Every
+// op must pass gate_noise_tile_supported.  counter advances by ops.size() x chans.size().
+struct GnLists {
+    void* buf[2];
+    size_t set_bytes;  // of one set (>= gate_noise_lists_bytes)
+    hipStream_t ms;
+    hipEvent_t built[2], used[2], start;
+};
+size_t gate_noise_lists_bytes(int n, uint64_t batch, const std::vector<NoiseChan>& chans);
+void launch_gate_noise_run(double2* st, int n, uint64_t batch, uint64_t traj0, const std::vector<Op>& ops,
+                           const std::vector<NoiseChan>& chans, uint64_t seed, uint64_t& counter, hipStream_t s,
+                           Timer* tm, const GnLists* L);
 // Pulled noise (noise.hip): the noise step after one gate (channels `chans`, passes counter0,
 // counter0 + 1, ...; the push kernels' draws) applied by the NEXT gate's pass: dst = U (P src)
 // out of place, op == null: the identity (the last step of a run).  words: >=

@@ -415,7 +415,7 @@ void launch_noise(double2* st, int n, int type, int qubit, double p, uint64_t se
 // tile whatever the channel count; LDS 76 KiB (two work-groups per CU).
 // ---------------------------------------------------------------------------------------
 constexpr int kGnTile = 12;
-constexpr int kGnMaxPrefix = 12;  // 2-bit fields of a 32-bit word (<= 16)
+constexpr int kGnMaxPrefix = 12;  // 2-bit fields of a 24-bit packed word
 struct GnArgs {
     double2* st;
     int n;
@@ -429,8 +429,85 @@ struct GnArgs {
     int np;                // prefix channels
     int pq[kGnMaxPrefix];  // tile-local position of each prefix channel's qubit
     FlipChan ch[kGnMaxPrefix];
+    // precomputed flip lists of this step (k_gn_lists, built on a second stream during the step
+    // before), or null: the work-group walks the blocks itself.  Per tile and prefix channel, cap
+    // entries (tile pair-local index << 2 | code) and the flip count (> cap: overflow, walked here)
+    const uint16_t* list;
+    const uint32_t* cnt;
+    int cap;
 };
 __device__ __forceinline__ int gn_local_pos(int q, int u) { return q <= 10 ? q : (q == u ? 11 : -1); }
+
+// Tile b of a step: its trajectory and its non-tile index bits (11 .. n-1 except u, ascending,
+// from the low bits of b); tile-local j -> gbase | (j & 2047) | (j >> 11) << u.
+__device__ __forceinline__ uint64_t gn_tile_base(uint64_t b, int n, int u, uint64_t* traj_out, uint64_t* loc_out) {
+    const int nfree = n - kGnTile;
+    const uint64_t traj = b >> nfree;
+    const uint64_t m = b & ((1ull << nfree) - 1ull);
+    uint64_t loc = 0;
+    int j = 0;
+    for (int q = 11; q < n; ++q) {
+        if (q == u) continue;
+        loc |= ((m >> j) & 1ull) << q;
+        ++j;
+    }
+    *traj_out = traj;
+    *loc_out = loc;
+    return (traj << n) | loc;
+}
+// Walk block jb (of 8) of prefix channel c over the tile at gbase: f(x, code) for every flip, x
+// the tile pair-local index.  The push kernels' draws exactly (flip_block: blocks of 256 global
+// pairs, geometric gaps from the same counter hash).
+template <class F>
+__device__ __forceinline__ void gn_walk(const GnArgs& a, int c, int jb, uint64_t traj, uint64_t gbase, F&& f) {
+    const FlipChan& ch = a.ch[c];
+    const int q = ch.target;
+    const uint64_t tl = gbase & ((1ull << a.n) - 1ull);  // trajectory-local base
+    // pair index (within the trajectory) of the tile's first pair of this channel
+    const uint64_t prb = ((tl >> (q + 1)) << q) | (tl & ((1ull << q) - 1ull));
+    uint64_t pr0;  // first pair of this walk's run
+    int run_base;  // tile pair-local index of that pair
+    if (q == a.u) {
+        pr0 = prb + (uint64_t)jb * 256;
+        run_base = jb * 256;
+    } else {  // two runs of 1024 pairs, bit u of the index -> pair bit u - 1
+        const int y = jb >> 2;
+        pr0 = prb + ((uint64_t)y << (a.u - 1)) + (uint64_t)(jb & 3) * 256;
+        run_base = (y << 10) + (jb & 3) * 256;
+    }
+    const uint64_t gb = (a.idx0 + (traj << (a.n - 1)) + pr0) >> kFlipBlockLog;
+    FlipCursor cur{nz_mix(ch.key ^ nz_mix(gb ^ kBlockSalt)), 0, -1, false};
+    uint64_t g = 0, h = 0;
+    const uint64_t lo = gb << kFlipBlockLog, hi = lo + kFlipBlock;
+    while (next_flip(cur, gb, lo, hi, ch, g, h)) {
+        uint32_t code = ch.type == 3 ? 1u : (ch.type == 4 ? 3u : 2u);
+        if (ch.type == 0) {
+            const float r2 = nz_uniform(nz_mix(h ^ 0x5bd1e9955bd1e995ull));
+            code = r2 < 1.0f / 3.0f ? 1u : (r2 < 2.0f / 3.0f ? 2u : 3u);
+        }
+        f(run_base + (int)(g - lo), code);
+    }
+}
+
+// The flip lists of one step: one thread per (tile, prefix channel) walks that channel's 8 blocks
+// over the tile (DP log per draw: run on a second stream while the previous step's tile kernel,
+// HBM-bound, streams).
+__global__ __launch_bounds__(256) void k_gn_lists(GnArgs a, uint16_t* list, uint32_t* cnt, uint64_t tiles) {
+    const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (tid >= tiles * (uint64_t)a.np) return;
+    const uint64_t b = tid / (uint64_t)a.np;
+    const int c = (int)(tid - b * (uint64_t)a.np);
+    uint64_t traj = 0, loc = 0;
+    const uint64_t gbase = gn_tile_base(b, a.n, a.u, &traj, &loc);
+    uint16_t* out = list + (b * kGnMaxPrefix + (uint64_t)c) * (uint64_t)a.cap;
+    uint32_t k = 0;
+    for (int jb = 0; jb < 8; ++jb)
+        gn_walk(a, c, jb, traj, gbase, [&](int x, uint32_t code) {
+            if (k < (uint32_t)a.cap) out[k] = (uint16_t)((x << 2) | (int)code);
+            ++k;
+        });
+    cnt[b * kGnMaxPrefix + (uint64_t)c] = k;
+}
 
 __global__ __launch_bounds__(256) void k_gate_noise_tile(GnArgs a) {
     __shared__ double2 v[1 << kGnTile];
@@ -444,24 +521,25 @@ __global__ __launch_bounds__(256) void k_gate_noise_tile(GnArgs a) {
     auto word_at = [&](int j) {
         return ((wlo[j >> 1] >> (16 * (j & 1))) & 0xffffu) | (((whi[j >> 2] >> (8 * (j & 3))) & 0xffu) << 16);
     };
-    const int t = threadIdx.x;
-    // this work-group's tile: trajectory traj, the n - 12 non-tile bits from the block index
-    const int nfree = a.n - kGnTile;
-    const uint64_t traj = (uint64_t)blockIdx.x >> nfree;
-    const uint64_t m = (uint64_t)blockIdx.x & ((1ull << nfree) - 1ull);
-    // non-tile local bits: 11 .. n-1 except u, ascending
-    uint64_t loc = 0;
-    {
-        int j = 0;
-        for (int b = 11; b < a.n; ++b) {
-            if (b == a.u) continue;
-            loc |= ((m >> j) & 1ull) << b;
-            ++j;
+    // a flip of prefix channel c on tile pair-local pair x: its code into both members' words
+    auto flip_or = [&](int c, int x, uint32_t code) {
+        const int pq = a.pq[c];
+        int j0;
+        if (pq == 11) {
+            j0 = x;
+        } else {
+            const int xl = x & 1023, y = x >> 10;
+            const int lo2 = xl & ((1 << pq) - 1);
+            j0 = (((xl ^ lo2) << 1) | lo2) | (y << 11);
         }
-    }
-    const uint64_t gbase = (traj << a.n) | loc;  // tile-local j -> gbase | (j & 2047) | (j >> 11) << u
+        word_or(j0, c, code);
+        word_or(j0 | (1 << pq), c, code);
+    };
+    const int t = threadIdx.x;
+    uint64_t traj = 0, loc = 0;
+    const uint64_t gbase = gn_tile_base(blockIdx.x, a.n, a.u, &traj, &loc);
     auto gidx = [&](int j) { return gbase | (uint64_t)(j & 2047) | ((uint64_t)(j >> 11) << a.u); };
-    // 1. the tile's loads, in flight during the walks
+    // 1. the tile's loads, in flight during the flip phase
     double2 r[16];
 #pragma unroll
     for (int k = 0; k < 16; ++k) r[k] = ld<true>(a.st + gidx(k * 256 + t));
@@ -470,46 +548,32 @@ __global__ __launch_bounds__(256) void k_gate_noise_tile(GnArgs a) {
 #pragma unroll
     for (int k = 0; k < 4; ++k) whi[k * 256 + t] = 0u;
     __syncthreads();
-    // 2. the prefix channels' flips: 8 blocks of 256 pairs per channel, one walk per thread
-    if (t < a.np * 8) {
-        const int c = t >> 3, jb = t & 7;
-        const FlipChan& ch = a.ch[c];
-        const int q = ch.target, pq = a.pq[c];
-        const uint64_t tl = gbase & ((1ull << a.n) - 1ull);  // trajectory-local base
-        // pair index (within the trajectory) of the tile's first pair of this channel
-        const uint64_t prb = ((tl >> (q + 1)) << q) | (tl & ((1ull << q) - 1ull));
-        uint64_t pr0;  // first pair of this walk's run
-        int run_base;  // tile pair-local index of that pair
-        if (q == a.u) {
-            pr0 = prb + (uint64_t)jb * 256;
-            run_base = jb * 256;
-        } else {  // two runs of 1024 pairs, bit u of the index -> pair bit u - 1
-            const int y = jb >> 2;
-            pr0 = prb + ((uint64_t)y << (a.u - 1)) + (uint64_t)(jb & 3) * 256;
-            run_base = (y << 10) + (jb & 3) * 256;
-        }
-        const uint64_t gb = (a.idx0 + (traj << (a.n - 1)) + pr0) >> kFlipBlockLog;
-        FlipCursor cur{nz_mix(ch.key ^ nz_mix(gb ^ kBlockSalt)), 0, -1, false};
-        uint64_t g = 0, h = 0;
-        const uint64_t lo = gb << kFlipBlockLog, hi = lo + kFlipBlock;
-        while (next_flip(cur, gb, lo, hi, ch, g, h)) {
-            uint32_t code = ch.type == 3 ? 1u : (ch.type == 4 ? 3u : 2u);
-            if (ch.type == 0) {
-                const float r2 = nz_uniform(nz_mix(h ^ 0x5bd1e9955bd1e995ull));
-                code = r2 < 1.0f / 3.0f ? 1u : (r2 < 2.0f / 3.0f ? 2u : 3u);
+    // 2. the prefix channels' flips into the code words
+    if (a.list) {
+        const uint16_t* L = a.list + (uint64_t)blockIdx.x * kGnMaxPrefix * (uint64_t)a.cap;
+        const uint32_t* C = a.cnt + (uint64_t)blockIdx.x * kGnMaxPrefix;
+        for (int sl = t; sl < a.np * a.cap; sl += 256) {
+            const int c = sl / a.cap, e = sl - c * a.cap;
+            if ((uint32_t)e < C[c]) {
+                const uint32_t w = L[(uint64_t)c * a.cap + e];
+                flip_or(c, (int)(w >> 2), w & 3u);
             }
-            const int x = run_base + (int)(g - lo);  // tile pair-local index
-            int j0;
-            if (pq == 11) {
-                j0 = x;
-            } else {
-                const int xl = x & 1023, y = x >> 10;
-                const int lo2 = xl & ((1 << pq) - 1);
-                j0 = (((xl ^ lo2) << 1) | lo2) | (y << 11);
-            }
-            word_or(j0, c, code);
-            word_or(j0 | (1 << pq), c, code);
         }
+        // (an overflowing list, > cap flips: that channel's blocks walked here, one per thread)
+        if (t < a.np * 8 && C[t >> 3] > (uint32_t)a.cap) {
+            const int c = t >> 3;
+            uint32_t k = 0;  // (the first cap flips of the channel are in the list: skip them)
+            int prior = 0;
+            for (int jb = 0; jb < (t & 7); ++jb)
+                gn_walk(a, c, jb, traj, gbase, [&](int, uint32_t) { ++prior; });
+            gn_walk(a, c, t & 7, traj, gbase, [&](int x, uint32_t code) {
+                if ((uint32_t)(prior + (int)k) >= (uint32_t)a.cap) flip_or(c, x, code);
+                ++k;
+            });
+        }
+    } else if (t < a.np * 8) {  // one walk per thread
+        const int c = t >> 3;
+        gn_walk(a, c, t & 7, traj, gbase, [&](int x, uint32_t code) { flip_or(c, x, code); });
     }
     // 3. registers -> LDS, the gate
 #pragma unroll
@@ -589,9 +653,11 @@ bool gate_noise_tile_supported(int n, const Op* op) {
     return true;
 }
 
-void launch_gate_noise_step(double2* st, int n, uint64_t batch, uint64_t traj0, const Op* op,
-                            const std::vector<NoiseChan>& chans, uint64_t seed, uint64_t& counter, hipStream_t s,
-                            Timer* tm) {
+// One step's kernel arguments: the gate and the prefix channels (keys from counter0, one counter
+// per channel entry whether it can fire or not, as the push kernels); *used: entries in the prefix
+// (the rest is the suffix).
+static GnArgs gn_args(double2* st, int n, uint64_t traj0, const Op* op, const std::vector<NoiseChan>& chans,
+                      uint64_t seed, uint64_t counter0, size_t* used_out) {
     GnArgs a{};
     a.st = st;
     a.n = n;
@@ -618,7 +684,7 @@ void launch_gate_noise_step(double2* st, int n, uint64_t batch, uint64_t traj0, 
     }
     // the prefix: channel entries in order whose qubit is in the tile (a channel that cannot fire
     // is skipped but still uses its counter, as the push kernels do)
-    uint64_t c = counter;
+    uint64_t c = counter0;
     size_t used = 0;
     const char* pe = std::getenv("QSIM_NOISE_TILE_PREFIX");  // (measurement: cap on the prefix)
     const size_t cap = pe ? (size_t)std::max(0, std::atoi(pe)) : chans.size();
@@ -635,17 +701,115 @@ void launch_gate_noise_step(double2* st, int n, uint64_t batch, uint64_t traj0, 
         }
         ++c;
     }
-    {
-        TimedLaunch tl(tm, "gate_noise", 32.0 * (double)(batch << n), s);
-        const uint64_t blocks = (batch << n) >> kGnTile;
-        hipLaunchKernelGGL(k_gate_noise_tile, dim3((unsigned)blocks), dim3(256), 0, s, a);
-        QSIM_HIPCHK(hipGetLastError());
-    }
-    counter = c;
+    *used_out = used;
+    return a;
+}
+
+static void launch_gn_tile(const GnArgs& a, uint64_t batch, hipStream_t s, Timer* tm) {
+    TimedLaunch tl(tm, "gate_noise", 32.0 * (double)(batch << a.n), s);
+    const uint64_t blocks = (batch << a.n) >> kGnTile;
+    hipLaunchKernelGGL(k_gate_noise_tile, dim3((unsigned)blocks), dim3(256), 0, s, a);
+    QSIM_HIPCHK(hipGetLastError());
+}
+
+void launch_gate_noise_step(double2* st, int n, uint64_t batch, uint64_t traj0, const Op* op,
+                            const std::vector<NoiseChan>& chans, uint64_t seed, uint64_t& counter, hipStream_t s,
+                            Timer* tm) {
+    size_t used = 0;
+    const GnArgs a = gn_args(st, n, traj0, op, chans, seed, counter, &used);
+    launch_gn_tile(a, batch, s, tm);
+    counter += used;
     if (used < chans.size()) {
         const std::vector<NoiseChan> rest(chans.begin() + (long)used, chans.end());
         launch_noise_after_gate(st, n, rest, seed, counter, s, tm, batch, traj0);
     }
+}
+
+// List capacity per (tile, channel) for the largest flip probability of `chans` (0: no lists —
+// above p ~ 0.1 the lists would outweigh the walks): mean 2048 P flips, cap = mean + 8 sigma + 16,
+// a multiple of 8; a list that overflows is walked by its tile kernel (exact either way).
+static int gn_list_cap(const std::vector<NoiseChan>& chans) {
+    double P = 0.0;
+    for (const NoiseChan& c : chans)
+        if (c.type == 0 || c.type >= 3) P = std::max(P, flip_probability(c.p));
+    if (!(P > 0.0)) return 0;
+    const char* e = std::getenv("QSIM_NOISE_LIST_CAP");  // (tests: a small cap forces overflows)
+    if (e && std::atoi(e) > 0) return (std::atoi(e) + 7) & ~7;
+    const double lam = 2048.0 * P;
+    const int cap = ((int)std::ceil(lam + 8.0 * std::sqrt(lam) + 16.0) + 7) & ~7;
+    return cap <= 256 ? cap : 0;
+}
+size_t gate_noise_lists_bytes(int n, uint64_t batch, const std::vector<NoiseChan>& chans) {
+    const char* e = std::getenv("QSIM_NOISE_TILE_LISTS");  // (read per run: 0 = walks in the tile kernel)
+    if (e && std::atoi(e) == 0) return 0;
+    const int cap = gn_list_cap(chans);
+    if (!cap || n < kGnTile) return 0;
+    const uint64_t tiles = (batch << n) >> kGnTile;
+    return (size_t)(tiles * kGnMaxPrefix * ((uint64_t)cap * sizeof(uint16_t) + sizeof(uint32_t)));
+}
+
+void launch_gate_noise_run(double2* st, int n, uint64_t batch, uint64_t traj0, const std::vector<Op>& ops,
+                           const std::vector<NoiseChan>& chans, uint64_t seed, uint64_t& counter, hipStream_t s,
+                           Timer* tm, const GnLists* L) {
+    const size_t G = ops.size(), nch = chans.size();
+    const uint64_t c0 = counter;
+    std::vector<GnArgs> args(G);
+    std::vector<size_t> used(G, 0);
+    for (size_t i = 0; i < G; ++i)
+        args[i] = gn_args(st, n, traj0, ops[i].kind >= 0 ? &ops[i] : nullptr, chans, seed, c0 + i * nch, &used[i]);
+    const int cap = L ? gn_list_cap(chans) : 0;
+    const uint64_t tiles = (batch << n) >> kGnTile;
+    const bool lists = L && cap && L->set_bytes >= (size_t)(tiles * kGnMaxPrefix *
+                                                            ((uint64_t)cap * sizeof(uint16_t) + sizeof(uint32_t)));
+    auto set_of = [&](size_t i, uint16_t** list, uint32_t** cnt) {
+        char* base = (char*)L->buf[i & 1];
+        *list = (uint16_t*)base;
+        *cnt = (uint32_t*)(base + tiles * kGnMaxPrefix * (uint64_t)cap * sizeof(uint16_t));
+    };
+    auto build = [&](size_t i) {
+        if (i >= 2) QSIM_HIPCHK(hipStreamWaitEvent(L->ms, L->used[i & 1], 0));  // tile kernel i - 2 done
+        GnArgs b = args[i];
+        b.cap = cap;
+        uint16_t* list = nullptr;
+        uint32_t* cnt = nullptr;
+        set_of(i, &list, &cnt);
+        if (b.np) {
+            const uint64_t threads = tiles * (uint64_t)b.np;
+            TimedLaunch tl(tm, "noise_lists", 0.0, L->ms);
+            hipLaunchKernelGGL(k_gn_lists, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, L->ms, b, list, cnt,
+                               tiles);
+            QSIM_HIPCHK(hipGetLastError());
+        }
+        QSIM_HIPCHK(hipEventRecord(L->built[i & 1], L->ms));
+    };
+    if (lists) {  // (the previous run's tile kernels may still read both sets)
+        QSIM_HIPCHK(hipEventRecord(L->start, s));
+        QSIM_HIPCHK(hipStreamWaitEvent(L->ms, L->start, 0));
+        for (size_t i = 0; i < std::min<size_t>(G, 2); ++i) build(i);
+    }
+    for (size_t i = 0; i < G; ++i) {
+        GnArgs a = args[i];
+        if (lists) {
+            QSIM_HIPCHK(hipStreamWaitEvent(s, L->built[i & 1], 0));
+            uint16_t* list = nullptr;
+            uint32_t* cnt = nullptr;
+            set_of(i, &list, &cnt);
+            a.list = list;
+            a.cnt = cnt;
+            a.cap = cap;
+        }
+        launch_gn_tile(a, batch, s, tm);
+        if (lists && i + 2 < G) {
+            QSIM_HIPCHK(hipEventRecord(L->used[i & 1], s));
+            build(i + 2);
+        }
+        uint64_t c = c0 + i * nch + used[i];
+        if (used[i] < nch) {
+            const std::vector<NoiseChan> rest(chans.begin() + (long)used[i], chans.end());
+            launch_noise_after_gate(st, n, rest, seed, c, s, tm, batch, traj0);
+        }
+    }
+    counter = c0 + G * nch;
 }
 
 // ---------------------------------------------------------------------------------------

@@ -175,7 +175,7 @@ class qsim_op(Structure):
 class qsim_dist_step(Structure):
     _fields_ = [("kind", c_int32), ("k", c_int32), ("op_begin", c_int32), ("op_end", c_int32),
                 ("gpos", c_int32 * 8), ("lpos", c_int32 * 8), ("pivot", c_int32), ("role", c_int32),
-                ("pmask", c_uint64)]
+                ("pmask", c_uint64), ("coarse", c_uint64)]
 
 
 class qsim_dist_post(Structure):
@@ -217,6 +217,11 @@ _sig(hip, "qsim_dist_plan", [c_int, c_int, c_int, POINTER(qsim_gate), c_size_t, 
 _sig(hip, "qsim_dist_plan_passes", [c_int, c_int, c_int, POINTER(qsim_gate), c_size_t,
                                     POINTER(c_int32), POINTER(c_int32), c_size_t, POINTER(c_size_t)])
 _sig(hip, "qsim_dist_plan_passes_carry", [c_int, c_int, c_int, POINTER(qsim_gate), c_size_t,
+                                          POINTER(c_int32), POINTER(c_uint64), POINTER(c_int32), c_size_t,
+                                          POINTER(c_size_t)])
+
+# ---- C++ API library (libqsim.so): circuit factories
+_sig(hip, "qsim_dist_plan_passes_coarse", [c_int, c_int, c_int, POINTER(qsim_gate), c_size_t,
                                           POINTER(c_int32), POINTER(c_uint64), POINTER(c_int32), c_size_t,
                                           POINTER(c_size_t)])
 

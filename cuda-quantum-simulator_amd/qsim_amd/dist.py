@@ -205,7 +205,7 @@ def plan(circuit: Circuit, world: int, rank: int, perm: Optional[List[int]] = No
     for s in steps[:ns.value]:
         if s.kind == 1:
             out_steps.append({"kind": "exchange", "k": s.k, "gpos": list(s.gpos[:s.k]),
-                              "lpos": list(s.lpos[:s.k]), "pivot": s.pivot, "pmask": s.pmask,
+                              "lpos": list(s.lpos[:s.k]), "pivot": s.pivot, "pmask": s.pmask, "coarse": s.coarse,
                               "pivots": [b for b in range(64) if (s.pmask >> b) & 1]})
         else:
             out_steps.append({"kind": "ops", "ops": out_ops[s.op_begin:s.op_end],

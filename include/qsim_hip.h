@@ -389,6 +389,7 @@ typedef struct qsim_dist_step {
     int32_t gpos[8], lpos[8];
     int32_t pivot, role;
     uint64_t pmask;
+    uint64_t coarse; /* exchange: pivots the step before's coarse passes leave untouched (0: none) */
 } qsim_dist_step;
 
 int qsim_dist_unique_id(void* id_out);  /* ncclGetUniqueId, on rank 0 */
@@ -461,6 +462,12 @@ int qsim_dist_plan_passes(int n_qubits, int world, int rank, const qsim_gate* ga
 int qsim_dist_plan_passes_carry(int n, int world, int rank, const qsim_gate* gates, size_t count,
                                 int32_t* perm_inout, uint64_t* carry_inout, int32_t* passes, size_t cap,
                                 size_t* n_steps);
+/* As qsim_dist_plan_passes_carry with five ints per step: passes, head, tail, then the coarse
+ * passes (those just ahead of the tail that run per coarse part, DStep::coarse / qsim_dist_step
+ * .coarse of the exchange after) and the number of coarse pivot bits. */
+int qsim_dist_plan_passes_coarse(int n, int world, int rank, const qsim_gate* gates, size_t count,
+                                 int32_t* perm_inout, uint64_t* carry_inout, int32_t* passes, size_t cap,
+                                 size_t* n_steps);
 
 /* Host-only: forget the process-wide memo of remap pivots (planning is then redone from scratch,
  * as in a fresh rank process). */

@@ -295,6 +295,33 @@ def test_gate_noise_tile_dense_flips_match_oracle(qsim, oracle, gpu_ready, monke
         np.testing.assert_allclose(s.getStateVector(t), whole[t], atol=1e-12, rtol=0)
 
 
+@pytest.mark.parametrize("lists,cap", [("1", "0"), ("1", "8"), ("0", "0")])
+def test_gate_noise_tile_lists_match_oracle(qsim, oracle, gpu_ready, monkeypatch, lists, cap):
+    """The flip lists built on the second stream one step ahead (k_gn_lists), at their natural
+    capacity, with a capacity of 8 (most lists overflow: the tile kernel walks the rest of those
+    blocks itself), and without lists; two runs (the list sets alternate across the run boundary),
+    a trajectory offset, a non-depolarizing flip channel in the prefix."""
+    monkeypatch.setenv("QSIM_NOISE_TILE", "1")
+    monkeypatch.setenv("QSIM_NOISE_TILE_LISTS", lists)
+    if cap != "0":
+        monkeypatch.setenv("QSIM_NOISE_LIST_CAP", cap)
+    n, B, seed, traj0, p = 13, 3, 41, 2, 0.03
+    c = _circuit(qsim, n, 15, seed)
+    nm = qsim.NoiseModel()
+    nm.addDepolarizingAll(n, p)
+    s = qsim.BatchedSimulator(n, B, nm, noise=qsim.BatchedNoise.Reference)
+    s.setSeed(seed)
+    s.setTrajectoryOffset(traj0)
+    entries = [(0, q, p) for q in range(n)]
+    whole, counter = None, 0
+    for _ in range(2):
+        s.run(c)
+        whole, counter = oracle.batched_reference_run(n, traj0 + B, oracle.gates_of(c), entries, seed,
+                                                      False, states=whole, counter=counter)
+    for t in range(B):
+        np.testing.assert_allclose(s.getStateVector(t), whole[traj0 + t], atol=1e-12, rtol=0)
+
+
 def test_gate_noise_tile_equals_push_16q(qsim, gpu_ready, monkeypatch):
     """Config-4 shape (16 qubits, depolarizing 0.01 on every qubit, W-HC and the mixed gate
     set): the tile kernel and gate kernel + push give bit-identical trajectories."""
