@@ -128,11 +128,17 @@ struct Gen {
             case S_TDG:
                 return "make_double2((" + a + ".x + " + a + ".y) * " + lit(c) + ", (-" + a + ".x + " + a +
                        ".y) * " + lit(c) + ")";
-            default: return "qcm(" + lit(t.m[2]) + ", " + lit(t.m[3]) + ", " + a + ")";
+            default: return scale(t.m[2], t.m[3], a);
         }
     }
-    std::string diag0(const TileOp& t, const std::string& a) {
-        return "qcm(" + lit(t.m[0]) + ", " + lit(t.m[1]) + ", " + a + ")";
+    std::string diag0(const TileOp& t, const std::string& a) { return scale(t.m[0], t.m[1], a); }
+    // (mr + i mi) * a; a real factor (the density-matrix channels' scales) as two multiplies
+    // instead of a complex product whose zero imaginary part the compiler cannot drop (IEEE)
+    static std::string scale(double mr, double mi, const std::string& a) {
+        if (mi != 0.0) return "qcm(" + lit(mr) + ", " + lit(mi) + ", " + a + ")";
+        if (mr == 1.0) return a;
+        if (mr == -1.0) return "make_double2(-" + a + ".x, -" + a + ".y)";
+        return "make_double2(" + lit(mr) + " * " + a + ".x, " + lit(mr) + " * " + a + ".y)";
     }
 
     void op(const TileOp& t) {
@@ -201,7 +207,16 @@ struct Gen {
                     break;
                 default: break;  // S_GEN: below
             }
-            if (t.sub == S_GEN) {  // double2 has no operator+ here: expand the sums
+            const bool real = t.m[1] == 0.0 && t.m[3] == 0.0 && t.m[5] == 0.0 && t.m[7] == 0.0;
+            if (t.sub == S_GEN && real) {  // a real 2x2 (density-matrix bit flip / damping): 4 FMA-able terms
+                auto lin = [&](int i, int j) {
+                    const std::string ma = lit(t.m[2 * i]), mb = lit(t.m[2 * j]);
+                    return "make_double2(" + ma + " * t0.x + " + mb + " * t1.x, " + ma + " * t0.y + " + mb + " * t1.y)";
+                };
+                o << "  { const double2 t0 = " << a0 << ", t1 = " << a1 << ";\n";
+                x0 = lin(0, 1);
+                x1 = lin(2, 3);
+            } else if (t.sub == S_GEN) {  // double2 has no operator+ here: expand the sums
                 auto sum = [](const std::string& a, const std::string& b) {
                     return "make_double2(" + a + ".x + " + b + ".x, " + a + ".y + " + b + ".y)";
                 };
@@ -213,7 +228,7 @@ struct Gen {
                   << "    const double2 w0 = " << cm(2, "t0") << ", w1 = " << cm(3, "t1") << ";\n";
                 x0 = sum("u0", "u1");
                 x1 = sum("w0", "w1");
-            } else {
+            } else if (t.sub != S_GEN) {
                 o << "  { const double2 t0 = " << a0 << ", t1 = " << a1 << ";\n";
             }
             if (!pred.empty()) {

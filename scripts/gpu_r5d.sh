@@ -26,3 +26,7 @@ grep "carry merges" $O/pytest_dist.log
 cd /tmp && timeout -k 10 400 rocprofv3 --marker-trace --kernel-trace --stats --output-format csv -d $O/prof_hc -o hc -- python3 $R/bench.py --cpu-budget 0 --profile-region hc --steps 20 --warmup 2 --no-1q28 --no-batch16 --no-extras > $O/bench_hc.json 2> $O/bench_hc.err || { tail -5 $O/bench_hc.err; exit 1; }
 cd $R
 python3 scripts/roofline_check.py hc $O/bench_hc.json $O/prof_hc/hc_kernel_trace.csv $O/check_hc.json --markers=$O/prof_hc/hc_marker_api_trace.csv | grep -E "frac|launches|avg|median"
+timeout -k 10 600 $PT -x tests/test_density.py tests/test_jit.py > $O/pytest_dm.log 2>&1 || { tail -30 $O/pytest_dm.log; exit 1; }
+tail -2 $O/pytest_dm.log
+timeout -k 10 300 python -u bench.py --workload dm --cpu-budget 0 --steps 5 > $O/dm.json 2> $O/dm.err || { tail -5 $O/dm.err; exit 1; }
+python3 -c "import json;d=json.load(open('$O/dm.json'));print('dm', d['value'], d['ms_per_step'], d['roofline'])"
