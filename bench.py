@@ -157,7 +157,10 @@ def cpu_baseline(circuit, n, budget, q=None, args=None):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import numpy_oracle as orc  # test infrastructure: the CPU baseline leg only
     gates = orc.gates_of(circuit)
-    done, secs = orc.time_prefix(n, gates, budget)
+    # median of >= 3 runs — three prefix runs of budget / 3 each, median rate
+    runs_n = [orc.time_prefix(n, gates, budget / 3.0) for _ in range(3)]
+    rates_n = sorted(d / s for d, s in runs_n if s > 0)
+    done, secs = runs_n[0]
     full20 = None
     if q is not None and args is not None and args.workload == "hc":
         # BASELINE.md §3 plan: the same W-HC circuit at 20 qubits, whole runs, median of 3
@@ -177,11 +180,14 @@ def cpu_baseline(circuit, n, budget, q=None, args=None):
     if q is not None and args is not None and args.workload == "hc" and budget > 0:
         # BASELINE.md §3 plan: the same circuit family at 28 qubits (config 3), a prefix of it
         c28 = q.createRandomHCCircuit(28, args.depth, args.seed)
-        d28, s28 = orc.time_prefix(28, orc.gates_of(c28), min(budget, 8.0))
-        if d28 and s28 > 0:
-            pre28 = {"value": round(d28 / s28, 3), "unit": "gates/s", "cores": 1, "kind": "port",
-                     "sample": f"prefix-extrapolated: first {d28} gates of W-HC depth {args.depth} seed "
-                               f"{args.seed} at 28 qubits, one run, single thread, {s28:.1f} s"}
+        g28 = orc.gates_of(c28)
+        r28 = [orc.time_prefix(28, g28, min(budget, 9.0) / 3.0) for _ in range(3)]
+        v28 = sorted(d / s for d, s in r28 if d and s > 0)
+        if v28:
+            pre28 = {"value": round(v28[len(v28) // 2], 3), "unit": "gates/s", "cores": 1, "kind": "port",
+                     "sample": f"prefix-extrapolated: W-HC depth {args.depth} seed {args.seed} at 28 qubits, "
+                               f"median of 3 prefix runs ({', '.join(str(d) for d, _ in r28)} gates in "
+                               f"{', '.join(f'{s:.1f}' for _, s in r28)} s), single thread"}
     cpu_model = "unknown"
     try:
         with open("/proc/cpuinfo") as f:
@@ -191,11 +197,12 @@ def cpu_baseline(circuit, n, budget, q=None, args=None):
                     break
     except OSError:
         pass
-    return {"value": done / secs if secs > 0 else None, "unit": "gates/s", "cores": 1,
+    return {"value": rates_n[len(rates_n) // 2] if rates_n else None, "unit": "gates/s", "cores": 1,
             "kind": "port", "w_hc_20q": full20, "w_hc_28q": pre28,
-            "sample": f"prefix-extrapolated: first {done} gates of the same circuit at n={n}, one "
-                      f"run, single thread, {secs:.1f} s ({cpu_model}; host has {os.cpu_count()} "
-                      f"logical CPUs); value = prefix gates / prefix time"}
+            "sample": f"prefix-extrapolated: median of 3 prefix runs of the same circuit at n={n} "
+                      f"({', '.join(str(d) for d, _ in runs_n)} gates in "
+                      f"{', '.join(f'{s:.1f}' for _, s in runs_n)} s), single thread ({cpu_model}; host "
+                      f"has {os.cpu_count()} logical CPUs); value = median of prefix gates / prefix time"}
 
 
 def run_single(args):
@@ -555,15 +562,45 @@ def measure_noisy(q, n, steps, warmup, seed, depth, p_noise):
             sim.synchronize()
         ts.append(time.perf_counter() - t0)
     stats = sv.profileStats()
+    # The pulled path builds the next step's code words (noise_map) on a second stream beside the
+    # pull pass, so their HIP-event spans overlap and each includes time shared with the other
+    # kernel.  One more run with the map on the main stream (QSIM_NOISE_MAP_OVERLAP=0, same states)
+    # gives each kernel's own duration: the kernel table and the rooflines come from that run.
+    prev = os.environ.get("QSIM_NOISE_MAP_OVERLAP")
+    os.environ["QSIM_NOISE_MAP_OVERLAP"] = "0"
+    try:
+        sim.reset()
+        sim.synchronize()
+        sv.profileReset()
+        sim.run(c)
+        sim.synchronize()
+        serial = sv.profileStats()
+    finally:
+        if prev is None:
+            os.environ.pop("QSIM_NOISE_MAP_OVERLAP", None)
+        else:
+            os.environ["QSIM_NOISE_MAP_OVERLAP"] = prev
     sv.profile(False)
     del sim
     med = _median(ts)
-    noise = [s for s in stats if s["name"] == "noise"]
+    # the noise kernels: the per-channel passes (push) or the pull pass, which applies the flips
+    # of the step before while it applies the gate (its bytes: one read + one write of the state
+    # plus the code words), with its PMC traffic (profiles/pmc_noisy_26q.json)
+    noise = [s for s in serial if s["name"] in ("noise", "pull_gate")]
+    noise_roof = _dominant_roofline(noise) if noise else None
+    pmc_path = os.path.join(ROOT, "profiles", f"pmc_noisy_{n}q.json")
+    if noise_roof and os.path.exists(pmc_path):
+        with open(pmc_path) as f:
+            ent = json.load(f).get("kernels", {}).get(noise_roof["kernel"], {})
+        noise_roof["traffic"] = ent.get("hbm_bytes_per_launch")
+        noise_roof["traffic_source"] = os.path.relpath(pmc_path, ROOT) if noise_roof["traffic"] else None
     return {"workload": f"NoisySimulator {n} qubits, W-HC depth {depth} seed {seed}, depolarizing "
                         f"{p_noise} on all qubits after every gate ({n} channel passes per gate)",
             "value": round(c.getGateCount() / med, 1), "unit": "gates/s", "ms_per_step": round(med * 1e3, 3),
-            "roofline": _dominant_roofline(stats),
-            "noise_roofline": _dominant_roofline(noise) if noise else None, "kernels": stats}
+            "roofline": _dominant_roofline(serial), "noise_roofline": noise_roof,
+            "kernels": serial, "kernels_note": "per-kernel durations from one run with the code-word map "
+                                               "on the main stream (no overlap); the timed runs overlap it",
+            "kernels_overlapped": stats}
 
 
 def roofline_1q28(q, steps=3):

@@ -610,34 +610,59 @@ __global__ __launch_bounds__(256) void k_gate_noise_tile(GnArgs a) {
         }
         __syncthreads();
     }
-    // 4. out[k] = (P v)[k], pulled through the code words, stored in place
-#pragma unroll 4
+    // 4. out[k] = (P v)[k], pulled through the code words, stored in place.  The walks of a
+    // thread's 16 amplitudes advance in lockstep (one step of every unfinished walk per round, the
+    // word loads of a round independent), so LDS latency is paid once per round, not per step of
+    // every amplitude (in a wave some lane almost always has a non-zero word).
+    int jj[16], ee[16];
+    uint32_t ww[16];
+#pragma unroll
     for (int k0 = 0; k0 < 16; ++k0) {
-        const int k = k0 * 256 + t;
-        uint32_t w = word_at(k);
-        int j = k, e = 0;
-        while (w) {
-            const int c = (31 - __builtin_clz(w)) >> 1;  // the last channel that flips j's pair
+        jj[k0] = k0 * 256 + t;
+        ee[k0] = 0;
+        ww[k0] = word_at(jj[k0]);
+    }
+    for (;;) {
+        uint32_t any = 0;
+#pragma unroll
+        for (int k0 = 0; k0 < 16; ++k0) any |= ww[k0];
+        if (!any) break;
+        bool mv[16];
+        uint32_t keep[16];
+#pragma unroll
+        for (int k0 = 0; k0 < 16; ++k0) {
+            mv[k0] = false;
+            keep[k0] = 0u;
+            const uint32_t w = ww[k0];
+            if (!w) continue;
+            const int c = (31 - __builtin_clz(w)) >> 1;  // the last channel that flips jj's pair
             const uint32_t code = (w >> (2 * c)) & 3u;
-            const int bit = (j >> a.pq[c]) & 1;
-            w &= (1u << (2 * c)) - 1u;  // the channels before it
-            if (code == 3u) {           // Z: -1 on the |1> member
-                e += 2 * bit;
-            } else {                    // X: partner; Y: partner with -i (|0> member) / +i (|1>)
-                if (code == 2u) e += bit ? 1 : 3;
-                j ^= 1 << a.pq[c];
-                w = word_at(j) & ((1u << (2 * c)) - 1u);
+            const int bit = (jj[k0] >> a.pq[c]) & 1;
+            keep[k0] = (1u << (2 * c)) - 1u;  // the channels before it
+            ww[k0] = w & keep[k0];
+            if (code == 3u) {  // Z: -1 on the |1> member
+                ee[k0] += 2 * bit;
+            } else {           // X: partner; Y: partner with -i (|0> member) / +i (|1>)
+                if (code == 2u) ee[k0] += bit ? 1 : 3;
+                jj[k0] ^= 1 << a.pq[c];
+                mv[k0] = true;
             }
         }
-        const double2 x = v[j];
+#pragma unroll
+        for (int k0 = 0; k0 < 16; ++k0)
+            if (mv[k0]) ww[k0] = word_at(jj[k0]) & keep[k0];
+    }
+#pragma unroll
+    for (int k0 = 0; k0 < 16; ++k0) {
+        const double2 x = v[jj[k0]];
         double2 y;
-        switch (e & 3) {
+        switch (ee[k0] & 3) {
             case 0: y = x; break;
             case 1: y = make_double2(-x.y, x.x); break;   // i
             case 2: y = make_double2(-x.x, -x.y); break;  // -1
             default: y = make_double2(x.y, -x.x); break;  // -i
         }
-        st<true>(a.st + gidx(k), y);
+        st<true>(a.st + gidx(k0 * 256 + t), y);
     }
 }
 

@@ -21,6 +21,7 @@ LABELS = [("k_fused_staged", "fused_tile"), ("k_fused_tile", "fused_tile"),
           ("k_swap_hh", "swap_hh"), ("k_swap_lh", "swap_lh"), ("k_swap_ll", "swap_ll"),
           ("k_pauli_apply", "pauli_apply"), ("k_exchange_copy", "alltoall_remap"),
           ("k_noise_units", "noise"), ("k_noise_flips", "noise"),
+          ("k_gate_noise_tile", "gate_noise"), ("k_gn_lists", "noise_lists"),
           ("k_pull_gate", "pull_gate"), ("k_noise_map", "noise_map"), ("k_noise_words", "noise_map"),
           ("qk", "fused_tile")]  # circuit-specialised pass kernels (jit.hip) are named qk<pass>
 
