@@ -428,6 +428,7 @@ struct GnArgs {
     double2 m[4];
     int np;                // prefix channels
     int pq[kGnMaxPrefix];  // tile-local position of each prefix channel's qubit
+    uint64_t pqpack;       // the same, 4 bits per channel (a per-lane channel index then costs no load)
     FlipChan ch[kGnMaxPrefix];
     // precomputed flip lists of this step (k_gn_lists, built on a second stream during the step
     // before), or null: the work-group walks the blocks itself.  Per tile and prefix channel, cap
@@ -521,9 +522,12 @@ __global__ __launch_bounds__(256) void k_gate_noise_tile(GnArgs a) {
     auto word_at = [&](int j) {
         return ((wlo[j >> 1] >> (16 * (j & 1))) & 0xffffu) | (((whi[j >> 2] >> (8 * (j & 3))) & 0xffu) << 16);
     };
+    // tile-local position of prefix channel c's qubit (c may differ between lanes: unpacked from
+    // a kernel argument, not indexed out of the argument block)
+    auto pq_of = [&](int c) { return (int)((a.pqpack >> (4 * c)) & 15ull); };
     // a flip of prefix channel c on tile pair-local pair x: its code into both members' words
     auto flip_or = [&](int c, int x, uint32_t code) {
-        const int pq = a.pq[c];
+        const int pq = pq_of(c);
         int j0;
         if (pq == 11) {
             j0 = x;
@@ -637,14 +641,15 @@ __global__ __launch_bounds__(256) void k_gate_noise_tile(GnArgs a) {
             if (!w) continue;
             const int c = (31 - __builtin_clz(w)) >> 1;  // the last channel that flips jj's pair
             const uint32_t code = (w >> (2 * c)) & 3u;
-            const int bit = (jj[k0] >> a.pq[c]) & 1;
+            const int pqc = pq_of(c);
+            const int bit = (jj[k0] >> pqc) & 1;
             keep[k0] = (1u << (2 * c)) - 1u;  // the channels before it
             ww[k0] = w & keep[k0];
             if (code == 3u) {  // Z: -1 on the |1> member
                 ee[k0] += 2 * bit;
             } else {           // X: partner; Y: partner with -i (|0> member) / +i (|1>)
                 if (code == 2u) ee[k0] += bit ? 1 : 3;
-                jj[k0] ^= 1 << a.pq[c];
+                jj[k0] ^= 1 << pqc;
                 mv[k0] = true;
             }
         }
@@ -722,6 +727,7 @@ static GnArgs gn_args(double2* st, int n, uint64_t traj0, const Op* op, const st
             if (a.np == kGnMaxPrefix) break;  // (the rest goes to the push kernel)
             flip_channel(ch.type, ch.qubit, ch.p, noise_key(seed, c), a.ch[a.np]);
             a.pq[a.np] = ch.qubit <= 10 ? ch.qubit : 11;
+            a.pqpack |= (uint64_t)a.pq[a.np] << (4 * a.np);
             ++a.np;
         }
         ++c;
