@@ -435,7 +435,7 @@ struct GnArgs {
     // entries (tile pair-local index << 2 | code) and the flip count (> cap: overflow, walked here)
     const uint16_t* list;
     const uint32_t* cnt;
-    int cap;
+    int cap, lcap;         // cap = 2^lcap
 };
 __device__ __forceinline__ int gn_local_pos(int q, int u) { return q <= 10 ? q : (q == u ? 11 : -1); }
 
@@ -539,14 +539,23 @@ __global__ __launch_bounds__(256) void k_gate_noise_tile(GnArgs a) {
         word_or(j0, c, code);
         word_or(j0 | (1 << pq), c, code);
     };
+    __shared__ uint32_t cnt_s[kGnMaxPrefix];
     const int t = threadIdx.x;
     uint64_t traj = 0, loc = 0;
     const uint64_t gbase = gn_tile_base(blockIdx.x, a.n, a.u, &traj, &loc);
     auto gidx = [&](int j) { return gbase | (uint64_t)(j & 2047) | ((uint64_t)(j >> 11) << a.u); };
-    // 1. the tile's loads, in flight during the flip phase
+    // 1. the tile's loads, and this tile's flip lists, all in flight during the flip phase
     double2 r[16];
 #pragma unroll
     for (int k = 0; k < 16; ++k) r[k] = ld<true>(a.st + gidx(k * 256 + t));
+    constexpr int kSlots = kGnMaxPrefix;  // list slots per thread: np * cap <= 12 * 256
+    uint16_t le[kSlots];
+    const int nsl = a.list ? a.np << a.lcap : 0;  // slots of this tile (cap = 2^lcap per channel)
+    const uint16_t* L = a.list + (uint64_t)blockIdx.x * kGnMaxPrefix * (uint64_t)(1u << a.lcap);
+    const uint32_t* C = a.cnt + (uint64_t)blockIdx.x * kGnMaxPrefix;
+#pragma unroll
+    for (int k = 0; k < kSlots; ++k) le[k] = k * 256 + t < nsl ? L[k * 256 + t] : (uint16_t)0;
+    if (a.list && t < a.np) cnt_s[t] = C[t];
 #pragma unroll
     for (int k = 0; k < 8; ++k) wlo[k * 256 + t] = 0u;
 #pragma unroll
@@ -554,17 +563,15 @@ __global__ __launch_bounds__(256) void k_gate_noise_tile(GnArgs a) {
     __syncthreads();
     // 2. the prefix channels' flips into the code words
     if (a.list) {
-        const uint16_t* L = a.list + (uint64_t)blockIdx.x * kGnMaxPrefix * (uint64_t)a.cap;
-        const uint32_t* C = a.cnt + (uint64_t)blockIdx.x * kGnMaxPrefix;
-        for (int sl = t; sl < a.np * a.cap; sl += 256) {
-            const int c = sl / a.cap, e = sl - c * a.cap;
-            if ((uint32_t)e < C[c]) {
-                const uint32_t w = L[(uint64_t)c * a.cap + e];
-                flip_or(c, (int)(w >> 2), w & 3u);
-            }
+#pragma unroll
+        for (int k = 0; k < kSlots; ++k) {
+            const int sl = k * 256 + t;
+            if (sl >= nsl) break;
+            const int c = sl >> a.lcap, e = sl & ((1 << a.lcap) - 1);
+            if ((uint32_t)e < cnt_s[c]) flip_or(c, (int)(le[k] >> 2), le[k] & 3u);
         }
         // (an overflowing list, > cap flips: that channel's blocks walked here, one per thread)
-        if (t < a.np * 8 && C[t >> 3] > (uint32_t)a.cap) {
+        if (t < a.np * 8 && cnt_s[t >> 3] > (uint32_t)a.cap) {
             const int c = t >> 3;
             uint32_t k = 0;  // (the first cap flips of the channel are in the list: skip them)
             int prior = 0;
@@ -757,17 +764,23 @@ void launch_gate_noise_step(double2* st, int n, uint64_t batch, uint64_t traj0, 
 }
 
 // List capacity per (tile, channel) for the largest flip probability of `chans` (0: no lists —
-// above p ~ 0.1 the lists would outweigh the walks): mean 2048 P flips, cap = mean + 8 sigma + 16,
-// a multiple of 8; a list that overflows is walked by its tile kernel (exact either way).
+// above p ~ 0.1 the lists would outweigh the walks): mean 2048 P flips, cap = the power of two
+// >= mean + 6 sigma + 8 (p = 0.01: 64; P(overflow) ~ 1e-12 per list); a list that overflows is
+// walked by its tile kernel (exact either way).
 static int gn_list_cap(const std::vector<NoiseChan>& chans) {
     double P = 0.0;
     for (const NoiseChan& c : chans)
         if (c.type == 0 || c.type >= 3) P = std::max(P, flip_probability(c.p));
     if (!(P > 0.0)) return 0;
+    auto pow2 = [](int x) {
+        int c = 8;
+        while (c < x) c <<= 1;
+        return c;
+    };
     const char* e = std::getenv("QSIM_NOISE_LIST_CAP");  // (tests: a small cap forces overflows)
-    if (e && std::atoi(e) > 0) return (std::atoi(e) + 7) & ~7;
+    if (e && std::atoi(e) > 0) return pow2(std::atoi(e));
     const double lam = 2048.0 * P;
-    const int cap = ((int)std::ceil(lam + 8.0 * std::sqrt(lam) + 16.0) + 7) & ~7;
+    const int cap = pow2((int)std::ceil(lam + 6.0 * std::sqrt(lam) + 8.0));
     return cap <= 256 ? cap : 0;
 }
 size_t gate_noise_lists_bytes(int n, uint64_t batch, const std::vector<NoiseChan>& chans) {
@@ -801,6 +814,7 @@ void launch_gate_noise_run(double2* st, int n, uint64_t batch, uint64_t traj0, c
         if (i >= 2) QSIM_HIPCHK(hipStreamWaitEvent(L->ms, L->used[i & 1], 0));  // tile kernel i - 2 done
         GnArgs b = args[i];
         b.cap = cap;
+        b.lcap = __builtin_ctz((unsigned)cap);
         uint16_t* list = nullptr;
         uint32_t* cnt = nullptr;
         set_of(i, &list, &cnt);
@@ -828,6 +842,7 @@ void launch_gate_noise_run(double2* st, int n, uint64_t batch, uint64_t traj0, c
             a.list = list;
             a.cnt = cnt;
             a.cap = cap;
+            a.lcap = __builtin_ctz((unsigned)cap);
         }
         launch_gn_tile(a, batch, s, tm);
         if (lists && i + 2 < G) {
