@@ -436,6 +436,8 @@ struct GnArgs {
     const uint16_t* list;
     const uint32_t* cnt;
     int cap, lcap;         // cap = 2^lcap
+    int skip;              // QSIM_NOISE_TILE_SKIP (measurement only, wrong states): 1 no flip
+                           // codes written, 2 no pulled walks (outputs read in place), 3 both
 };
 __device__ __forceinline__ int gn_local_pos(int q, int u) { return q <= 10 ? q : (q == u ? 11 : -1); }
 
@@ -562,7 +564,8 @@ __global__ __launch_bounds__(256) void k_gate_noise_tile(GnArgs a) {
     for (int k = 0; k < 4; ++k) whi[k * 256 + t] = 0u;
     __syncthreads();
     // 2. the prefix channels' flips into the code words
-    if (a.list) {
+    if (a.skip & 1) {
+    } else if (a.list) {
 #pragma unroll
         for (int k = 0; k < kSlots; ++k) {
             const int sl = k * 256 + t;
@@ -634,6 +637,7 @@ __global__ __launch_bounds__(256) void k_gate_noise_tile(GnArgs a) {
         ww[k0] = word_at(jj[k0]);
     }
     for (;;) {
+        if (a.skip & 2) break;
         uint32_t any = 0;
 #pragma unroll
         for (int k0 = 0; k0 < 16; ++k0) any |= ww[k0];
@@ -740,6 +744,8 @@ static GnArgs gn_args(double2* st, int n, uint64_t traj0, const Op* op, const st
         ++c;
     }
     *used_out = used;
+    const char* sk = std::getenv("QSIM_NOISE_TILE_SKIP");  // (measurement only)
+    a.skip = sk ? std::atoi(sk) : 0;
     return a;
 }
 
