@@ -1535,6 +1535,29 @@ int qsim_dm_run(qsim_state* s, int n, const qsim_gate* gates, size_t count,
     });
 }
 
+int qsim_dm_plan_info(int n, const qsim_gate* gates, size_t count, const qsim_noise_channel* channels,
+                      size_t n_channels, int flags, int32_t* info, size_t cap, size_t* n_passes) {
+    return guarded([&] {
+        if (n < 1 || n > QSIM_DM_MAX_QUBITS) fail(QSIM_ERR_INVALID_ARGUMENT, "bad qubit count");
+        QSIM_REQUIRE(gates || count == 0, QSIM_ERR_INVALID_ARGUMENT, "null gate list");
+        QSIM_REQUIRE(channels || n_channels == 0, QSIM_ERR_INVALID_ARGUMENT, "null channel list");
+        std::vector<Op> ops;
+        dm_lower(n, gates, count, channels, n_channels, ops, (flags & QSIM_DM_REFERENCE_Y) != 0);
+        const Plan plan = plan_fused(ops, 2 * n);  // (as qsim_dm_run's run_fused plans it)
+        for (size_t p = 0; p < plan.passes.size() && p < cap && info; ++p) {
+            const FusedPass& fp = plan.passes[p];
+            int nops = 0;
+            for (int st = fp.stage_begin; st < fp.stage_end; ++st) nops += plan.stages[st].op_end - plan.stages[st].op_begin;
+            if (fp.stage_end == fp.stage_begin) nops = fp.op_end - fp.op_begin;
+            info[4 * p] = fp.single >= 0 ? -1 : fp.h;
+            info[4 * p + 1] = nops;
+            info[4 * p + 2] = fp.stage_end - fp.stage_begin;
+            info[4 * p + 3] = fp.r0;
+        }
+        if (n_passes) *n_passes = plan.passes.size();
+    });
+}
+
 int qsim_dm_apply_channel(qsim_state* s, int n, int type, int qubit, double p) {
     return guarded([&] {
         check_dm(s, n);

@@ -158,6 +158,8 @@ _sig(hip, "qsim_noise_check_flips", [POINTER(c_uint64)])
 _sig(hip, "qsim_noisy_run", [_P, POINTER(qsim_gate), c_size_t, POINTER(qsim_noise_channel), c_size_t,
                              c_uint64, POINTER(c_uint64), c_int])
 
+_sig(hip, "qsim_dm_plan_info", [c_int, POINTER(qsim_gate), c_size_t, POINTER(qsim_noise_channel), c_size_t,
+                                  c_int, POINTER(c_int32), c_size_t, POINTER(c_size_t)])
 _sig(hip, "qsim_dm_run", [_P, c_int, POINTER(qsim_gate), c_size_t, POINTER(qsim_noise_channel),
                           c_size_t, c_int])
 _sig(hip, "qsim_dm_apply_channel", [_P, c_int, c_int, c_int, c_double])

@@ -352,6 +352,11 @@ int qsim_noisy_run(qsim_state* s, const qsim_gate* gates, size_t count,
 #define QSIM_DM_REFERENCE_Y 8
 int qsim_dm_run(qsim_state* rho, int n_qubits, const qsim_gate* gates, size_t count,
                 const qsim_noise_channel* channels, size_t n_channels, int flags);
+/* Host-only: the fused plan qsim_dm_run (QSIM_RUN_FUSED) would run for this circuit, four ints
+ * per pass: tile height h (tile = 64 << h elements; -1: a per-gate step), ops, register stages,
+ * contiguous run bits r0. */
+int qsim_dm_plan_info(int n_qubits, const qsim_gate* gates, size_t count, const qsim_noise_channel* channels,
+                      size_t n_channels, int flags, int32_t* info, size_t cap, size_t* n_passes);
 /* One channel (applyDepolarizing ... applyBitPhaseFlip, :298-356) on `qubit`. */
 int qsim_dm_apply_channel(qsim_state* rho, int n_qubits, int type, int qubit, double p);
 int qsim_dm_diagonal(qsim_state* rho, int n_qubits, double* dst);          /* 2^n: Re rho_ii */
