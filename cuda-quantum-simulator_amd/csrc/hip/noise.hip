@@ -546,18 +546,21 @@ __global__ __launch_bounds__(256) void k_gate_noise_tile(GnArgs a) {
     uint64_t traj = 0, loc = 0;
     const uint64_t gbase = gn_tile_base(blockIdx.x, a.n, a.u, &traj, &loc);
     auto gidx = [&](int j) { return gbase | (uint64_t)(j & 2047) | ((uint64_t)(j >> 11) << a.u); };
-    // 1. the tile's loads, and this tile's flip lists, all in flight during the flip phase
-    double2 r[16];
-#pragma unroll
-    for (int k = 0; k < 16; ++k) r[k] = ld<true>(a.st + gidx(k * 256 + t));
+    // 1. this tile's flip lists, then the tile's loads, all in flight during the flip phase (the
+    // lists first: the flip phase then waits only for them — loads retire in order)
     constexpr int kSlots = kGnMaxPrefix;  // list slots per thread: np * cap <= 12 * 256
     uint16_t le[kSlots];
     const int nsl = a.list ? a.np << a.lcap : 0;  // slots of this tile (cap = 2^lcap per channel)
     const uint16_t* L = a.list + (uint64_t)blockIdx.x * kGnMaxPrefix * (uint64_t)(1u << a.lcap);
     const uint32_t* C = a.cnt + (uint64_t)blockIdx.x * kGnMaxPrefix;
+    uint32_t cl = 0;
+    if (a.list && t < a.np) cl = C[t];
 #pragma unroll
     for (int k = 0; k < kSlots; ++k) le[k] = k * 256 + t < nsl ? L[k * 256 + t] : (uint16_t)0;
-    if (a.list && t < a.np) cnt_s[t] = C[t];
+    double2 r[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) r[k] = ld<true>(a.st + gidx(k * 256 + t));
+    if (a.list && t < a.np) cnt_s[t] = cl;
 #pragma unroll
     for (int k = 0; k < 8; ++k) wlo[k * 256 + t] = 0u;
 #pragma unroll
