@@ -24,8 +24,6 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
-#include <map>
-#include <mutex>
 #include <string>
 
 #include "device_ops.hpp"
@@ -72,8 +70,7 @@ struct FlipChan {
     int target;
     int type;    // 0 depolarizing, 3 X, 4 Z, 5 Y
     int always;  // P == 1: every pair flips
-    float inv_l2q;       // 1 / log2(1 - P) (< 0): the gap estimate
-    const uint64_t* thr; // gap thresholds of P (flip_table): thr[k] = floor((1 - P)^k 2^53), k <= 256
+    int pad;
 };
 // Next flip of a block's walk inside [lo, hi): false when the block is exhausted.
 struct FlipCursor {
@@ -89,15 +86,9 @@ __device__ __forceinline__ bool next_flip(FlipCursor& cur, uint64_t b, uint64_t 
         if (c.always) {
             cur.pos += 1;
         } else {
-            // gap = the largest k <= 256 with u1 <= thr[k] (u = u1 2^-53 uniform in (0, 1]:
-            // P(gap >= k) = (1 - P)^k up to 2^-53): a float log2 estimate corrected exactly on
-            // the integer thresholds (round 5; a double log and division per draw before)
-            const uint64_t u1 = (h >> 11) + 1ull;
-            const float est = (__log2f((float)u1) - 53.0f) * c.inv_l2q;
-            int gap = est >= 256.0f ? 256 : (est > 0.0f ? (int)est : 0);
-            while (gap < (int)kFlipBlock && u1 <= c.thr[gap + 1]) ++gap;
-            while (gap > 0 && u1 > c.thr[gap]) --gap;
-            if (gap >= (int)kFlipBlock) {
+            const double u = (double)((h >> 11) + 1ull) * 0x1.0p-53;  // (0, 1]
+            const double gap = floor(log(u) / c.lq);
+            if (gap >= (double)kFlipBlock) {
                 cur.done = true;
                 break;
             }
@@ -290,32 +281,6 @@ static void check_channel(int n, int type, int qubit, double p) {
     if (!std::isfinite(p)) fail(QSIM_ERR_INVALID_ARGUMENT, "noise probability must be finite");
 }
 
-// Gap thresholds of flip probability P (0 < P < 1): thr[0] = 2^53, thr[k] = floor((1 - P)^k 2^53)
-// for k = 1..256, computed in double with the host libm (oracle/numpy_oracle.py flip_thresholds
-// computes the same table the same way).  One device copy per (device, P), kept for the process.
-constexpr int kFlipThr = (int)kFlipBlock + 1;
-static void flip_thresholds(double P, uint64_t* thr) {
-    const double lq = std::log1p(-P);
-    thr[0] = 1ull << 53;
-    for (int k = 1; k < kFlipThr; ++k) thr[k] = (uint64_t)std::floor(std::ldexp(std::exp((double)k * lq), 53));
-}
-static const uint64_t* flip_table(double P) {
-    static std::mutex mu;
-    static std::map<std::pair<int, double>, uint64_t*> tables;
-    int dev = 0;
-    QSIM_HIPCHK(hipGetDevice(&dev));
-    std::lock_guard<std::mutex> lock(mu);
-    auto it = tables.find({dev, P});
-    if (it != tables.end()) return it->second;
-    uint64_t host[kFlipThr];
-    flip_thresholds(P, host);
-    uint64_t* d = nullptr;
-    QSIM_HIPCHK(hipMalloc((void**)&d, sizeof host));
-    QSIM_HIPCHK(hipMemcpy(d, host, sizeof host, hipMemcpyHostToDevice));
-    tables[{dev, P}] = d;
-    return d;
-}
-
 // false when the channel never fires (P == 0)
 static bool flip_channel(int type, int qubit, double p, uint64_t key, FlipChan& c) {
     const double P = flip_probability(p);
@@ -325,8 +290,6 @@ static bool flip_channel(int type, int qubit, double p, uint64_t key, FlipChan& 
     c.type = type;
     c.always = P >= 1.0 ? 1 : 0;
     c.lq = c.always ? -1.0 : std::log1p(-P);
-    c.inv_l2q = c.always ? 0.0f : (float)(1.0 / std::log2(1.0 - P));
-    c.thr = c.always ? nullptr : flip_table(P);
     return true;
 }
 
@@ -1267,14 +1230,6 @@ void launch_pull_noise_step(const double2* src, double2* dst, int n, uint64_t ba
 }
 
 }  // namespace qsim_hip
-
-extern "C" int qsim_noise_flip_thresholds(double p, uint64_t* out) {
-    if (!out) return QSIM_ERR_INVALID_ARGUMENT;
-    const double P = qsim_hip::flip_probability(p);
-    if (!(P > 0.0) || P >= 1.0) return QSIM_ERR_INVALID_ARGUMENT;
-    qsim_hip::flip_thresholds(P, out);
-    return QSIM_OK;
-}
 
 extern "C" int qsim_noise_check_flips(uint64_t* flips) {
     if (!flips) return QSIM_ERR_INVALID_ARGUMENT;

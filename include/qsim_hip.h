@@ -328,10 +328,6 @@ int qsim_noise_apply(qsim_state* s, int type, int qubit, double probability, uin
 /* Flips applied so far by range-checked noise launches (QSIM_NOISE_CHECK=1: the one-launch
  * reference noise kernel counts every access outside its work-group's pairs on the device and
  * fails the call if there is one; tests read this to see the check had work to do). */
-/* Host-only: the 257 geometric-gap thresholds the flip channels draw with for probability p
- * (0 < P(float uniform < p) < 1): out[k] = floor((1 - P)^k 2^53); a block's next flip is gap + 1
- * pairs on, gap = the largest k <= 256 with (hash >> 11) + 1 <= out[k] (256: no further flip). */
-int qsim_noise_flip_thresholds(double p, uint64_t* out);
 int qsim_noise_check_flips(uint64_t* flips);
 /* NoisySimulator::run (src/NoiseModel.cu:369-382): each gate, then every channel entry in order,
  * one noise pass each; *counter advances by one per pass.  With no channel entries the circuit

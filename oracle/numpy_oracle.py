@@ -242,14 +242,6 @@ def flip_probability(p):
     return min(16777216.0, max(0.0, c)) / 16777216.0
 
 
-def flip_thresholds(P):
-    """Gap thresholds of flip probability P (csrc/hip/noise.hip flip_thresholds, same double
-    arithmetic through the host libm): t[0] = 2^53, t[k] = floor((1 - P)^k 2^53), k = 1..256."""
-    lq = math.log1p(-P)
-    return np.array([1 << 53] + [int(math.floor(math.ldexp(math.exp(k * lq), 53)))
-                                 for k in range(1, (1 << _FLIP_BLOCK_LOG) + 1)], dtype=np.uint64)
-
-
 def flip_events(key, idx0, pairs, p, depolarizing):
     """(global pair indices, Pauli codes 1 X / 2 Y / 3 Z or None) of one flip pass over the
     global pairs [idx0, idx0 + pairs), in the engine's draw order."""
@@ -257,10 +249,8 @@ def flip_events(key, idx0, pairs, p, depolarizing):
     if P <= 0.0 or pairs == 0:
         return np.zeros(0, np.uint64), np.zeros(0, np.int64)
     always = P >= 1.0
+    lq = -1.0 if always else math.log1p(-P)
     B = 1 << _FLIP_BLOCK_LOG
-    # gap = the largest k <= B with u1 <= t[k] (u1 = (h >> 11) + 1): t[1..B] descending, so the
-    # count of thresholds >= u1
-    asc = None if always else flip_thresholds(P)[1:][::-1].copy()
     blocks = np.arange(idx0 >> _FLIP_BLOCK_LOG, ((idx0 + pairs - 1) >> _FLIP_BLOCK_LOG) + 1,
                        dtype=np.uint64)
     stream = _mix_np(np.uint64(key) ^ _mix_np(blocks ^ np.uint64(_BLOCK_SALT)))
@@ -274,8 +264,8 @@ def flip_events(key, idx0, pairs, p, depolarizing):
             if always:
                 step = np.ones(blocks.size, np.int64)
             else:
-                u1 = (h >> np.uint64(11)) + np.uint64(1)
-                gap = B - np.searchsorted(asc, u1, side="left")
+                u = ((h >> np.uint64(11)) + np.uint64(1)).astype(np.float64) * 2.0 ** -53
+                gap = np.floor(np.log(u) / lq)
                 live &= gap < B
                 step = np.where(live, np.minimum(gap, B), 0).astype(np.int64) + 1
             pos = np.where(live, pos + step, pos)

@@ -124,30 +124,3 @@ def test_threaded_oracle_is_bit_identical(oracle, threads):
     want = oracle.run_cpu(n, gates, state=start)
     got = oracle.run_cpu_mt(n, gates, state=start, threads=threads)
     assert np.array_equal(got, want)
-
-
-@pytest.mark.parametrize("p", [0.01, 0.2, 0.5, 1e-6, 0.9])
-def test_flip_thresholds_engine_equals_oracle(oracle, qsim, p):
-    """The flip channels' geometric-gap thresholds (csrc/hip/noise.hip flip_thresholds, host code)
-    equal the oracle's restatement bit for bit, and the gaps they define follow the geometric law
-    P(gap >= k) = (1 - P)^k (the reference's per-pair flip probability, src/NoiseModel.cu:857)."""
-    import ctypes
-    from qsim_amd import _lib
-    out = (ctypes.c_uint64 * 257)()
-    _lib.check(_lib.hip.qsim_noise_flip_thresholds(p, out))
-    P = oracle.flip_probability(p)
-    want = oracle.flip_thresholds(P)
-    assert np.array_equal(np.array(out[:], dtype=np.uint64), want)
-    assert all(want[k] >= want[k + 1] for k in range(256))
-    for k in (1, 2, 10, 100):
-        assert abs(float(want[k]) / 2.0 ** 53 - (1 - P) ** k) < 1e-12
-
-
-def test_flip_events_geometric_rate(oracle):
-    """Flips drawn with the threshold rule over many blocks: the fraction of pairs flipped is P."""
-    p = 0.03
-    g, _ = oracle.flip_events(0x1234, 0, 1 << 20, p, False)
-    P = oracle.flip_probability(p)
-    rate = g.size / float(1 << 20)
-    assert abs(rate - P) < 5 * (P * (1 - P) / (1 << 20)) ** 0.5
-    assert np.unique(g).size == g.size  # a pair flips at most once per pass
