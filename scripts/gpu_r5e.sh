@@ -16,6 +16,8 @@ prof() {  # region, extra bench args...
   python3 scripts/roofline_check.py $rg $O/bench_$rg.json $O/prof_$rg/${rg}_kernel_trace.csv $O/check_$rg.json \
     --markers=$O/prof_$rg/${rg}_marker_api_trace.csv | grep -E "frac|\"launches|avg_ms|median_ms"
 }
+timeout -k 10 600 python -u -m pytest -v --timeout 120 --timeout-method thread -m gpu -x tests/test_batched_refnoise_gpu.py tests/test_noisy_gpu.py > $O/pytest_noise.log 2>&1 || { tail -30 $O/pytest_noise.log; exit 1; }
+tail -1 $O/pytest_noise.log
 prof 1q28 --steps 3 --warmup 1 --no-batch16 --no-extras || exit 1
 prof batch16ref --steps 3 --warmup 1 --no-1q28 --no-extras || exit 1
 run_pmc() {  # name, command...
@@ -33,3 +35,7 @@ run_pmc noisy_26q python3 $R/bench.py --workload noisy --cpu-budget 0 --steps 2 
 cp $O/pmc_noisy_26q.json profiles/pmc_noisy_26q.json
 timeout -k 10 300 python -u bench.py --workload noisy --cpu-budget 0 --steps 3 > $O/noisy.json 2> $O/noisy.err || { tail -5 $O/noisy.err; exit 1; }
 python3 -c "import json;d=json.load(open('$O/noisy.json'));print('noisy', d['value'], d['ms_per_step'], d['noise_roofline']); print([(k['name'], round(k['ms']/max(1,k['launches']),4)) for k in d['kernels']])"
+cd /tmp && timeout -k 10 400 rocprofv3 --marker-trace --kernel-trace --stats --output-format csv -d $O/prof_noisy26 -o noisy26 -- python3 $R/bench.py --workload noisy --cpu-budget 0 --steps 3 --profile-region noisy26 > $O/bench_noisy26.json 2> $O/bench_noisy26.err || { tail -5 $O/bench_noisy26.err; exit 1; }
+cd /tmp && timeout -k 10 400 rocprofv3 --marker-trace --kernel-trace --stats --output-format csv -d $O/prof_dm14 -o dm14 -- python3 $R/bench.py --workload dm --cpu-budget 0 --steps 5 --profile-region dm14 > $O/bench_dm14.json 2> $O/bench_dm14.err || { tail -5 $O/bench_dm14.err; exit 1; }
+cd $R
+python3 scripts/roofline_check.py dm14 $O/bench_dm14.json $O/prof_dm14/dm14_kernel_trace.csv $O/check_dm14.json --markers=$O/prof_dm14/dm14_marker_api_trace.csv | grep -E "frac|\"launches"

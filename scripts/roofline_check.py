@@ -25,12 +25,15 @@ REGIONS = {
     "hc": (lambda o: o["roofline"], r"^(qk\d+|.*k_fused_(staged|tile).*)"),
     "1q28": (lambda o: o["roofline_1q28"], r".*k_m1_(slice|lane).*"),
     "batch16ref": (lambda o: o["roofline_batch16"]["reference"]["roofline"], None),
-    "noisy26": (lambda o: o["noisy_26q"]["roofline"], None),
-    "dm14": (lambda o: o["dm_14q"]["roofline"], r"^(qk\d+|.*k_fused_(staged|tile).*)"),
+    # (the default line's nested objects, or the --workload noisy / dm line itself)
+    "noisy26": (lambda o: o.get("noisy_26q", o)["noise_roofline"], None),
+    "dm14": (lambda o: o.get("dm_14q", o)["roofline"], r"^(qk\d+|.*k_fused_(staged|tile).*)"),
 }
 # the engine's kernel-table names -> rocprof symbol patterns (bench.py / engine Timer names)
 ENGINE_NAMES = {
     "noise_units": r".*k_noise_units.*",
+    "noise": r".*k_noise_(units|flips).*",
+    "gate_noise": r".*k_gate_noise_tile.*",
     "pull_gate": r".*k_pull_gate.*",
     "noise_map": r".*k_noise_words.*",
     "fused_tile": r"^(qk\d+|.*k_fused_(staged|tile).*)",
