@@ -112,6 +112,14 @@ def main():
     if len(sys.argv) > 4:
         with open(sys.argv[4], "w") as f:
             f.write(js + "\n")
+        # the rocprof kernel summary of the timed region alone (every kernel in the window)
+        allk = durations(trace, r".*", window)
+        rows = sorted(allk.items(), key=lambda kv: -sum(kv[1]))
+        with open(sys.argv[4].replace(".json", "_timed_kernel_stats.csv"), "w", newline="") as f:
+            w = csv.writer(f)
+            w.writerow(["Name", "Calls", "TotalDurationNs", "AverageNs", "MedianNs", "MinNs", "MaxNs"])
+            for name, v in rows:
+                w.writerow([name, len(v), sum(v), round(statistics.fmean(v), 1), statistics.median(v), min(v), max(v)])
 
 
 if __name__ == "__main__":
