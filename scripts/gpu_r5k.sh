@@ -25,7 +25,7 @@ prof() {  # region, extra bench args...
     > $O/bench_$rg.json 2> $O/bench_$rg.err || { tail -5 $O/bench_$rg.err; return 1; }
   cd $R
   python3 scripts/roofline_check.py $rg $O/bench_$rg.json $O/prof_$rg/${rg}_kernel_trace.csv $O/check_$rg.json \
-    --markers=$O/prof_$rg/${rg}_marker_api_trace.csv | grep -E "frac|\\"launches"
+    --markers=$O/prof_$rg/${rg}_marker_api_trace.csv | grep -E "frac|launches"
 }
 prof noisy26 --workload noisy --steps 3 || exit 1
 prof dm14 --workload dm --steps 5 || exit 1
