@@ -50,13 +50,17 @@ def load_line(path):
 
 
 def marker_window(marker_csv, region):
-    """[start, end] of the roctx range "timed_<region>" (rocprofv3 --marker-trace csv)."""
+    """[(start, end), ...] of every roctx range "timed_<region>" (rocprofv3 --marker-trace csv; a
+    region entered once per timed step gives one range per step)."""
+    out = []
     with open(marker_csv, newline="") as f:
         for row in csv.DictReader(f):
             msg = row.get("Function") or row.get("Message") or row.get("Name") or ""
             if msg == f"timed_{region}" or row.get("Message", "") == f"timed_{region}":
-                return int(row["Start_Timestamp"]), int(row["End_Timestamp"])
-    raise SystemExit(f"no range timed_{region} in {marker_csv}")
+                out.append((int(row["Start_Timestamp"]), int(row["End_Timestamp"])))
+    if not out:
+        raise SystemExit(f"no range timed_{region} in {marker_csv}")
+    return out
 
 
 def durations(trace_csv, pattern, window=None):
@@ -68,7 +72,7 @@ def durations(trace_csv, pattern, window=None):
             if name is None or not rx.match(name):
                 continue
             t0, t1 = int(row["Start_Timestamp"]), int(row["End_Timestamp"])
-            if window and not (window[0] <= t0 <= window[1]):
+            if window and not any(a <= t0 <= b for a, b in window):
                 continue
             out.setdefault(name, []).append(t1 - t0)
     return out
