@@ -212,6 +212,10 @@ struct qsim_state {
     // (steps alternate), so the next step's words are built on noise_stream during this pass
     unsigned char* noise_codes = nullptr;
     size_t noise_codes_cap = 0;  // bytes of ONE set
+    // in-tile noise (noise.hip launch_gate_noise_run): two sets of per-step flip lists, built on
+    // noise_stream one step ahead
+    char* noise_lists = nullptr;
+    size_t noise_lists_cap = 0;  // bytes of ONE set
     hipStream_t noise_stream = nullptr;
     hipEvent_t nev_map[2] = {}, nev_pull[2] = {}, nev_start = nullptr;
     ~qsim_state() {
@@ -223,6 +227,7 @@ struct qsim_state {
         if (base) (void)hipFree(base);
         if (alt_base) (void)hipFree(alt_base);
         if (noise_codes) (void)hipFree(noise_codes);
+        if (noise_lists) (void)hipFree(noise_lists);
         if (d_partials) (void)hipFree(d_partials);
         if (d_result) (void)hipFree(d_result);
         if (stream) (void)hipStreamDestroy(stream);
@@ -288,6 +293,13 @@ static void release_alt(qsim_state* s) {
     s->alt = nullptr;
 }
 
+// The noise side stream and its events (the pulled path's code-word maps, the in-tile path's lists).
+static void ensure_noise_stream(qsim_state* s) {
+    if (s->noise_stream) return;
+    QSIM_HIPCHK(hipStreamCreateWithFlags(&s->noise_stream, hipStreamNonBlocking));
+    for (hipEvent_t* e : {&s->nev_map[0], &s->nev_map[1], &s->nev_pull[0], &s->nev_pull[1], &s->nev_start})
+        QSIM_HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
+}
 // Buffers of the pulled noise path: the second state buffer, two sets of per-step code words.
 static bool ensure_noise_buffers(qsim_state* s, size_t nch) {
     const size_t codes_b = pull_noise_codes_bytes(s->n, 1, nch);
@@ -310,11 +322,35 @@ static bool ensure_noise_buffers(qsim_state* s, size_t nch) {
         if (!grab(&s->noise_codes, 2 * codes_b)) return false;
         s->noise_codes_cap = codes_b;
     }
-    if (!s->noise_stream) {
-        QSIM_HIPCHK(hipStreamCreateWithFlags(&s->noise_stream, hipStreamNonBlocking));
-        for (hipEvent_t* e : {&s->nev_map[0], &s->nev_map[1], &s->nev_pull[0], &s->nev_pull[1], &s->nev_start})
-            QSIM_HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
+    ensure_noise_stream(s);
+    return true;
+}
+
+// Two sets of the in-tile path's flip lists, when they fit beside a margin (false: the tile
+// kernels walk the draws themselves).
+static bool ensure_noise_lists(qsim_state* s, size_t bytes) {
+    if (bytes > s->noise_lists_cap) {
+        if (s->noise_lists) {
+            QSIM_HIPCHK(hipStreamSynchronize(s->stream));
+            if (s->noise_stream) QSIM_HIPCHK(hipStreamSynchronize(s->noise_stream));
+            (void)hipFree(s->noise_lists);
+            s->noise_lists = nullptr;
+            s->noise_lists_cap = 0;
+        }
+        size_t free_b = 0, total_b = 0;
+        if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) {
+            (void)hipGetLastError();
+            return false;
+        }
+        if (free_b < 2 * bytes + kAltMarginBytes) return false;
+        if (hipMalloc((void**)&s->noise_lists, 2 * bytes) != hipSuccess) {
+            (void)hipGetLastError();
+            s->noise_lists = nullptr;
+            return false;
+        }
+        s->noise_lists_cap = bytes;
     }
+    ensure_noise_stream(s);
     return true;
 }
 
@@ -339,6 +375,9 @@ static void trim_noise_buffers(qsim_state* s) {
     if (s->noise_codes) (void)hipFree(s->noise_codes);
     s->noise_codes = nullptr;
     s->noise_codes_cap = 0;
+    if (s->noise_lists) (void)hipFree(s->noise_lists);
+    s->noise_lists = nullptr;
+    s->noise_lists_cap = 0;
     if (!s->relayout) release_alt(s);
 }
 
@@ -1384,7 +1423,7 @@ int qsim_state_memory_bytes(qsim_state* s, uint64_t* bytes) {
         QSIM_REQUIRE(bytes, QSIM_ERR_INVALID_ARGUMENT, "null out");
         const uint64_t amps = sizeof(double2) << s->n;
         *bytes = amps + (s->alt_base ? amps : 0) + 4096 * sizeof(double) + sizeof(double) + s->scratch.cap +
-                 s->ops.cap + s->stages.cap + 2 * s->noise_codes_cap;
+                 s->ops.cap + s->stages.cap + 2 * s->noise_codes_cap + 2 * s->noise_lists_cap;
     });
 }
 
@@ -1453,6 +1492,37 @@ int qsim_noisy_run(qsim_state* s, const qsim_gate* gates, size_t count,
         // where the amplitudes are now: a pinned state's handed-out pointer (prep() leaves the
         // amplitudes of a pinned state in the buffer that was handed out, which may be either one)
         double2* const home = s->d;
+        // From 12 qubits, flip-only models run in place through the in-tile path (noise.hip
+        // launch_gate_noise_run: the gate and the channel prefix whose qubits lie in its tile in one
+        // LDS pass, their flips from lists built one step ahead on noise_stream, the rest pushed one
+        // launch per channel) — the same draws, so the same states as the pulled and pushed paths.
+        // QSIM_NOISY_TILE=0: the pulled path.
+        {
+            const char* te = std::getenv("QSIM_NOISY_TILE");  // (read per run: tests switch it)
+            bool tile = (te == nullptr || std::atoi(te) != 0) && s->n >= 12;
+            for (const NoiseChan& ch : chans) tile = tile && (ch.type == 0 || ch.type >= 3);
+            for (const Op& op : ops) tile = tile && gate_noise_tile_supported(s->n, &op);
+            if (tile) {
+                const size_t lb = gate_noise_lists_bytes(s->n, 1, chans);
+                GnLists L{};
+                const bool lists = lb && ensure_noise_lists(s, lb);
+                if (lists) {
+                    L.buf[0] = s->noise_lists;
+                    L.buf[1] = s->noise_lists + s->noise_lists_cap;
+                    L.set_bytes = s->noise_lists_cap;
+                    L.ms = s->noise_stream;
+                    L.built[0] = s->nev_map[0];
+                    L.built[1] = s->nev_map[1];
+                    L.used[0] = s->nev_pull[0];
+                    L.used[1] = s->nev_pull[1];
+                    L.start = s->nev_start;
+                }
+                launch_gate_noise_run(s->d, s->n, 1, 0, ops, chans, seed, *counter, s->stream, &s->timer,
+                                      lists ? &L : nullptr);
+                trim_noise_buffers(s);
+                return;
+            }
+        }
         if (pull_noise_supported(s->n, chans, true) && ensure_noise_buffers(s, chans.size())) {
             // Flip channels only: the noise after gate i is applied by gate i+1's pass (out of
             // place), the noise after the last gate by one identity pass (noise.hip); the same

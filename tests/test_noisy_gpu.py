@@ -156,6 +156,7 @@ def test_pulled_flip_noise_matches_oracle(qsim, oracle, gpu_ready, monkeypatch, 
     step's code words built on a second stream or not, and with > 16 channel entries (64-bit
     words, fourth case).  A damping channel in the model keeps the per-channel passes (third)."""
     monkeypatch.setenv("QSIM_NOISE_MAP_OVERLAP", overlap)
+    monkeypatch.setenv("QSIM_NOISY_TILE", "0")  # (from 12 qubits the in-tile path is the default)
     rng = np.random.default_rng(seed)
     c = qsim.createRandomCircuit(n, 16, seed)
     channels = [(int(t), int(rng.integers(0, n)), float(rng.uniform(0.1, 0.5))) for t in types]
@@ -181,14 +182,16 @@ def _read_device(ptr, n):
     return out
 
 
+@pytest.mark.parametrize("tile", ["0", "1"])
 @pytest.mark.parametrize("keep", ["1", "0"])
-def test_pulled_noise_on_a_pinned_pointer(qsim, oracle, gpu_ready, monkeypatch, keep):
+def test_pulled_noise_on_a_pinned_pointer(qsim, oracle, gpu_ready, monkeypatch, keep, tile):
     """an unpinned pulled run with an odd gate count leaves the amplitudes in
     the second buffer; devicePtr() then hands that buffer out.  The next pulled runs must leave
     their result where that pointer points (odd and even gate counts), never free it, and the
     pointer must equal getStateVector and the oracle.  keep=0 frees the noise buffers after every
     run (the low-memory branch), keep=1 keeps them."""
     monkeypatch.setenv("QSIM_NOISE_KEEP_BUFFERS", keep)
+    monkeypatch.setenv("QSIM_NOISY_TILE", tile)  # (tile = 1: the in-tile path, in place)
     n, seed = 12, 9
     channels = [(0, q, 0.2) for q in range(n)]
     c_odd = qsim.createRandomCircuit(n, 15, seed)
@@ -211,3 +214,26 @@ def test_pulled_noise_on_a_pinned_pointer(qsim, oracle, gpu_ready, monkeypatch, 
     c = qsim.createRandomHCCircuit(n, 40, 3)
     sim.state.run(c, qsim.RunMode.Fused)
     np.testing.assert_allclose(_read_device(ptr, n), oracle.run_cpu(n, oracle.gates_of(c)), atol=1e-12, rtol=0)
+
+
+@pytest.mark.parametrize("lists", ["1", "0"])
+@pytest.mark.parametrize("n,seed,types,p", [(12, 11, (0,) * 12, 0.05), (13, 12, (0, 3, 4, 5, 0, 3), 0.3),
+                                            (14, 13, (0,) * 14, 0.01)])
+def test_tile_noise_matches_oracle(qsim, oracle, gpu_ready, monkeypatch, lists, n, seed, types, p):
+    """From 12 qubits flip-only models run through the in-tile path (noise.hip
+    launch_gate_noise_run: the gate and the channel prefix inside its 4096-amplitude tile in one LDS
+    pass, flips from per-step lists built on the noise stream, the rest pushed per channel) —
+    exactly the oracle's per-pair passes, two runs (the counter continues), lists on and off."""
+    monkeypatch.setenv("QSIM_NOISE_TILE_LISTS", lists)
+    rng = np.random.default_rng(seed)
+    c = qsim.createRandomCircuit(n, 24, seed)
+    c.cnot(n - 1, 2).swap(3, n - 2).cz(0, n - 1)
+    channels = [(int(t), int(q), p) for t, q in zip(types, rng.permutation(n))]
+    sim = qsim.NoisySimulator(n, _model(qsim, channels))
+    sim.setSeed(3000 + seed)
+    sim.run(c)
+    want, ctr = oracle.noisy_run(n, oracle.gates_of(c), channels, 3000 + seed)
+    np.testing.assert_allclose(sim.getStateVector(), want, atol=1e-12, rtol=0)
+    sim.run(c)
+    want2, _ = oracle.noisy_run(n, oracle.gates_of(c), channels, 3000 + seed, ctr, want)
+    np.testing.assert_allclose(sim.getStateVector(), want2, atol=1e-12, rtol=0)
