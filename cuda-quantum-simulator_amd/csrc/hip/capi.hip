@@ -1492,14 +1492,15 @@ int qsim_noisy_run(qsim_state* s, const qsim_gate* gates, size_t count,
         // where the amplitudes are now: a pinned state's handed-out pointer (prep() leaves the
         // amplitudes of a pinned state in the buffer that was handed out, which may be either one)
         double2* const home = s->d;
-        // From 12 qubits, flip-only models run in place through the in-tile path (noise.hip
+        // QSIM_NOISY_TILE=1 (from 12 qubits, flip-only models): the in-tile path (noise.hip
         // launch_gate_noise_run: the gate and the channel prefix whose qubits lie in its tile in one
         // LDS pass, their flips from lists built one step ahead on noise_stream, the rest pushed one
         // launch per channel) — the same draws, so the same states as the pulled and pushed paths.
-        // QSIM_NOISY_TILE=0: the pulled path.
+        // Opt-in: at 26 qubits with 26 channels the 14-15 per-channel suffix launches (0.04 ms
+        // each) outweigh the pull pass, 904 vs 1 024 gates/s.
         {
             const char* te = std::getenv("QSIM_NOISY_TILE");  // (read per run: tests switch it)
-            bool tile = (te == nullptr || std::atoi(te) != 0) && s->n >= 12;
+            bool tile = te != nullptr && std::atoi(te) != 0 && s->n >= 12;
             for (const NoiseChan& ch : chans) tile = tile && (ch.type == 0 || ch.type >= 3);
             for (const Op& op : ops) tile = tile && gate_noise_tile_supported(s->n, &op);
             if (tile) {

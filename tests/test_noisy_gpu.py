@@ -156,7 +156,7 @@ def test_pulled_flip_noise_matches_oracle(qsim, oracle, gpu_ready, monkeypatch, 
     step's code words built on a second stream or not, and with > 16 channel entries (64-bit
     words, fourth case).  A damping channel in the model keeps the per-channel passes (third)."""
     monkeypatch.setenv("QSIM_NOISE_MAP_OVERLAP", overlap)
-    monkeypatch.setenv("QSIM_NOISY_TILE", "0")  # (from 12 qubits the in-tile path is the default)
+    monkeypatch.setenv("QSIM_NOISY_TILE", "0")  # (the default; the in-tile path is opt-in)
     rng = np.random.default_rng(seed)
     c = qsim.createRandomCircuit(n, 16, seed)
     channels = [(int(t), int(rng.integers(0, n)), float(rng.uniform(0.1, 0.5))) for t in types]
@@ -220,11 +220,12 @@ def test_pulled_noise_on_a_pinned_pointer(qsim, oracle, gpu_ready, monkeypatch, 
 @pytest.mark.parametrize("n,seed,types,p", [(12, 11, (0,) * 12, 0.05), (13, 12, (0, 3, 4, 5, 0, 3), 0.3),
                                             (14, 13, (0,) * 14, 0.01)])
 def test_tile_noise_matches_oracle(qsim, oracle, gpu_ready, monkeypatch, lists, n, seed, types, p):
-    """From 12 qubits flip-only models run through the in-tile path (noise.hip
+    """QSIM_NOISY_TILE=1: from 12 qubits flip-only models run through the in-tile path (noise.hip
     launch_gate_noise_run: the gate and the channel prefix inside its 4096-amplitude tile in one LDS
     pass, flips from per-step lists built on the noise stream, the rest pushed per channel) —
     exactly the oracle's per-pair passes, two runs (the counter continues), lists on and off."""
     monkeypatch.setenv("QSIM_NOISE_TILE_LISTS", lists)
+    monkeypatch.setenv("QSIM_NOISY_TILE", "1")
     rng = np.random.default_rng(seed)
     c = qsim.createRandomCircuit(n, 24, seed)
     c.cnot(n - 1, 2).swap(3, n - 2).cz(0, n - 1)
