@@ -331,7 +331,16 @@ void settle_in_d0(qsim_batch* b) {
 // map_stream and its events (the pulled path's word maps, the tile path's flip lists).
 void ensure_map_stream(qsim_batch* b) {
     if (b->map_stream) return;
-    QSIM_HIPCHK(hipStreamCreateWithFlags(&b->map_stream, hipStreamNonBlocking));
+    // QSIM_NOISE_STREAM_PRIO (experiments): 1 = the side stream at the lowest priority, so the
+    // list builds yield the CUs to the main stream's kernels
+    const char* pe = std::getenv("QSIM_NOISE_STREAM_PRIO");
+    if (pe && std::atoi(pe) != 0) {
+        int lo = 0, hi = 0;
+        QSIM_HIPCHK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+        QSIM_HIPCHK(hipStreamCreateWithPriority(&b->map_stream, hipStreamNonBlocking, lo));
+    } else {
+        QSIM_HIPCHK(hipStreamCreateWithFlags(&b->map_stream, hipStreamNonBlocking));
+    }
     for (hipEvent_t* e : {&b->ev_map[0], &b->ev_map[1], &b->ev_pull[0], &b->ev_pull[1], &b->ev_start})
         QSIM_HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
 }
