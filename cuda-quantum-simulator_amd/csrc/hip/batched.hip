@@ -275,6 +275,15 @@ struct qsim_batch {
     // on map_stream one step ahead.
     char* d_lists = nullptr;
     size_t lists_cap = 0;           // bytes of ONE set
+    // QSIM_NOISE_SPLIT=k (experiment): the in-tile path runs the ensemble as k trajectory parts on
+    // k streams (part 0 on `stream`), so one part's tile pass can overlap another's suffix push
+    struct SplitPart {
+        hipStream_t s = nullptr, ms = nullptr;
+        hipEvent_t built[2] = {}, used[2] = {}, start = nullptr, fork = nullptr, join = nullptr;
+        char* lists = nullptr;
+        size_t cap = 0;
+    };
+    std::vector<SplitPart> split;
     hipStream_t map_stream = nullptr;
     hipEvent_t ev_map[2] = {}, ev_pull[2] = {}, ev_start = nullptr;
     bool pinned = false;
@@ -288,6 +297,15 @@ struct qsim_batch {
         if (d1) (void)hipFree(d1);
         if (d_codes) (void)hipFree(d_codes);
         if (d_lists) (void)hipFree(d_lists);
+        for (SplitPart& p : split) {
+            if (p.s) (void)hipStreamSynchronize(p.s);
+            if (p.ms) (void)hipStreamSynchronize(p.ms);
+            for (hipEvent_t e : {p.built[0], p.built[1], p.used[0], p.used[1], p.start, p.fork, p.join})
+                if (e) (void)hipEventDestroy(e);
+            if (p.s) (void)hipStreamDestroy(p.s);
+            if (p.ms) (void)hipStreamDestroy(p.ms);
+            if (p.lists) (void)hipFree(p.lists);
+        }
         if (d_xz) (void)hipFree(d_xz);
         if (d_e) (void)hipFree(d_e);
         if (d_ch) (void)hipFree(d_ch);
@@ -370,6 +388,65 @@ bool ensure_list_buffers(qsim_batch* b, size_t bytes) {
     }
     ensure_map_stream(b);
     return true;
+}
+// The in-tile run over k trajectory parts on k streams (QSIM_NOISE_SPLIT): part 0 on the object's
+// stream with its list sets, part j > 0 on a stream of its own with its own side stream and lists;
+// every part draws with the global pair index, so the states are the one-part run's.
+void split_tile_run(qsim_batch* b, const std::vector<Op>& ops, const std::vector<NoiseChan>& dep, int k,
+                    const GnLists& L0) {
+    const uint64_t B = (uint64_t)b->batch;
+    if ((int)b->split.size() < k - 1) b->split.resize(k - 1);
+    const uint64_t c0 = b->ncounter;
+    uint64_t c_end = c0;
+    std::vector<GnLists> Ls(k);
+    std::vector<uint64_t> first(k + 1);
+    for (int j = 0; j <= k; ++j) first[j] = B * (uint64_t)j / (uint64_t)k;
+    Ls[0] = L0;
+    for (int j = 1; j < k; ++j) {
+        qsim_batch::SplitPart& p = b->split[j - 1];
+        if (!p.s) {
+            QSIM_HIPCHK(hipStreamCreateWithFlags(&p.s, hipStreamNonBlocking));
+            QSIM_HIPCHK(hipStreamCreateWithFlags(&p.ms, hipStreamNonBlocking));
+            for (hipEvent_t* e : {&p.built[0], &p.built[1], &p.used[0], &p.used[1], &p.start, &p.fork, &p.join})
+                QSIM_HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
+        }
+        const size_t lb = gate_noise_lists_bytes(b->n, first[j + 1] - first[j], dep);
+        if (lb > p.cap) {
+            if (p.lists) {
+                QSIM_HIPCHK(hipStreamSynchronize(p.s));
+                QSIM_HIPCHK(hipStreamSynchronize(p.ms));
+                (void)hipFree(p.lists);
+                p.lists = nullptr;
+                p.cap = 0;
+            }
+            QSIM_HIPCHK(hipMalloc((void**)&p.lists, 2 * lb));
+            p.cap = lb;
+        }
+        GnLists& L = Ls[j];
+        L.buf[0] = p.lists;
+        L.buf[1] = p.lists + p.cap;
+        L.set_bytes = p.cap;
+        L.ms = p.ms;
+        L.built[0] = p.built[0];
+        L.built[1] = p.built[1];
+        L.used[0] = p.used[0];
+        L.used[1] = p.used[1];
+        L.start = p.start;
+        QSIM_HIPCHK(hipEventRecord(p.fork, b->stream));  // (after everything before this run)
+        QSIM_HIPCHK(hipStreamWaitEvent(p.s, p.fork, 0));
+    }
+    for (int j = 0; j < k; ++j) {
+        hipStream_t sj = j == 0 ? b->stream : b->split[j - 1].s;
+        uint64_t c = c0;
+        launch_gate_noise_run(b->d + (first[j] << b->n), b->n, first[j + 1] - first[j], b->traj0 + first[j], ops, dep,
+                              b->seed, c, sj, &b->timer, &Ls[j]);
+        c_end = c;
+    }
+    for (int j = 1; j < k; ++j) {
+        QSIM_HIPCHK(hipEventRecord(b->split[j - 1].join, b->split[j - 1].s));
+        QSIM_HIPCHK(hipStreamWaitEvent(b->stream, b->split[j - 1].join, 0));
+    }
+    b->ncounter = c_end;
 }
 // Buffers of the pulled noise path (second ensemble buffer, flip codes, touched bits), allocated
 // when the device has room for them beside a margin; false: run the push kernels instead.
@@ -663,6 +740,12 @@ int qsim_batch_run(qsim_batch* b, const qsim_gate* gates, size_t count,
                     L.used[0] = b->ev_pull[0];
                     L.used[1] = b->ev_pull[1];
                     L.start = b->ev_start;
+                }
+                const char* se = std::getenv("QSIM_NOISE_SPLIT");  // (experiment; read per run)
+                const int k = se ? std::max(1, std::min(4, std::atoi(se))) : 1;
+                if (k > 1 && b->batch >= k && lists) {
+                    split_tile_run(b, ops, dep, k, L);
+                    return;
                 }
                 launch_gate_noise_run(b->d, b->n, (uint64_t)b->batch, b->traj0, ops, dep, b->seed, b->ncounter,
                                       b->stream, &b->timer, lists ? &L : nullptr);

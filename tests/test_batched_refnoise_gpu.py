@@ -339,3 +339,29 @@ def test_gate_noise_tile_equals_push_16q(qsim, gpu_ready, monkeypatch):
             out.append(np.stack([s.getStateVector(t) for t in (0, 31, 63)]))
             s.close()
         assert np.array_equal(out[0], out[1])
+
+
+@pytest.mark.parametrize("k", ["2", "3"])
+def test_gate_noise_tile_split_parts_equal_one_part(qsim, oracle, gpu_ready, monkeypatch, k):
+    """QSIM_NOISE_SPLIT=k (experiment): the in-tile run as k trajectory parts on k streams gives the
+    one-part run's trajectories bit for bit (draws keyed by the global pair index), over two runs."""
+    n, B = 13, 7
+    nm = qsim.NoiseModel()
+    nm.addDepolarizingAll(n, 0.03)
+    c = _circuit(qsim, n, 20, 17)
+    out = []
+    for split in ("1", k):
+        monkeypatch.setenv("QSIM_NOISE_SPLIT", split)
+        s = qsim.BatchedSimulator(n, B, nm, noise=qsim.BatchedNoise.Reference)
+        s.setSeed(17)
+        s.run(c)
+        s.run(c)
+        out.append(np.stack([s.getStateVector(t) for t in range(B)]))
+        s.close()
+    assert np.array_equal(out[0], out[1])
+    entries = [(0, q, 0.03) for q in range(n)]
+    whole, counter = None, 0
+    for _ in range(2):
+        whole, counter = oracle.batched_reference_run(n, B, oracle.gates_of(c), entries, 17, False,
+                                                      states=whole, counter=counter)
+    np.testing.assert_allclose(out[1], whole, atol=1e-12, rtol=0)
