@@ -343,7 +343,7 @@ def test_gate_noise_tile_equals_push_16q(qsim, gpu_ready, monkeypatch):
 
 @pytest.mark.parametrize("k", ["2", "3"])
 def test_gate_noise_tile_split_parts_equal_one_part(qsim, oracle, gpu_ready, monkeypatch, k):
-    """QSIM_NOISE_SPLIT=k (experiment): the in-tile run as k trajectory parts on k streams gives the
+    """QSIM_NOISE_SPLIT=k (default 2): the in-tile run as k trajectory parts on k streams gives the
     one-part run's trajectories bit for bit (draws keyed by the global pair index), over two runs."""
     n, B = 13, 7
     nm = qsim.NoiseModel()
