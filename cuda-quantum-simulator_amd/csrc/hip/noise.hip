@@ -298,7 +298,12 @@ uint64_t noise_check_flips = 0;  // flips applied by range-checked launches (qsi
 void launch_noise_after_gate(double2* st, int n, const std::vector<NoiseChan>& chans, uint64_t seed,
                              uint64_t& counter, hipStream_t s, Timer* tm, uint64_t batch, uint64_t traj0) {
     const int log_ppt = n - 1;
-    const int log_unit = std::max(log_ppt, 16);  // whole trajectories, >= 256 blocks of 256 pairs
+    // whole trajectories, >= 256 blocks of 256 pairs (QSIM_NOISE_UNIT_LOG: experiments, >= n - 1)
+    static const int unit_log_env = [] {
+        const char* e = std::getenv("QSIM_NOISE_UNIT_LOG");
+        return e ? std::atoi(e) : 16;
+    }();
+    const int log_unit = std::max(log_ppt, unit_log_env);
     const uint64_t pairs = batch << log_ppt, idx0 = traj0 << log_ppt;
     const uint64_t units = ((idx0 + pairs - 1) >> log_unit) - (idx0 >> log_unit) + 1;
     bool flips = true;
