@@ -549,10 +549,6 @@ __global__ __launch_bounds__(256) void k_gate_noise_tile(GnArgs a) {
         word_or(j0 | (1 << pq), c, code);
     };
     __shared__ uint32_t cnt_s[kGnMaxPrefix];
-    // fast pull path (step 4): amplitudes of non-isolated flips (bit mask), per-wave compact lists
-    constexpr int kWl = 256;  // list entries per wave (expected ~30 at p = 0.01; more: slow walks)
-    __shared__ uint32_t nim[(1 << kGnTile) / 32];
-    __shared__ uint16_t wl[4][kWl];
     const int t = threadIdx.x;
     uint64_t traj = 0, loc = 0;
     const uint64_t gbase = gn_tile_base(blockIdx.x, a.n, a.u, &traj, &loc);
@@ -576,7 +572,6 @@ __global__ __launch_bounds__(256) void k_gate_noise_tile(GnArgs a) {
     for (int k = 0; k < 8; ++k) wlo[k * 256 + t] = 0u;
 #pragma unroll
     for (int k = 0; k < 4; ++k) whi[k * 256 + t] = 0u;
-    if (t < (1 << kGnTile) / 32) nim[t] = 0u;
     __syncthreads();
     // 2. the prefix channels' flips into the code words
     if (a.skip & 1) {
@@ -633,130 +628,10 @@ __global__ __launch_bounds__(256) void k_gate_noise_tile(GnArgs a) {
         }
         __syncthreads();
     }
-    // 4. out[k] = (P v)[k], stored in place.
-    // Fast path (flip lists, none overflowing): (a) every ISOLATED flip — the only flip in both of
-    // its members' code words — is applied in place by the thread holding it, the members of the
-    // other flips are marked (a walk from a marked amplitude only ever meets marked amplitudes, so
-    // the values it reads are untouched); (b) each wave compacts its marked amplitudes into a list
-    // and pulls them through the words with every lane busy (~3 % of the amplitudes at p = 0.01 on
-    // 12 channels; a per-slot pull leaves most lanes idle); (c) the stores read v[k] or the pulled
-    // source with its phase.  Otherwise every amplitude is pulled, 16 walks per thread in lockstep.
-    bool fast = a.list != nullptr && !(a.skip & 2);
-    for (int c = 0; c < a.np; ++c) fast = fast && cnt_s[c] <= (uint32_t)a.cap;  // (uniform)
-    auto walk1 = [&](int k, int& j, int& e) {  // one amplitude's pull walk
-        uint32_t w = word_at(k);
-        j = k;
-        e = 0;
-        while (w) {
-            const int c = (31 - __builtin_clz(w)) >> 1;
-            const uint32_t code = (w >> (2 * c)) & 3u;
-            const int pqc = pq_of(c);
-            const int bit = (j >> pqc) & 1;
-            const uint32_t keep = (1u << (2 * c)) - 1u;
-            w &= keep;
-            if (code == 3u) {
-                e += 2 * bit;
-            } else {
-                if (code == 2u) e += bit ? 1 : 3;
-                j ^= 1 << pqc;
-                w = word_at(j) & keep;
-            }
-        }
-    };
-    auto phase = [](double2 x, int e) {
-        switch (e & 3) {
-            case 0: return x;
-            case 1: return make_double2(-x.y, x.x);   // i
-            case 2: return make_double2(-x.x, -x.y);  // -1
-            default: return make_double2(x.y, -x.x);  // -i
-        }
-    };
-    if (fast) {
-        // (a) isolated flips pushed, the others' members marked
-#pragma unroll
-        for (int k = 0; k < kSlots; ++k) {
-            const int sl = k * 256 + t;
-            if (sl >= nsl) break;
-            const int c = sl >> a.lcap, e = sl & ((1 << a.lcap) - 1);
-            if ((uint32_t)e >= cnt_s[c]) continue;
-            const int x = (int)(le[k] >> 2);
-            const uint32_t code = le[k] & 3u;
-            const int pq = pq_of(c);
-            int j0;
-            if (pq == 11) {
-                j0 = x;
-            } else {
-                const int xl = x & 1023, y = x >> 10;
-                const int lo2 = xl & ((1 << pq) - 1);
-                j0 = (((xl ^ lo2) << 1) | lo2) | (y << 11);
-            }
-            const int j1 = j0 | (1 << pq);
-            const uint32_t only = code << (2 * c);
-            if (word_at(j0) == only && word_at(j1) == only) {
-                if (code == 3u) {
-                    const double2 w1 = v[j1];
-                    v[j1] = make_double2(-w1.x, -w1.y);
-                } else {
-                    const double2 a0 = v[j0], a1 = v[j1];
-                    if (code == 1u) {
-                        v[j0] = a1;
-                        v[j1] = a0;
-                    } else {
-                        v[j0] = make_double2(a1.y, -a1.x);
-                        v[j1] = make_double2(-a0.y, a0.x);
-                    }
-                }
-            } else {
-                atomicOr(&nim[j0 >> 5], 1u << (j0 & 31));
-                atomicOr(&nim[j1 >> 5], 1u << (j1 & 31));
-            }
-        }
-        __syncthreads();
-        // (b) this wave's marked amplitudes, compacted and pulled
-        const int wv = t >> 6, lane = t & 63;
-        const uint64_t below = (1ull << lane) - 1ull;
-        int cnt = 0;
-#pragma unroll
-        for (int k0 = 0; k0 < 16; ++k0) {
-            const int k = k0 * 256 + t;
-            const bool mk = (nim[k >> 5] >> (k & 31)) & 1u;
-            const uint64_t bal = __ballot(mk);
-            const int pos = cnt + __popcll(bal & below);
-            if (mk && pos < kWl) wl[wv][pos] = (uint16_t)k;
-            cnt += __popcll(bal);
-        }
-        if (cnt <= kWl)
-            for (int i = lane; i < cnt; i += 64) {
-                int j = 0, e = 0;
-                walk1((int)wl[wv][i], j, e);
-                wl[wv][i] = (uint16_t)(j | (e << 12));
-            }
-        __syncthreads();  // (the list entries are read back by other lanes)
-        // (c) the stores
-        int pos0 = 0;
-#pragma unroll 4
-        for (int k0 = 0; k0 < 16; ++k0) {
-            const int k = k0 * 256 + t;
-            const bool mk = (nim[k >> 5] >> (k & 31)) & 1u;
-            const uint64_t bal = __ballot(mk);
-            const int pos = pos0 + __popcll(bal & below);
-            pos0 += __popcll(bal);
-            int j = k, e = 0;
-            if (mk) {
-                if (cnt <= kWl) {
-                    const uint32_t r = wl[wv][pos];
-                    j = (int)(r & 4095u);
-                    e = (int)(r >> 12);
-                } else {
-                    walk1(k, j, e);
-                }
-            }
-            st<true>(a.st + gidx(k), phase(v[j], e));
-        }
-        return;
-    }
-    // Every amplitude pulled: the walks of a thread's 16 amplitudes advance in lockstep (one step
-    // of every unfinished walk per round, the word loads of a round independent).
+    // 4. out[k] = (P v)[k], pulled through the code words, stored in place.  The walks of a
+    // thread's 16 amplitudes advance in lockstep (one step of every unfinished walk per round, the
+    // word loads of a round independent), so LDS latency is paid once per round, not per step of
+    // every amplitude (in a wave some lane almost always has a non-zero word).
     int jj[16], ee[16];
     uint32_t ww[16];
 #pragma unroll
