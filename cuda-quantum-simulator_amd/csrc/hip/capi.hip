@@ -1635,6 +1635,26 @@ int qsim_dm_plan_info(int n, const qsim_gate* gates, size_t count, const qsim_no
     });
 }
 
+int qsim_dm_jit_source(int n, const qsim_gate* gates, size_t count, const qsim_noise_channel* channels,
+                       size_t n_channels, int flags, char* buf, size_t cap, size_t* len) {
+    return guarded([&] {
+        if (n < 1 || n > QSIM_DM_MAX_QUBITS) fail(QSIM_ERR_INVALID_ARGUMENT, "bad qubit count");
+        QSIM_REQUIRE(gates || count == 0, QSIM_ERR_INVALID_ARGUMENT, "null gate list");
+        QSIM_REQUIRE(channels || n_channels == 0, QSIM_ERR_INVALID_ARGUMENT, "null channel list");
+        std::vector<Op> ops;
+        dm_lower(n, gates, count, channels, n_channels, ops, (flags & QSIM_DM_REFERENCE_Y) != 0);
+        const int th = tile_height_for(2 * n);
+        const TileHeightScope tile_h(th, tile_rb_for(2 * n, th));
+        const std::string src = jit_source(plan_fused(ops, 2 * n));
+        if (len) *len = src.size();
+        if (buf && cap) {
+            const size_t m = std::min(cap - 1, src.size());
+            std::memcpy(buf, src.data(), m);
+            buf[m] = 0;
+        }
+    });
+}
+
 int qsim_dm_apply_channel(qsim_state* s, int n, int type, int qubit, double p) {
     return guarded([&] {
         check_dm(s, n);

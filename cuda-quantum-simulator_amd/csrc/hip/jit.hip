@@ -153,6 +153,43 @@ struct Gen {
         }
         op_body(t);
     }
+    // CX(c -> r) · diag(1, g) on r · CX(c -> r) with g real: each amplitude whose r and c bits
+    // differ is scaled by g (the density-matrix depolarizing / phase-damping / phase-flip
+    // lowering, density.hip dm_channel).  Emitted as that scale alone — with a thread-bit or
+    // tile-constant control the two CXs would otherwise be 2 x 16 predicated selects — and the same
+    // products as the three ops (x * 1.0 == x), so bit-identical to them.
+    bool xor_diag(const TileOp& a, const TileOp& b, const TileOp& c) {
+        auto one_bit = [](uint64_t m) { return m && !(m & (m - 1)); };
+        const int nc = (a.cm_reg != 0) + (a.cm_thr != 0) + (a.cm_out != 0);
+        if (a.kind != K_M1 || a.sub != S_X || a.p0 < 0 || nc != 1 ||
+            !one_bit(a.cm_reg | a.cm_thr | a.cm_out))
+            return false;
+        if (c.kind != a.kind || c.sub != a.sub || c.p0 != a.p0 || c.cm_reg != a.cm_reg || c.cm_thr != a.cm_thr ||
+            c.cm_out != a.cm_out)
+            return false;
+        if (b.kind != K_DIAG || b.sub != S_GEN || b.p0 != a.p0 || !b.d0_one || b.m[3] != 0.0 || b.cm_reg ||
+            b.cm_thr || b.cm_out)
+            return false;
+        const int P = a.p0;
+        const std::string g = lit(b.m[2]);
+        if (a.cm_reg) {  // both bits in registers: decided per register here
+            const int C = __builtin_ctz(a.cm_reg);
+            for (int r = 0; r < R; ++r)
+                if (((r >> P) ^ (r >> C)) & 1) o << "  " << v(r) << " = " << scale(b.m[2], 0.0, v(r)) << ";\n";
+            return true;
+        }
+        const std::string pc = "c" + std::to_string(tmp++), f0 = "f" + std::to_string(tmp++),
+                          f1 = "f" + std::to_string(tmp++);
+        if (a.cm_thr) o << "  const bool " << pc << " = (jb & " << a.cm_thr << "u) != 0u;\n";
+        else o << "  const bool " << pc << " = (base & " << hexu(a.cm_out) << ") != 0ull;\n";
+        o << "  const double " << f0 << " = " << pc << " ? " << g << " : 1.0, " << f1 << " = " << pc << " ? 1.0 : " << g
+          << ";\n";
+        for (int r = 0; r < R; ++r) {
+            const std::string f = ((r >> P) & 1) ? f1 : f0, x = v(r);
+            o << "  " << x << " = make_double2(" << f << " * " << x << ".x, " << f << " * " << x << ".y);\n";
+        }
+        return true;
+    }
     bool no_rename = false;
     void op_body(const TileOp& t) {
         const uint32_t cr = t.cm_reg;
@@ -303,6 +340,11 @@ int jit_xcd() {
     static const int v = env_or("QSIM_JIT_XCD", 1);
     return v;
 }
+// CX · real diag · CX triples emitted as one scale (Gen::xor_diag; QSIM_JIT_XOR_DIAG=0: as three ops)
+bool xor_diag_on() {
+    static const bool v = env_or("QSIM_JIT_XOR_DIAG", 1) != 0;
+    return v;
+}
 std::string tile_id_expr() {
     const int x = jit_xcd();
     const std::string b = "(unsigned long long)blockIdx.x";
@@ -442,7 +484,13 @@ void gen_pass(std::ostringstream& out, const Plan& plan, const FusedPass& p, int
                 for (int r = 0; r < R; ++r)
                     o << "  " << g.v(r) << " = *reinterpret_cast<const double2*>(lds + (lb ^ " << st.lds[r] << "u));\n";
             }
-            for (int i = st.op_begin; i < st.op_end; ++i) g.op(plan.ops[i]);
+            for (int i = st.op_begin; i < st.op_end; ++i) {
+                if (xor_diag_on() && i + 2 < st.op_end && g.xor_diag(plan.ops[i], plan.ops[i + 1], plan.ops[i + 2])) {
+                    i += 2;
+                    continue;
+                }
+                g.op(plan.ops[i]);
+            }
             if (s == se - 1) {
                 const double sc = std::ldexp(1.0, -(p.hu_count / 2)) * ((p.hu_count & 1) ? kInvSqrt2 : 1.0);
                 for (int r = 0; r < R; ++r) {

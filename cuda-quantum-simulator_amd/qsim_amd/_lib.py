@@ -160,6 +160,8 @@ _sig(hip, "qsim_noisy_run", [_P, POINTER(qsim_gate), c_size_t, POINTER(qsim_nois
 
 _sig(hip, "qsim_dm_plan_info", [c_int, POINTER(qsim_gate), c_size_t, POINTER(qsim_noise_channel), c_size_t,
                                   c_int, POINTER(c_int32), c_size_t, POINTER(c_size_t)])
+_sig(hip, "qsim_dm_jit_source", [c_int, POINTER(qsim_gate), c_size_t, POINTER(qsim_noise_channel), c_size_t,
+                                   c_int, c_char_p, c_size_t, POINTER(c_size_t)])
 _sig(hip, "qsim_dm_run", [_P, c_int, POINTER(qsim_gate), c_size_t, POINTER(qsim_noise_channel),
                           c_size_t, c_int])
 _sig(hip, "qsim_dm_apply_channel", [_P, c_int, c_int, c_int, c_double])

@@ -357,6 +357,9 @@ int qsim_dm_run(qsim_state* rho, int n_qubits, const qsim_gate* gates, size_t co
  * contiguous run bits r0. */
 int qsim_dm_plan_info(int n_qubits, const qsim_gate* gates, size_t count, const qsim_noise_channel* channels,
                       size_t n_channels, int flags, int32_t* info, size_t cap, size_t* n_passes);
+/* Host-only: the circuit-specialised kernel source of that plan (as qsim_jit_source). */
+int qsim_dm_jit_source(int n_qubits, const qsim_gate* gates, size_t count, const qsim_noise_channel* channels,
+                       size_t n_channels, int flags, char* buf, size_t cap, size_t* len);
 /* One channel (applyDepolarizing ... applyBitPhaseFlip, :298-356) on `qubit`. */
 int qsim_dm_apply_channel(qsim_state* rho, int n_qubits, int type, int qubit, double p);
 int qsim_dm_diagonal(qsim_state* rho, int n_qubits, double* dst);          /* 2^n: Re rho_ii */

@@ -28,7 +28,7 @@ from qsim_amd import _lib  # noqa: E402
 
 n = int(os.environ.get("QUBITS", 30))
 world = int(os.environ.get("WORLD", 8))
-runs = int(os.environ.get("RUNS", 6))
+runs = int(os.environ.get("RUNS", 8))
 seed = int(os.environ.get("SEED", 42))
 carry_on = os.environ.get("QSIM_DIST_CARRY", "0") != "0"  # (the engine's default: off)
 L = n - (world.bit_length() - 1)

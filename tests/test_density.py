@@ -186,3 +186,52 @@ def test_reference_compatible_y(qsim, oracle, gpu_ready, n, seed):
         np.testing.assert_allclose(sim.getDensityMatrix(), want, atol=1e-12, rtol=0)
     ny = sum(1 for g in c.getGates() if g.type == qsim.GateType.Y)
     assert abs(np.trace(want).real - (-1) ** ny) < 1e-10
+
+
+def _dm_jit_source(qsim, n, circuit, channels):
+    import ctypes
+    from qsim_amd import _lib
+    g, ng = circuit.to_abi()
+    arr = (_lib.qsim_noise_channel * max(1, len(channels)))()
+    for i, (t, qb, p) in enumerate(channels):
+        arr[i].type, arr[i].qubit, arr[i].probability = t, qb, p
+    size = ctypes.c_size_t()
+    _lib.check(_lib.hip.qsim_dm_jit_source(n, g, ng, arr, len(channels), 1, None, 0, ctypes.byref(size)))
+    buf = ctypes.create_string_buffer(size.value + 1)
+    _lib.check(_lib.hip.qsim_dm_jit_source(n, g, ng, arr, len(channels), 1, buf, size.value + 1,
+                                           ctypes.byref(size)))
+    return buf.value.decode()
+
+
+def test_channel_triples_emitted_as_one_scale(qsim):
+    """Host-only: the depolarizing / phase-damping / phase-flip lowering CX · diag(1, g) · CX
+    (density.hip dm_channel) is generated as one per-register scale by g where the row and column
+    bits differ (jit.hip Gen::xor_diag), so the circuit-specialised DM kernels carry far fewer
+    per-lane selects than three ops would."""
+    n = 14
+    c = qsim.createRandomHCCircuit(n, 100, 42)
+    src = _dm_jit_source(qsim, n, c, [(0, -1, 0.01)])
+    assert src.count("__global__") >= 6
+    g = repr(1.0 - 4.0 * 0.01 / 3.0)
+    fused = sum(1 for line in src.splitlines() if line.lstrip().startswith("const double f") and "1.0" in line)
+    assert fused > 0 or g in src  # per-lane factor pairs (thread-bit rows) or compile-time scales
+    assert src.count("qsel(") < 1200  # (2 657 with the three ops emitted one by one)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,seed", [(6, 11), (7, 12)])
+def test_specialised_kernels_match_oracle(qsim, oracle, gpu_ready, n, seed):
+    """The DM passes as circuit-specialised kernels (JIT forced below its 20-bit threshold), every
+    channel type: the full rho equals the oracle at 1e-12 (the fused channel scales included)."""
+    from qsim_amd.plan import set_jit
+    c = _circuit(qsim, n, 40, seed)
+    channels = [(0, -1, 0.05), (2, 1, 0.2), (4, n - 1, 0.15), (5, 0, 0.1), (1, 2, 0.3), (3, 3, 0.1)]
+    want = oracle.dm_run(n, oracle.gates_of(c), channels)
+    set_jit(2, 0)
+    try:
+        sim = qsim.DensityMatrixSimulator(n, _noise(qsim, channels))
+        sim.run(c)
+        got = sim.getDensityMatrix()
+    finally:
+        set_jit(1, 20)
+    np.testing.assert_allclose(got, want, atol=1e-12, rtol=0)
