@@ -460,6 +460,14 @@ static void canonicalize(qsim_state* s) {
     s->perm.clear();
     if (!swaps.empty()) run_fused(s, swaps, false);
 }
+// Before an entry that overwrites every amplitude: the labels are dropped, not restored.
+static void drop_layout(qsim_state* s) {
+    if (s->relayout) {  // (a relayout plan's second buffer: as canonicalize would leave it)
+        canonicalize(s);
+    }
+    s->perm.clear();
+    s->basis = false;
+}
 // Before an entry that reads amplitudes by index (touch: and writes them).
 static void prep(qsim_state* s, bool touch) {
     canonicalize(s);
@@ -768,6 +776,37 @@ static void choose_first_layout(qsim_state* s, const qsim_gate* gates, size_t co
     if (heights) s->tile_h = w.h;
     s->perm = std::move(w.perm);
     memo_put(s->perm);
+}
+
+// An op with every index bit moved through pi (bit b -> position pi[b]).
+static Op permute_op(Op o, const std::vector<int>& pi) {
+    o.t0 = pi[o.t0];
+    if (o.t1 >= 0) o.t1 = pi[o.t1];
+    uint64_t m = 0;
+    for (uint64_t c = o.cmask; c; c &= c - 1) m |= 1ull << pi[__builtin_ctzll(c)];
+    o.cmask = m;
+    return o;
+}
+// Density-matrix relabeling: the 2n index bits of rho under a permutation that plans the lowered
+// circuit (density.hip dm_lower) into fewer passes — the state-vector search (relabel.hip
+// choose_layout: seeded random labelings, the fewest-pass ones annealed on the layout cost
+// model) over bit positions rather than qubits, so row and column bits move independently.
+// QSIM_DM_RELABEL_TRIES (default 48) labelings; 0 turns it off.
+static int dm_relabel_tries() {
+    static const int v = [] {
+        const char* e = std::getenv("QSIM_DM_RELABEL_TRIES");
+        return e ? std::max(0, std::atoi(e)) : 48;
+    }();
+    return v;
+}
+static LayoutChoice dm_choose_layout(int nbits, const std::vector<Op>& ops) {
+    auto lower = [&](const std::vector<int>& pi) {
+        std::vector<Op> out;
+        out.reserve(ops.size());
+        for (const Op& o : ops) out.push_back(permute_op(o, pi));
+        return out;
+    };
+    return choose_layout(nbits, lower, dm_relabel_tries(), 0);
 }
 
 static qsim_gate map_gate(const qsim_state* s, const qsim_gate& g) {
@@ -1598,13 +1637,42 @@ int qsim_dm_run(qsim_state* s, int n, const qsim_gate* gates, size_t count,
         QSIM_REQUIRE(gates || count == 0, QSIM_ERR_INVALID_ARGUMENT, "null gate list");
         QSIM_REQUIRE(channels || n_channels == 0, QSIM_ERR_INVALID_ARGUMENT, "null channel list");
         DeviceGuard dg(s->device);
-        prep(s, true);
         std::vector<Op> ops;
         dm_lower(n, gates, count, channels, n_channels, ops, (flags & QSIM_DM_REFERENCE_Y) != 0);
         // the state-vector size rule for the 2n index bits (13-qubit tiles for 26-28 bits: DM 13-14
         // qubits; W-HC + depolarizing at 14 qubits 6.87 k -> 7.35 k gates/s, 8 -> 7 passes)
         const int th = tile_height_for(s->n);
         const TileHeightScope tile_h(th, tile_rb_for(s->n, th));
+        // First fused run on |0><0| (a reset rho: basis index 0, which every labeling leaves at 0):
+        // choose the index-bit labels (dm_choose_layout; W-HC + depolarizing 14q: 7 -> 6 passes),
+        // memoised per (circuit, channels, flags).  Later runs keep the labels and map their ops
+        // through them; readers restore the identity first (prep).  A pinned state (handed-out
+        // device pointer) is never relabeled.
+        const bool fresh = (flags & QSIM_RUN_FUSED) && !s->pinned && s->basis && s->basis_idx == 0 &&
+                           s->perm.empty() && count > 0 && s->n >= 16 && dm_relabel_tries() > 0;
+        if (fresh) {
+            std::vector<unsigned char> key(count * sizeof(qsim_gate) + n_channels * sizeof(qsim_noise_channel) +
+                                           sizeof(int));
+            std::memcpy(key.data(), gates, count * sizeof(qsim_gate));
+            if (n_channels) std::memcpy(key.data() + count * sizeof(qsim_gate), channels, n_channels * sizeof(qsim_noise_channel));
+            std::memcpy(key.data() + key.size() - sizeof(int), &flags, sizeof(int));
+            std::vector<int> memo;
+            if (layout_memo_get(s->n, 3, key.data(), key.size(), memo, nullptr)) {
+                s->perm = memo;
+            } else {
+                LayoutChoice lc = dm_choose_layout(s->n, ops);
+                if (!lc.perm.empty()) {
+                    s->plans.put(lc.ops, s->n, std::move(lc.plan), s->stream);
+                    s->perm = lc.perm;
+                }
+                layout_memo_put(s->n, 3, key.data(), key.size(), s->perm, -1);
+            }
+        } else if (s->pinned || s->relayout) {
+            prep(s, true);  // (identity labels; a relayout-plan layout is the state vector's own)
+        }
+        s->basis = false;
+        if (!s->perm.empty())
+            for (Op& o : ops) o = permute_op(o, s->perm);
         if (flags & QSIM_RUN_FUSED) run_fused(s, ops);
         else for (const Op& op : ops) launch_op(s->d, s->n, 1, op, s->stream, &s->timer);
     });
@@ -1620,7 +1688,11 @@ int qsim_dm_plan_info(int n, const qsim_gate* gates, size_t count, const qsim_no
         dm_lower(n, gates, count, channels, n_channels, ops, (flags & QSIM_DM_REFERENCE_Y) != 0);
         const int th = tile_height_for(2 * n);
         const TileHeightScope tile_h(th, tile_rb_for(2 * n, th));
-        const Plan plan = plan_fused(ops, 2 * n);  // (as qsim_dm_run's run_fused plans it)
+        Plan plan;
+        LayoutChoice lc;
+        if (flags & QSIM_DM_PLAN_RELABELED) lc = dm_choose_layout(2 * n, ops);
+        if (!lc.perm.empty()) plan = std::move(lc.plan);
+        else plan = plan_fused(ops, 2 * n);  // (as qsim_dm_run's run_fused plans it)
         for (size_t p = 0; p < plan.passes.size() && p < cap && info; ++p) {
             const FusedPass& fp = plan.passes[p];
             int nops = 0;
@@ -1684,7 +1756,7 @@ int qsim_dm_init_pure(qsim_state* s, int n, const double* psi) {
         check_dm(s, n);
         QSIM_REQUIRE(psi, QSIM_ERR_INVALID_ARGUMENT, "null state");
         DeviceGuard dg(s->device);
-        prep(s, true);
+        drop_layout(s);
         double2* d_psi = (double2*)s->scratch.get(sizeof(double2) << n, s->stream);
         QSIM_HIPCHK(hipMemcpyAsync(d_psi, psi, sizeof(double2) << n, hipMemcpyHostToDevice, s->stream));
         launch_dm_init(s->d, d_psi, n, s->stream);
@@ -1696,7 +1768,7 @@ int qsim_dm_init_maximally_mixed(qsim_state* s, int n) {
     return guarded([&] {
         check_dm(s, n);
         DeviceGuard dg(s->device);
-        prep(s, true);
+        drop_layout(s);
         launch_dm_init(s->d, nullptr, n, s->stream);
         QSIM_HIPCHK(hipStreamSynchronize(s->stream));
     });

@@ -354,7 +354,9 @@ int qsim_dm_run(qsim_state* rho, int n_qubits, const qsim_gate* gates, size_t co
                 const qsim_noise_channel* channels, size_t n_channels, int flags);
 /* Host-only: the fused plan qsim_dm_run (QSIM_RUN_FUSED) would run for this circuit, four ints
  * per pass: tile height h (tile = 64 << h elements; -1: a per-gate step), ops, register stages,
- * contiguous run bits r0. */
+ * contiguous run bits r0.  With QSIM_DM_PLAN_RELABELED in flags: the plan under the index-bit
+ * labels a first run on |0><0| chooses. */
+#define QSIM_DM_PLAN_RELABELED 0x100
 int qsim_dm_plan_info(int n_qubits, const qsim_gate* gates, size_t count, const qsim_noise_channel* channels,
                       size_t n_channels, int flags, int32_t* info, size_t cap, size_t* n_passes);
 /* Host-only: the circuit-specialised kernel source of that plan (as qsim_jit_source). */

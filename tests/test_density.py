@@ -235,3 +235,49 @@ def test_specialised_kernels_match_oracle(qsim, oracle, gpu_ready, n, seed):
     finally:
         set_jit(1, 20)
     np.testing.assert_allclose(got, want, atol=1e-12, rtol=0)
+
+
+def test_relabeled_plan_has_fewer_passes(qsim):
+    """Host-only (qsim_dm_plan_info with QSIM_DM_PLAN_RELABELED): the first-run index-bit labels
+    (capi.hip dm_choose_layout) plan the bench's DM circuit into fewer passes than the identity."""
+    import ctypes
+    from qsim_amd import _lib
+    n = 14
+    c = qsim.createRandomHCCircuit(n, 100, 42)
+    g, ng = c.to_abi()
+    arr = (_lib.qsim_noise_channel * 1)()
+    arr[0].type, arr[0].qubit, arr[0].probability = 0, -1, 0.01
+    passes = []
+    for flags in (1, 1 | 0x100):
+        info = (ctypes.c_int32 * 400)()
+        npass = ctypes.c_size_t()
+        _lib.check(_lib.hip.qsim_dm_plan_info(n, g, ng, arr, 1, flags, info, 100, ctypes.byref(npass)))
+        passes.append(npass.value)
+    assert passes[1] < passes[0], passes
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,depth,seed", [(8, 30, 21), (9, 16, 22)])
+def test_relabeled_runs_match_oracle(qsim, oracle, gpu_ready, n, depth, seed):
+    """16 / 18 index bits: the first fused run of a reset rho takes relabeled index bits
+    (capi.hip qsim_dm_run); a second run keeps them (its ops mapped through the labels); readers
+    restore the identity first.  Every step equals the oracle at 1e-12, and a reset + rerun (the
+    memoised labels) gives the same rho."""
+    channels = [(0, -1, 0.03), (2, 1, 0.2), (1, 2, 0.1), (3, n - 1, 0.05), (4, 0, 0.1)]
+    c1 = _circuit(qsim, n, depth, seed)
+    c2 = _circuit(qsim, n, depth // 2, seed + 100)
+    want1 = oracle.dm_run(n, oracle.gates_of(c1), channels)
+    want2 = oracle.dm_run(n, oracle.gates_of(c2), channels, rho=want1)
+    want3 = oracle.dm_channel(want2, n, 1, 3, 0.25)
+    sim = qsim.DensityMatrixSimulator(n, _noise(qsim, channels))
+    sim.run(c1)
+    sim.run(c2)  # (no reader in between: still under the first run's labels)
+    sim.run(qsim.Circuit(n))  # (an empty run keeps the state as it is)
+    np.testing.assert_allclose(sim.getDensityMatrix(), want2, atol=1e-12, rtol=0)
+    sim.applyChannel(qsim.NoiseType.AmplitudeDamping, 3, 0.25)
+    np.testing.assert_allclose(sim.getDensityMatrix(), want3, atol=1e-12, rtol=0)
+    sim.reset()
+    sim.run(c1)
+    np.testing.assert_allclose(sim.getProbabilities(), np.real(np.diag(want1)), atol=1e-12, rtol=0)
+    np.testing.assert_allclose(sim.getDensityMatrix(), want1, atol=1e-12, rtol=0)
+    assert abs(sim.getPurity() - np.sum(np.abs(want1) ** 2)) < 1e-12
