@@ -799,14 +799,14 @@ static int dm_relabel_tries() {
     }();
     return v;
 }
-static LayoutChoice dm_choose_layout(int nbits, const std::vector<Op>& ops) {
+static LayoutChoice dm_choose_layout(int nbits, const std::vector<Op>& ops, size_t want_alts = 0) {
     auto lower = [&](const std::vector<int>& pi) {
         std::vector<Op> out;
         out.reserve(ops.size());
         for (const Op& o : ops) out.push_back(permute_op(o, pi));
         return out;
     };
-    return choose_layout(nbits, lower, dm_relabel_tries(), 0);
+    return choose_layout(nbits, lower, dm_relabel_tries(), want_alts);
 }
 
 static qsim_gate map_gate(const qsim_state* s, const qsim_gate& g) {
@@ -1660,8 +1660,23 @@ int qsim_dm_run(qsim_state* s, int n, const qsim_gate* gates, size_t count,
             if (layout_memo_get(s->n, 3, key.data(), key.size(), memo, nullptr)) {
                 s->perm = memo;
             } else {
-                LayoutChoice lc = dm_choose_layout(s->n, ops);
-                if (!lc.perm.empty()) {
+                // with layout calibration (inline compilation, >= 26 index bits by default) the
+                // fewest-pass candidates are timed on the device, as a state vector's are: the
+                // cost model prices run lengths, not the register stages that DM passes spend
+                // most of their time in (QSIM_DM_RELABEL_CANDIDATES, default 4)
+                static const size_t alts = [] {
+                    const char* e = std::getenv("QSIM_DM_RELABEL_CANDIDATES");
+                    return (size_t)std::max(1, e ? std::atoi(e) : 4) - 1;
+                }();
+                LayoutChoice lc = dm_choose_layout(s->n, ops, relabel_calibrate(s->n) ? alts : 0);
+                if (!lc.perm.empty() && !lc.alts.empty()) {
+                    std::vector<LayoutCandidate> cands;
+                    cands.push_back(LayoutCandidate{th, lc.perm, std::move(lc.ops), std::move(lc.plan), false});
+                    for (LayoutChoice::Alt& a : lc.alts)
+                        cands.push_back(LayoutCandidate{th, a.perm, std::move(a.ops), std::move(a.plan), false});
+                    s->perm = cands[calibrate_candidates(s, cands)].perm;  // (every plan stays cached)
+                    s->calibrated = true;
+                } else if (!lc.perm.empty()) {
                     s->plans.put(lc.ops, s->n, std::move(lc.plan), s->stream);
                     s->perm = lc.perm;
                 }

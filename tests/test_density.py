@@ -257,12 +257,27 @@ def test_relabeled_plan_has_fewer_passes(qsim):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n,depth,seed", [(8, 30, 21), (9, 16, 22)])
-def test_relabeled_runs_match_oracle(qsim, oracle, gpu_ready, n, depth, seed):
+@pytest.mark.parametrize("n,depth,seed,timed", [(8, 30, 21, False), (9, 16, 22, False), (8, 24, 23, True)])
+def test_relabeled_runs_match_oracle(qsim, oracle, gpu_ready, n, depth, seed, timed):
     """16 / 18 index bits: the first fused run of a reset rho takes relabeled index bits
-    (capi.hip qsim_dm_run); a second run keeps them (its ops mapped through the labels); readers
-    restore the identity first.  Every step equals the oracle at 1e-12, and a reset + rerun (the
-    memoised labels) gives the same rho."""
+    (capi.hip qsim_dm_run; timed: the candidates timed on the device, specialised kernels); a
+    second run keeps them (its ops mapped through the labels); readers restore the identity first.
+    Every step equals the oracle at 1e-12, and a reset + rerun (the memoised labels) gives the
+    same rho."""
+    if timed:
+        from qsim_amd.plan import set_calibrate, set_jit
+        set_jit(2, 0)
+        set_calibrate(1, 16)
+        try:
+            _relabeled_runs(qsim, oracle, n, depth, seed)
+        finally:
+            set_calibrate(1, 26)
+            set_jit(1, 20)
+    else:
+        _relabeled_runs(qsim, oracle, n, depth, seed)
+
+
+def _relabeled_runs(qsim, oracle, n, depth, seed):
     channels = [(0, -1, 0.03), (2, 1, 0.2), (1, 2, 0.1), (3, n - 1, 0.05), (4, 0, 0.1)]
     c1 = _circuit(qsim, n, depth, seed)
     c2 = _circuit(qsim, n, depth // 2, seed + 100)
