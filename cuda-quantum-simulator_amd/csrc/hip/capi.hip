@@ -791,13 +791,15 @@ static Op permute_op(Op o, const std::vector<int>& pi) {
 // circuit (density.hip dm_lower) into fewer passes — the state-vector search (relabel.hip
 // choose_layout: seeded random labelings, the fewest-pass ones annealed on the layout cost
 // model) over bit positions rather than qubits, so row and column bits move independently.
-// QSIM_DM_RELABEL_TRIES (default 48) labelings; 0 turns it off.
-static int dm_relabel_tries() {
+// QSIM_DM_RELABEL_TRIES labelings (default 48, about 1 s of host planning at 14 qubits; 256 when
+// the candidates are timed on the device — more fewest-pass candidates to time: 14q 9.19k ->
+// 9.52k gates/s); 0 turns it off.
+static int dm_relabel_tries(bool timed = false) {
     static const int v = [] {
         const char* e = std::getenv("QSIM_DM_RELABEL_TRIES");
-        return e ? std::max(0, std::atoi(e)) : 48;
+        return e ? std::max(0, std::atoi(e)) : -1;
     }();
-    return v;
+    return v >= 0 ? v : timed ? 256 : 48;
 }
 static LayoutChoice dm_choose_layout(int nbits, const std::vector<Op>& ops, size_t want_alts = 0) {
     auto lower = [&](const std::vector<int>& pi) {
@@ -806,7 +808,7 @@ static LayoutChoice dm_choose_layout(int nbits, const std::vector<Op>& ops, size
         for (const Op& o : ops) out.push_back(permute_op(o, pi));
         return out;
     };
-    return choose_layout(nbits, lower, dm_relabel_tries(), want_alts);
+    return choose_layout(nbits, lower, dm_relabel_tries(want_alts > 0), want_alts);
 }
 
 static qsim_gate map_gate(const qsim_state* s, const qsim_gate& g) {
@@ -1663,10 +1665,11 @@ int qsim_dm_run(qsim_state* s, int n, const qsim_gate* gates, size_t count,
                 // with layout calibration (inline compilation, >= 26 index bits by default) the
                 // fewest-pass candidates are timed on the device, as a state vector's are: the
                 // cost model prices run lengths, not the register stages that DM passes spend
-                // most of their time in (QSIM_DM_RELABEL_CANDIDATES, default 4)
+                // most of their time in (QSIM_DM_RELABEL_CANDIDATES, default 8; 14q: the 6-pass
+                // candidates run 10.4-11.9 ms)
                 static const size_t alts = [] {
                     const char* e = std::getenv("QSIM_DM_RELABEL_CANDIDATES");
-                    return (size_t)std::max(1, e ? std::atoi(e) : 4) - 1;
+                    return (size_t)std::max(1, e ? std::atoi(e) : 8) - 1;
                 }();
                 LayoutChoice lc = dm_choose_layout(s->n, ops, relabel_calibrate(s->n) ? alts : 0);
                 if (!lc.perm.empty() && !lc.alts.empty()) {
