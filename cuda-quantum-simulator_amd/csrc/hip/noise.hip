@@ -70,7 +70,7 @@ struct FlipChan {
     int target;
     int type;    // 0 depolarizing, 3 X, 4 Z, 5 Y
     int always;  // P == 1: every pair flips
-    int pad;
+    float il2;   // ln 2 / lq (the single-precision first try of next_flip; 0: always double)
 };
 // Next flip of a block's walk inside [lo, hi): false when the block is exhausted.
 struct FlipCursor {
@@ -87,7 +87,19 @@ __device__ __forceinline__ bool next_flip(FlipCursor& cur, uint64_t b, uint64_t 
             cur.pos += 1;
         } else {
             const double u = (double)((h >> 11) + 1ull) * 0x1.0p-53;  // (0, 1]
-            const double gap = floor(log(u) / c.lq);
+            // gap = floor(ln u / lq) in double.  First in single precision (the hardware log2):
+            // its error bound is tiny next to the distance from the nearest integer except in a
+            // fraction ~1e-4 of draws, which take the double path — so the result is always
+            // the double one (the flips, hence the states, do not change).
+            double gap;
+            const float gf = __log2f((float)u) * c.il2;
+            const float fl = floorf(gf);
+            // error of gf: |il2| x (rounding of u, <= 2^-24 / ln 2, + the hardware log2's error)
+            // + |gf| x (its relative error and two roundings) — bounded here with a wide margin
+            // (2^-16 relative, 2^-13 x |il2| absolute; a few per cent of draws fall back at p = 0.01)
+            const float err = fabsf(gf) * 0x1.0p-16f + fabsf(c.il2) * 0x1.0p-13f;
+            if (c.il2 != 0.0f && gf - fl > err && fl + 1.0f - gf > err && gf < 4.0e6f) gap = (double)fl;
+            else gap = floor(log(u) / c.lq);
             if (gap >= (double)kFlipBlock) {
                 cur.done = true;
                 break;
@@ -290,6 +302,11 @@ static bool flip_channel(int type, int qubit, double p, uint64_t key, FlipChan& 
     c.type = type;
     c.always = P >= 1.0 ? 1 : 0;
     c.lq = c.always ? -1.0 : std::log1p(-P);
+    // (QSIM_NOISE_FAST_LOG=0: the double log for every draw — tests and measurements; read per
+    // channel set-up, on the host)
+    const char* fe = std::getenv("QSIM_NOISE_FAST_LOG");
+    const bool fast = fe == nullptr || std::atoi(fe) != 0;
+    c.il2 = fast && !c.always ? (float)(0.69314718055994530942 / c.lq) : 0.0f;
     return true;
 }
 
@@ -903,7 +920,8 @@ void launch_gate_noise_run(double2* st, int n, uint64_t batch, uint64_t traj0, c
 constexpr int kRegionLogMax = 12;
 constexpr int kMinPullQubits = 9;
 constexpr int kMaxPullChannels = 32;
-constexpr int kWordThreads = 256;
+constexpr int kWordThreads = 256;     // (the least; launches size the work-group to the walk count)
+constexpr int kWordThreadsMax = 512;
 struct MapArgs {
     void* words;
     uint64_t amps;       // batch << n (this object's)
@@ -931,15 +949,16 @@ __device__ __forceinline__ void walk_block(uint64_t gb, const FlipChan& c, F&& f
 }
 
 template <class W>
-__global__ __launch_bounds__(kWordThreads) void k_noise_words(MapArgs a) {
+__global__ __launch_bounds__(kWordThreadsMax) void k_noise_words(MapArgs a) {
     __shared__ W w[1 << kRegionLogMax];
     const int t = threadIdx.x;
     const int R = 1 << a.rl;
-    for (int i = t; i < R; i += kWordThreads) w[i] = 0;
+    const int T = (int)blockDim.x;
+    for (int i = t; i < R; i += T) w[i] = 0;
     __syncthreads();
     const uint64_t K0 = (uint64_t)blockIdx.x << a.rl;  // the region's first amplitude (this object)
     const uint64_t traj = K0 >> a.n, r0 = K0 & ((1ull << a.n) - 1ull);
-    for (int task = t; task < a.task_off[a.nch]; task += kWordThreads) {
+    for (int task = t; task < a.task_off[a.nch]; task += T) {
         int c = 0;
         while (task >= a.task_off[c + 1]) ++c;
         const int j = task - a.task_off[c];
@@ -967,7 +986,7 @@ __global__ __launch_bounds__(kWordThreads) void k_noise_words(MapArgs a) {
     }
     __syncthreads();
     W* out = static_cast<W*>(a.words) + K0;
-    for (int i = t; i < R; i += kWordThreads) out[i] = w[i];
+    for (int i = t; i < R; i += T) out[i] = w[i];
 }
 
 struct PullArgs {
@@ -1150,8 +1169,18 @@ void launch_noise_map(int n, uint64_t batch, uint64_t traj0, const std::vector<N
         m.task_off[c + 1] = m.task_off[c] + (1 << (m.ch[c].target < m.rl ? m.rl - 9 : m.rl - 8));
     TimedLaunch tl(tm, "noise_map", 0.0, s);
     const dim3 grid((unsigned)(amps >> m.rl));
-    if (wb == sizeof(uint32_t)) hipLaunchKernelGGL(k_noise_words<uint32_t>, grid, dim3(kWordThreads), 0, s, m);
-    else hipLaunchKernelGGL(k_noise_words<unsigned long long>, grid, dim3(kWordThreads), 0, s, m);
+    // one walk per thread where the work-group allows it (26 channels at 26 qubits: 320 walks per
+    // region, one round of 320 threads instead of two rounds of 256 — the walks are the kernel's
+    // time; QSIM_NOISE_WORD_THREADS overrides, measurements)
+    static const int wt_env = [] {
+        const char* e = std::getenv("QSIM_NOISE_WORD_THREADS");
+        return e ? std::atoi(e) : 0;
+    }();
+    const int tasks = m.task_off[m.nch];
+    int wt = wt_env > 0 ? wt_env : ((tasks + 63) / 64) * 64;
+    wt = std::max(kWordThreads, std::min(kWordThreadsMax, (wt + 63) / 64 * 64));
+    if (wb == sizeof(uint32_t)) hipLaunchKernelGGL(k_noise_words<uint32_t>, grid, dim3(wt), 0, s, m);
+    else hipLaunchKernelGGL(k_noise_words<unsigned long long>, grid, dim3(wt), 0, s, m);
     QSIM_HIPCHK(hipGetLastError());
 }
 
