@@ -365,3 +365,37 @@ def test_gate_noise_tile_split_parts_equal_one_part(qsim, oracle, gpu_ready, mon
         whole, counter = oracle.batched_reference_run(n, B, oracle.gates_of(c), entries, 17, False,
                                                       states=whole, counter=counter)
     np.testing.assert_allclose(out[1], whole, atol=1e-12, rtol=0)
+
+
+@pytest.mark.parametrize("p", [0.01, 0.3, 1e-4, 0.9])
+def test_single_precision_gap_draws_equal_double(qsim, gpu_ready, monkeypatch, p):
+    """noise.hip next_flip takes each geometric gap from the hardware single-precision log2 unless
+    the value lies within its error bound of an integer (then the double log): the trajectories
+    equal the all-double walks bit for bit (QSIM_NOISE_FAST_LOG=0) — millions of draws at config-4
+    shape, the in-tile lists, the pushed suffix and the pulled NoisySimulator words alike."""
+    n, B = 16, 64
+    nm = qsim.NoiseModel()
+    nm.addDepolarizingAll(n, p)
+    c = qsim.createRandomHCCircuit(n, 30, 7)
+    out = []
+    for fast in ("1", "0"):
+        monkeypatch.setenv("QSIM_NOISE_FAST_LOG", fast)
+        s = qsim.BatchedSimulator(n, B, nm, noise=qsim.BatchedNoise.Reference)
+        s.setSeed(11)
+        s.run(c)
+        out.append(np.stack([s.getStateVector(t) for t in (0, 17, 40, 63)]))
+        s.close()
+    assert np.array_equal(out[0], out[1])
+    m = 20
+    nm2 = qsim.NoiseModel()
+    nm2.addDepolarizingAll(m, p)
+    c2 = qsim.createRandomHCCircuit(m, 20, 8)
+    got = []
+    for fast in ("1", "0"):
+        monkeypatch.setenv("QSIM_NOISE_FAST_LOG", fast)
+        sim = qsim.NoisySimulator(m, nm2)
+        sim.setSeed(5)
+        sim.run(c2)
+        got.append(sim.getStateVector())
+        del sim
+    assert np.array_equal(got[0], got[1])
