@@ -920,8 +920,7 @@ void launch_gate_noise_run(double2* st, int n, uint64_t batch, uint64_t traj0, c
 constexpr int kRegionLogMax = 12;
 constexpr int kMinPullQubits = 9;
 constexpr int kMaxPullChannels = 32;
-constexpr int kWordThreads = 256;     // (the least; launches size the work-group to the walk count)
-constexpr int kWordThreadsMax = 512;
+constexpr int kWordThreads = 256;
 struct MapArgs {
     void* words;
     uint64_t amps;       // batch << n (this object's)
@@ -949,16 +948,15 @@ __device__ __forceinline__ void walk_block(uint64_t gb, const FlipChan& c, F&& f
 }
 
 template <class W>
-__global__ __launch_bounds__(kWordThreadsMax) void k_noise_words(MapArgs a) {
+__global__ __launch_bounds__(kWordThreads) void k_noise_words(MapArgs a) {
     __shared__ W w[1 << kRegionLogMax];
     const int t = threadIdx.x;
     const int R = 1 << a.rl;
-    const int T = (int)blockDim.x;
-    for (int i = t; i < R; i += T) w[i] = 0;
+    for (int i = t; i < R; i += kWordThreads) w[i] = 0;
     __syncthreads();
     const uint64_t K0 = (uint64_t)blockIdx.x << a.rl;  // the region's first amplitude (this object)
     const uint64_t traj = K0 >> a.n, r0 = K0 & ((1ull << a.n) - 1ull);
-    for (int task = t; task < a.task_off[a.nch]; task += T) {
+    for (int task = t; task < a.task_off[a.nch]; task += kWordThreads) {
         int c = 0;
         while (task >= a.task_off[c + 1]) ++c;
         const int j = task - a.task_off[c];
@@ -986,7 +984,7 @@ __global__ __launch_bounds__(kWordThreadsMax) void k_noise_words(MapArgs a) {
     }
     __syncthreads();
     W* out = static_cast<W*>(a.words) + K0;
-    for (int i = t; i < R; i += T) out[i] = w[i];
+    for (int i = t; i < R; i += kWordThreads) out[i] = w[i];
 }
 
 struct PullArgs {
@@ -1169,18 +1167,11 @@ void launch_noise_map(int n, uint64_t batch, uint64_t traj0, const std::vector<N
         m.task_off[c + 1] = m.task_off[c] + (1 << (m.ch[c].target < m.rl ? m.rl - 9 : m.rl - 8));
     TimedLaunch tl(tm, "noise_map", 0.0, s);
     const dim3 grid((unsigned)(amps >> m.rl));
-    // one walk per thread where the work-group allows it (26 channels at 26 qubits: 320 walks per
-    // region, one round of 320 threads instead of two rounds of 256 — the walks are the kernel's
-    // time; QSIM_NOISE_WORD_THREADS overrides, measurements)
-    static const int wt_env = [] {
-        const char* e = std::getenv("QSIM_NOISE_WORD_THREADS");
-        return e ? std::atoi(e) : 0;
-    }();
-    const int tasks = m.task_off[m.nch];
-    int wt = wt_env > 0 ? wt_env : ((tasks + 63) / 64) * 64;
-    wt = std::max(kWordThreads, std::min(kWordThreadsMax, (wt + 63) / 64 * 64));
-    if (wb == sizeof(uint32_t)) hipLaunchKernelGGL(k_noise_words<uint32_t>, grid, dim3(wt), 0, s, m);
-    else hipLaunchKernelGGL(k_noise_words<unsigned long long>, grid, dim3(wt), 0, s, m);
+    // (256-thread work-groups: one round of 320 threads for the 320 walks of a 26-qubit region
+    // shortens the map alone, 0.240 -> 0.218 ms, but the overlapped step loses: 1 112 -> 1 067
+    // gates/s, profiles/r05/fast_log/)
+    if (wb == sizeof(uint32_t)) hipLaunchKernelGGL(k_noise_words<uint32_t>, grid, dim3(kWordThreads), 0, s, m);
+    else hipLaunchKernelGGL(k_noise_words<unsigned long long>, grid, dim3(kWordThreads), 0, s, m);
     QSIM_HIPCHK(hipGetLastError());
 }
 
