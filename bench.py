@@ -586,7 +586,7 @@ def measure_noisy(q, n, steps, warmup, seed, depth, p_noise):
     # the noise kernels: the per-channel passes (push) or the pull pass, which applies the flips
     # of the step before while it applies the gate (its bytes: one read + one write of the state
     # plus the code words), with its PMC traffic (profiles/pmc_noisy_26q.json)
-    noise = [s for s in serial if s["name"] in ("noise", "pull_gate")]
+    noise = [s for s in serial if s["name"] in ("noise", "pull_gate", "pull_gate_map")]
     noise_roof = _dominant_roofline(noise) if noise else None
     pmc_path = os.path.join(ROOT, "profiles", f"pmc_noisy_{n}q.json")
     if noise_roof and os.path.exists(pmc_path):

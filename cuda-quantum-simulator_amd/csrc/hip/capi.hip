@@ -1578,6 +1578,33 @@ int qsim_noisy_run(qsim_state* s, const qsim_gate* gates, size_t count,
             const uint64_t c0 = *counter;
             *counter += (uint64_t)G * n_channels;
             auto words = [&](size_t i) { return (void*)(s->noise_codes + (i & 1) * s->noise_codes_cap); };
+            // QSIM_NOISE_MAP_FUSED=1 (opt-in): step i's pass also builds step i + 1's words (its
+            // hash-and-log walks meant to fill its own memory stalls; noise.hip k_pull_gate<...,
+            // MAP>), one stream.  Measured slower at 26 qubits: 1.22 ms per fused pass against
+            // 0.70 + 0.24 ms apart, 815 vs 1 063 gates/s (the walks and their LDS cost the pass its
+            // occupancy), so the default is the word map as a kernel of its own, beside the pass
+            // (overlap) or before it.
+            const char* fe = std::getenv("QSIM_NOISE_MAP_FUSED");
+            if (fe != nullptr && std::atoi(fe) != 0 && G) {
+                launch_noise_map(s->n, 1, 0, chans, seed, c0, words(0), s->stream, &s->timer);
+                launch_op(s->d, s->n, 1, ops[0], s->stream, &s->timer);
+                for (size_t i = 0; i < G; ++i) {
+                    double2* dst = s->alt;
+                    const PullMapNext nx{0, seed, c0 + (i + 1) * n_channels, words(i + 1)};
+                    launch_pull_gate(s->d, dst, s->n, 1, chans, i + 1 < G ? &ops[i + 1] : nullptr, words(i), s->stream,
+                                     &s->timer, i + 1 < G ? &nx : nullptr);
+                    s->alt = s->d;
+                    s->d = dst;
+                }
+                if (s->pinned && s->d != home) {
+                    QSIM_HIPCHK(hipMemcpyAsync(home, s->d, sizeof(double2) << s->n, hipMemcpyDeviceToDevice,
+                                               s->stream));
+                    s->alt = s->d;
+                    s->d = home;
+                }
+                trim_noise_buffers(s);
+                return;
+            }
             hipStream_t ms = overlap ? s->noise_stream : s->stream;
             auto map = [&](size_t i) {
                 if (overlap && i >= 2) QSIM_HIPCHK(hipStreamWaitEvent(ms, s->nev_pull[i & 1], 0));

@@ -414,8 +414,14 @@ void launch_pull_noise_step(const double2* src, double2* dst, int n, uint64_t ba
 // step's pass runs (the map reads no amplitudes).
 void launch_noise_map(int n, uint64_t batch, uint64_t traj0, const std::vector<NoiseChan>& chans, uint64_t seed,
                       uint64_t counter0, void* words, hipStream_t s, Timer* tm);
+// next (optional): this pass also builds the NEXT step's code words (counter0: its first pass
+// counter) — the word map fused into the pull pass (QSIM_NOISE_MAP_FUSED).
+struct PullMapNext {
+    uint64_t traj0, seed, counter0;
+    void* words;
+};
 void launch_pull_gate(const double2* src, double2* dst, int n, uint64_t batch, const std::vector<NoiseChan>& chans,
-                      const Op* op, const void* words, hipStream_t s, Timer* tm);
+                      const Op* op, const void* words, hipStream_t s, Timer* tm, const PullMapNext* next = nullptr);
 
 // Density matrices as 2n-index-bit states (density.hip).
 void dm_lower(int n, const qsim_gate* gates, size_t count, const qsim_noise_channel* ch,

@@ -923,6 +923,7 @@ constexpr int kMaxPullChannels = 32;
 constexpr int kWordThreads = 256;
 struct MapArgs {
     void* words;
+    int rpw;             // (fused into the pull pass) regions per work-group
     uint64_t amps;       // batch << n (this object's)
     uint64_t idx0;       // global pair index of local pair 0
     int n, rl;           // qubits per trajectory, region log (min(12, n))
@@ -947,6 +948,37 @@ __device__ __forceinline__ void walk_block(uint64_t gb, const FlipChan& c, F&& f
     }
 }
 
+// Walk task `task` (channel c, j-th block of pairs with a member in the region starting at
+// amplitude K0 of 2^a.rl) and OR its flips' codes into the region's LDS words w.
+template <class W>
+__device__ __forceinline__ void map_task(const MapArgs& a, W* w, uint64_t K0, int task) {
+    const uint64_t traj = K0 >> a.n, r0 = K0 & ((1ull << a.n) - 1ull);
+    int c = 0;
+    while (task >= a.task_off[c + 1]) ++c;
+    const int j = task - a.task_off[c];
+    const FlipChan& ch = a.ch[c];
+    const int q = ch.target;
+    const W sh = (W)(2 * c);
+    uint64_t lbase;  // the first pair (this object's pair index) with a member in the region
+    if (q < a.rl) {  // both members in the region: 2^(rl-1) pairs
+        lbase = (traj << (a.n - 1)) + (r0 >> 1);
+    } else {         // one member in the region (bit q fixed): 2^rl consecutive pairs
+        lbase = (traj << (a.n - 1)) + (((r0 >> (q + 1)) << q) | (r0 & ((1ull << q) - 1ull)));
+    }
+    const uint64_t gb = ((a.idx0 + lbase) >> kFlipBlockLog) + (uint64_t)j;
+    walk_block(gb, ch, [&](uint32_t l, uint32_t code) {
+        const uint32_t lp = (uint32_t)j * (uint32_t)kFlipBlock + l;  // region-local pair
+        if (q < a.rl) {
+            const uint32_t lo = lp & ((1u << q) - 1u);
+            const uint32_t a0 = ((lp ^ lo) << 1) | lo;
+            atomicOr(&w[a0], (W)code << sh);
+            atomicOr(&w[a0 | (1u << q)], (W)code << sh);
+        } else {
+            atomicOr(&w[lp], (W)code << sh);
+        }
+    });
+}
+
 template <class W>
 __global__ __launch_bounds__(kWordThreads) void k_noise_words(MapArgs a) {
     __shared__ W w[1 << kRegionLogMax];
@@ -955,33 +987,7 @@ __global__ __launch_bounds__(kWordThreads) void k_noise_words(MapArgs a) {
     for (int i = t; i < R; i += kWordThreads) w[i] = 0;
     __syncthreads();
     const uint64_t K0 = (uint64_t)blockIdx.x << a.rl;  // the region's first amplitude (this object)
-    const uint64_t traj = K0 >> a.n, r0 = K0 & ((1ull << a.n) - 1ull);
-    for (int task = t; task < a.task_off[a.nch]; task += kWordThreads) {
-        int c = 0;
-        while (task >= a.task_off[c + 1]) ++c;
-        const int j = task - a.task_off[c];
-        const FlipChan& ch = a.ch[c];
-        const int q = ch.target;
-        const W sh = (W)(2 * c);
-        uint64_t lbase;  // the first pair (this object's pair index) with a member in the region
-        if (q < a.rl) {  // both members in the region: 2^(rl-1) pairs
-            lbase = (traj << (a.n - 1)) + (r0 >> 1);
-        } else {         // one member in the region (bit q fixed): 2^rl consecutive pairs
-            lbase = (traj << (a.n - 1)) + (((r0 >> (q + 1)) << q) | (r0 & ((1ull << q) - 1ull)));
-        }
-        const uint64_t gb = ((a.idx0 + lbase) >> kFlipBlockLog) + (uint64_t)j;
-        walk_block(gb, ch, [&](uint32_t l, uint32_t code) {
-            const uint32_t lp = (uint32_t)j * (uint32_t)kFlipBlock + l;  // region-local pair
-            if (q < a.rl) {
-                const uint32_t lo = lp & ((1u << q) - 1u);
-                const uint32_t a0 = ((lp ^ lo) << 1) | lo;
-                atomicOr(&w[a0], (W)code << sh);
-                atomicOr(&w[a0 | (1u << q)], (W)code << sh);
-            } else {
-                atomicOr(&w[lp], (W)code << sh);
-            }
-        });
-    }
+    for (int task = t; task < a.task_off[a.nch]; task += kWordThreads) map_task(a, w, K0, task);
     __syncthreads();
     W* out = static_cast<W*>(a.words) + K0;
     for (int i = t; i < R; i += kWordThreads) out[i] = w[i];
@@ -1038,18 +1044,54 @@ __device__ __forceinline__ double2 pull_walk(const PullArgs& a, const int* sq, c
 //   PAIR (2x2 with target >= 6): item = pair; both members' runs are contiguous across lanes.
 //   else item = amplitude: a 2x2 on a target below 6 takes the partner from the lane 2^t0 away
 //   (a wave holds both members), diagonals act per amplitude, SWAP / identity read their source.
-template <class W, bool PAIR, int kPullU, bool NT>
-__global__ __launch_bounds__(256) void k_pull_gate(PullArgs a) {
+// MAP: the work-group also builds the NEXT step's code words (m: its channels and keys, regions
+// of 2^m.rl amplitudes, m.rpw of them per work-group) while its own loads are in flight — the word
+// map's hash-and-log walks fill the pull pass's memory stalls instead of running as a kernel of
+// their own beside it (the two share HBM and overlapped by ~2 %, profiles/r05/noisy_probe/).
+constexpr int kMapRegionLog = 10;  // 1 024 amplitudes per region in the fused form
+template <class W, bool MAP>
+struct PullMapLds {
+    W w[2 << kMapRegionLog];
+};
+template <class W>
+struct PullMapLds<W, false> {
+    W w[1];
+};
+template <class W, bool PAIR, int kPullU, bool NT, bool MAP = false>
+__global__ __launch_bounds__(256) void k_pull_gate(PullArgs a, MapArgs m) {
     __shared__ int sq[kMaxPullChannels];
+    __shared__ PullMapLds<W, MAP> lds;
     if (threadIdx.x < kMaxPullChannels) sq[threadIdx.x] = a.q[threadIdx.x];
+    if constexpr (MAP) {
+        const int R = m.rpw << m.rl;
+        for (int i = threadIdx.x; i < R; i += 256) lds.w[i] = 0;
+    }
     __syncthreads();
+    // the next step's words for regions blockIdx.x * rpw .. + rpw - 1 (after this work-group's
+    // loads are issued; their stores before its pulled walks)
+    auto build_map = [&]() {
+        if constexpr (MAP) {
+            const int tasks = m.task_off[m.nch];
+            for (int t = threadIdx.x; t < tasks * m.rpw; t += 256) {
+                const int r = t / tasks;
+                const uint64_t K0 = ((uint64_t)blockIdx.x * (uint64_t)m.rpw + (uint64_t)r) << m.rl;
+                map_task(m, lds.w + (r << m.rl), K0, t - r * tasks);
+            }
+            __syncthreads();
+            W* out = static_cast<W*>(m.words) + (((uint64_t)blockIdx.x * (uint64_t)m.rpw) << m.rl);
+            for (int i = threadIdx.x; i < (m.rpw << m.rl); i += 256) out[i] = lds.w[i];
+        }
+    };
     const W* words = static_cast<const W*>(a.words);
     const uint64_t base = ((uint64_t)blockIdx.x * kPullU) << 8;
     // items is a multiple of 256, so each item group u (256 consecutive items) is wholly in or
     // wholly out of range for the whole work-group; groups past the end do nothing (a 9- or
     // 10-qubit state has fewer items than one work-group's kPullU groups)
     const int nu = (int)std::min<uint64_t>((uint64_t)kPullU, (a.items - std::min(a.items, base)) >> 8);
-    if (nu == 0) return;
+    if (nu == 0) {
+        if constexpr (MAP) build_map();
+        return;
+    }
     if constexpr (PAIR) {
         uint64_t j0[kPullU];
         W w0[kPullU], w1[kPullU];
@@ -1066,6 +1108,7 @@ __global__ __launch_bounds__(256) void k_pull_gate(PullArgs a) {
             x0[u] = ld<NT>(a.src + j0[u]);
             x1[u] = ld<NT>(a.src + j1);
         }
+        build_map();
 #pragma unroll
         for (int u = 0; u < kPullU; ++u) {
             if (u >= nu) break;
@@ -1092,6 +1135,7 @@ __global__ __launch_bounds__(256) void k_pull_gate(PullArgs a) {
             w[u] = words[s];
             x[u] = ld<NT>(a.src + s);
         }
+        build_map();
 #pragma unroll
         for (int u = 0; u < kPullU; ++u) {
             if (u >= nu) break;
@@ -1176,11 +1220,27 @@ void launch_noise_map(int n, uint64_t batch, uint64_t traj0, const std::vector<N
 }
 
 void launch_pull_gate(const double2* src, double2* dst, int n, uint64_t batch, const std::vector<NoiseChan>& chans,
-                      const Op* op, const void* words, hipStream_t s, Timer* tm) {
+                      const Op* op, const void* words, hipStream_t s, Timer* tm, const PullMapNext* next) {
     const uint64_t amps = batch << n, pairs = amps >> 1;
     MapArgs m{};
     PullArgs a{};
     pull_channels(n, chans, 0, 0, m, a);  // (the live channels and their qubits; keys unused)
+    // the next step's words built by this pass (below), or by the word map before it
+    MapArgs nm{};
+    bool fuse = false;
+    if (next) {
+        PullArgs tmp{};
+        nm.words = next->words;
+        nm.amps = amps;
+        nm.idx0 = next->traj0 << (n - 1);
+        nm.n = n;
+        nm.rl = std::min(n, kMapRegionLog);
+        pull_channels(n, chans, next->seed, next->counter0, nm, tmp);
+        for (int c = 0; c < nm.nch; ++c)
+            nm.task_off[c + 1] = nm.task_off[c] + (1 << (nm.ch[c].target < nm.rl ? nm.rl - 9 : nm.rl - 8));
+        fuse = nm.nch > 0;
+        if (!fuse) launch_noise_map(n, batch, next->traj0, chans, next->seed, next->counter0, next->words, s, tm);
+    }
     a.src = src;
     a.dst = dst;
     a.words = words;
@@ -1205,12 +1265,31 @@ void launch_pull_gate(const double2* src, double2* dst, int n, uint64_t batch, c
     const bool nt = ne == nullptr || std::atoi(ne) != 0;
     const int Uc = U <= 2 ? 2 : (U >= 8 ? 8 : 4);
     const dim3 grid((unsigned)((a.items + 256 * Uc - 1) / (256 * Uc)));
-    TimedLaunch tl(tm, "pull_gate", 32.0 * (double)amps, s);
     const bool w32 = chans.size() <= 16;
+    if (fuse) {  // the fused form: 4 items per thread, non-temporal, 1 or 2 whole regions per group
+        const uint64_t regions = amps >> nm.rl;
+        nm.rpw = (int)(regions / grid.x);
+        if (Uc != 4 || !nt || (nm.rpw != 1 && nm.rpw != 2) || (uint64_t)nm.rpw * grid.x != regions) {
+            fuse = false;
+            launch_noise_map(n, batch, next->traj0, chans, next->seed, next->counter0, next->words, s, tm);
+        }
+    }
+    TimedLaunch tl(tm, fuse ? "pull_gate_map" : "pull_gate", 32.0 * (double)amps, s);
+    if (fuse) {
+        if (w32) {
+            if (pair) hipLaunchKernelGGL((k_pull_gate<uint32_t, true, 4, true, true>), grid, dim3(256), 0, s, a, nm);
+            else hipLaunchKernelGGL((k_pull_gate<uint32_t, false, 4, true, true>), grid, dim3(256), 0, s, a, nm);
+        } else {
+            if (pair) hipLaunchKernelGGL((k_pull_gate<unsigned long long, true, 4, true, true>), grid, dim3(256), 0, s, a, nm);
+            else hipLaunchKernelGGL((k_pull_gate<unsigned long long, false, 4, true, true>), grid, dim3(256), 0, s, a, nm);
+        }
+        QSIM_HIPCHK(hipGetLastError());
+        return;
+    }
 #define QSIM_PULL_LAUNCH(W_, UU, NTT)                                                                      \
     do {                                                                                                 \
-        if (pair) hipLaunchKernelGGL((k_pull_gate<W_, true, UU, NTT>), grid, dim3(256), 0, s, a);       \
-        else hipLaunchKernelGGL((k_pull_gate<W_, false, UU, NTT>), grid, dim3(256), 0, s, a);           \
+        if (pair) hipLaunchKernelGGL((k_pull_gate<W_, true, UU, NTT>), grid, dim3(256), 0, s, a, m);    \
+        else hipLaunchKernelGGL((k_pull_gate<W_, false, UU, NTT>), grid, dim3(256), 0, s, a, m);        \
     } while (0)
 #define QSIM_PULL_LAUNCH_U(W_, NTT)                  \
     do {                                           \

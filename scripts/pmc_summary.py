@@ -27,6 +27,8 @@ LABELS = [("k_fused_staged", "fused_tile"), ("k_fused_tile", "fused_tile"),
 
 
 def label_of(name):
+    if "k_pull_gate<" in name and name.split("(")[0].replace(" ", "").endswith(",true>"):
+        return "pull_gate_map"  # (the word map fused in: k_pull_gate<W, PAIR, U, NT, MAP = true>)
     for key, lab in LABELS:
         if key in name:
             return lab

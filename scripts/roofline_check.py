@@ -35,6 +35,7 @@ ENGINE_NAMES = {
     "noise": r".*k_noise_(units|flips).*",
     "gate_noise": r".*k_gate_noise_tile.*",
     "pull_gate": r".*k_pull_gate.*",
+    "pull_gate_map": r".*k_pull_gate<.*, *true>\(.*",
     "noise_map": r".*k_noise_words.*",
     "fused_tile": r"^(qk\d+|.*k_fused_(staged|tile).*)",
 }

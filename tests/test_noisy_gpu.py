@@ -147,15 +147,17 @@ def test_noise_free_run_is_fused_and_exact(qsim, oracle, gpu_ready):
         sim.applyNoiseToQubit(qsim.NoiseType.BitFlip, n, 0.5)
 
 
-@pytest.mark.parametrize("overlap", ["1", "0"])
+@pytest.mark.parametrize("mode", ["fused", "overlap", "serial"])
 @pytest.mark.parametrize("n,seed,types", [(10, 4, (0, 3, 4, 5)), (12, 5, (0, 0, 5, 3)), (11, 6, (0, 1, 3)),
-                                          (9, 7, (0,) * 20)])
-def test_pulled_flip_noise_matches_oracle(qsim, oracle, gpu_ready, monkeypatch, n, seed, types, overlap):
+                                          (9, 7, (0,) * 20), (13, 8, (0,) * 18)])
+def test_pulled_flip_noise_matches_oracle(qsim, oracle, gpu_ready, monkeypatch, n, seed, types, mode):
     """From 9 qubits, flip-only noise models run pulled (the noise after gate i applied by gate
     i+1's pass, out of place; noise.hip) — exactly the oracle's per-pair passes, with the next
-    step's code words built on a second stream or not, and with > 16 channel entries (64-bit
-    words, fourth case).  A damping channel in the model keeps the per-channel passes (third)."""
-    monkeypatch.setenv("QSIM_NOISE_MAP_OVERLAP", overlap)
+    step's code words built on a second stream (the default), before the pass, or by the pass
+    itself (fused, opt-in), and with > 16 channel entries (64-bit words, fourth and fifth cases).  A damping
+    channel in the model keeps the per-channel passes (third)."""
+    monkeypatch.setenv("QSIM_NOISE_MAP_FUSED", "1" if mode == "fused" else "0")
+    monkeypatch.setenv("QSIM_NOISE_MAP_OVERLAP", "1" if mode == "overlap" else "0")
     monkeypatch.setenv("QSIM_NOISY_TILE", "0")  # (the default; the in-tile path is opt-in)
     rng = np.random.default_rng(seed)
     c = qsim.createRandomCircuit(n, 16, seed)
