@@ -296,3 +296,30 @@ def _relabeled_runs(qsim, oracle, n, depth, seed):
     np.testing.assert_allclose(sim.getProbabilities(), np.real(np.diag(want1)), atol=1e-12, rtol=0)
     np.testing.assert_allclose(sim.getDensityMatrix(), want1, atol=1e-12, rtol=0)
     assert abs(sim.getPurity() - np.sum(np.abs(want1) ** 2)) < 1e-12
+
+
+@pytest.mark.gpu
+def test_relabeled_run_reference_y_and_pinned_pointer(qsim, oracle, gpu_ready):
+    """18 index bits: the relabeled first run with the reference's Y sign (its global -1 op moves
+    with the labels), and a rho whose device pointer was handed out before the run (never
+    relabeled: the pointer holds row-major rho right after the run, no reader in between)."""
+    import ctypes
+    n = 9
+    c = _circuit(qsim, n, 14, 31)
+    c.y(3)
+    channels = [(0, -1, 0.02), (4, 2, 0.1)]
+    want = oracle.dm_run(n, oracle.gates_of(c), channels, reference_y=True)
+    sim = qsim.DensityMatrixSimulator(n, _noise(qsim, channels))
+    sim.setReferenceCompatible()
+    sim.run(c)
+    np.testing.assert_allclose(sim.getDensityMatrix(), want, atol=1e-12, rtol=0)
+    want2 = oracle.dm_run(n, oracle.gates_of(c), channels)
+    sim2 = qsim.DensityMatrixSimulator(n, _noise(qsim, channels))
+    ptr = sim2.density.state.devicePtr()
+    sim2.run(c)
+    sim2.density.state.synchronize()
+    hip = ctypes.CDLL("libamdhip64.so.7")
+    hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    raw = np.empty(1 << (2 * n), dtype=np.complex128)
+    assert hip.hipMemcpy(raw.ctypes.data, ctypes.c_void_p(ptr), raw.nbytes, 2) == 0  # D2H
+    np.testing.assert_allclose(raw.reshape(1 << n, 1 << n), want2, atol=1e-12, rtol=0)
