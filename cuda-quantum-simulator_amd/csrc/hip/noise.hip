@@ -94,10 +94,13 @@ __device__ __forceinline__ bool next_flip(FlipCursor& cur, uint64_t b, uint64_t 
             double gap;
             const float gf = __log2f((float)u) * c.il2;
             const float fl = floorf(gf);
-            // error of gf: |il2| x (rounding of u, <= 2^-24 / ln 2, + the hardware log2's error)
-            // + |gf| x (its relative error and two roundings) — bounded here with a wide margin
-            // (2^-16 relative, 2^-13 x |il2| absolute; a few per cent of draws fall back at p = 0.01)
-            const float err = fabsf(gf) * 0x1.0p-16f + fabsf(c.il2) * 0x1.0p-13f;
+            // error of gf: |il2| x (rounding of u, <= 2^-24 / ln 2 absolute in log2 u, + the
+            // hardware log2's error, ~2^-22 absolute near 1) + |gf| x (its relative error and two
+            // roundings, ~2^-22) — bounded here by 2^-17 x |il2| + 2^-20 x |gf| (16x and 4x
+            // margins).  The margin is kept tight on purpose: a lane that falls back makes its whole
+            // wave run the double log, so at p = 0.01 a 1 % per-lane fallback rate (a 2^-13 x |il2|
+            // bound) left most iterations of a 64-lane wave on the slow path; this one is ~0.1 %.
+            const float err = fabsf(gf) * 0x1.0p-20f + fabsf(c.il2) * 0x1.0p-17f;
             if (c.il2 != 0.0f && gf - fl > err && fl + 1.0f - gf > err && gf < 4.0e6f) gap = (double)fl;
             else gap = floor(log(u) / c.lq);
             if (gap >= (double)kFlipBlock) {
@@ -923,6 +926,7 @@ constexpr int kMaxPullChannels = 32;
 constexpr int kWordThreads = 256;
 struct MapArgs {
     void* words;
+    int skip;            // QSIM_MAP_SKIP (measurement only, wrong states): 1 no walks, 2 no stores
     int rpw;             // (fused into the pull pass) regions per work-group
     uint64_t amps;       // batch << n (this object's)
     uint64_t idx0;       // global pair index of local pair 0
@@ -950,13 +954,16 @@ __device__ __forceinline__ void walk_block(uint64_t gb, const FlipChan& c, F&& f
 
 // Walk task `task` (channel c, j-th block of pairs with a member in the region starting at
 // amplitude K0 of 2^a.rl) and OR its flips' codes into the region's LDS words w.
+// (chs / toff: the channel table and the task offsets, staged in LDS by the caller — indexed per
+// lane, they would otherwise be vector loads from the kernel-argument segment in every task)
 template <class W>
-__device__ __forceinline__ void map_task(const MapArgs& a, W* w, uint64_t K0, int task) {
+__device__ __forceinline__ void map_task(const MapArgs& a, const FlipChan* chs, const int* toff, W* w, uint64_t K0,
+                                         int task) {
     const uint64_t traj = K0 >> a.n, r0 = K0 & ((1ull << a.n) - 1ull);
     int c = 0;
-    while (task >= a.task_off[c + 1]) ++c;
-    const int j = task - a.task_off[c];
-    const FlipChan& ch = a.ch[c];
+    while (task >= toff[c + 1]) ++c;
+    const int j = task - toff[c];
+    const FlipChan ch = chs[c];
     const int q = ch.target;
     const W sh = (W)(2 * c);
     uint64_t lbase;  // the first pair (this object's pair index) with a member in the region
@@ -982,15 +989,21 @@ __device__ __forceinline__ void map_task(const MapArgs& a, W* w, uint64_t K0, in
 template <class W>
 __global__ __launch_bounds__(kWordThreads) void k_noise_words(MapArgs a) {
     __shared__ W w[1 << kRegionLogMax];
+    __shared__ FlipChan chs[kMaxPullChannels];
+    __shared__ int toff[kMaxPullChannels + 1];
     const int t = threadIdx.x;
     const int R = 1 << a.rl;
     for (int i = t; i < R; i += kWordThreads) w[i] = 0;
+    if (t < a.nch) chs[t] = a.ch[t];
+    if (t <= a.nch) toff[t] = a.task_off[t];
     __syncthreads();
     const uint64_t K0 = (uint64_t)blockIdx.x << a.rl;  // the region's first amplitude (this object)
-    for (int task = t; task < a.task_off[a.nch]; task += kWordThreads) map_task(a, w, K0, task);
+    if (!(a.skip & 1))
+        for (int task = t; task < toff[a.nch]; task += kWordThreads) map_task(a, chs, toff, w, K0, task);
     __syncthreads();
     W* out = static_cast<W*>(a.words) + K0;
-    for (int i = t; i < R; i += kWordThreads) out[i] = w[i];
+    if (!(a.skip & 2))
+        for (int i = t; i < R; i += kWordThreads) out[i] = w[i];
 }
 
 struct PullArgs {
@@ -1061,10 +1074,14 @@ template <class W, bool PAIR, int kPullU, bool NT, bool MAP = false>
 __global__ __launch_bounds__(256) void k_pull_gate(PullArgs a, MapArgs m) {
     __shared__ int sq[kMaxPullChannels];
     __shared__ PullMapLds<W, MAP> lds;
+    __shared__ FlipChan mchs[MAP ? kMaxPullChannels : 1];
+    __shared__ int mtoff[MAP ? kMaxPullChannels + 1 : 1];
     if (threadIdx.x < kMaxPullChannels) sq[threadIdx.x] = a.q[threadIdx.x];
     if constexpr (MAP) {
         const int R = m.rpw << m.rl;
         for (int i = threadIdx.x; i < R; i += 256) lds.w[i] = 0;
+        if ((int)threadIdx.x < m.nch) mchs[threadIdx.x] = m.ch[threadIdx.x];
+        if ((int)threadIdx.x <= m.nch) mtoff[threadIdx.x] = m.task_off[threadIdx.x];
     }
     __syncthreads();
     // the next step's words for regions blockIdx.x * rpw .. + rpw - 1 (after this work-group's
@@ -1075,7 +1092,7 @@ __global__ __launch_bounds__(256) void k_pull_gate(PullArgs a, MapArgs m) {
             for (int t = threadIdx.x; t < tasks * m.rpw; t += 256) {
                 const int r = t / tasks;
                 const uint64_t K0 = ((uint64_t)blockIdx.x * (uint64_t)m.rpw + (uint64_t)r) << m.rl;
-                map_task(m, lds.w + (r << m.rl), K0, t - r * tasks);
+                map_task(m, mchs, mtoff, lds.w + (r << m.rl), K0, t - r * tasks);
             }
             __syncthreads();
             W* out = static_cast<W*>(m.words) + (((uint64_t)blockIdx.x * (uint64_t)m.rpw) << m.rl);
@@ -1202,6 +1219,8 @@ void launch_noise_map(int n, uint64_t batch, uint64_t traj0, const std::vector<N
     m.n = n;
     m.rl = std::min(n, kRegionLogMax);
     pull_channels(n, chans, seed, counter0, m, a);
+    const char* ske = std::getenv("QSIM_MAP_SKIP");
+    m.skip = ske ? std::atoi(ske) : 0;
     const size_t wb = chans.size() <= 16 ? sizeof(uint32_t) : sizeof(uint64_t);
     if (!m.nch) {  // no channel can fire: every word zero
         QSIM_HIPCHK(hipMemsetAsync(words, 0, amps * wb, s));
