@@ -72,6 +72,36 @@ struct FlipChan {
     int always;  // P == 1: every pair flips
     float il2;   // ln 2 / lq (the single-precision first try of next_flip; 0: always double)
 };
+// The geometric gap of draw h: floor(ln u / lq), u = ((h >> 11) + 1) 2^-53 in (0, 1] — in double,
+// exactly up to kFlipBlock (a larger value only says "past the block").  *fb (optional): set when
+// the single-precision first try could not decide it.
+__device__ __forceinline__ double flip_gap(uint64_t h, const FlipChan& c, bool* fb = nullptr) {
+    const double u = (double)((h >> 11) + 1ull) * 0x1.0p-53;  // (0, 1]
+    // gap = floor(ln u / lq) in double.  First in single precision (the hardware log2):
+    // its error bound is tiny next to the distance from the nearest integer except in ~0.1 %
+    // of draws (p = 0.01), which take the double path — so the result is always the double
+    // one (the flips, hence the states, do not change; qsim_noise_gap_check counts both).
+    double gap;
+    const float gf = __log2f((float)u) * c.il2;  // (>= 0: log2 u <= 0, il2 < 0)
+    // error of gf: |il2| x (rounding of u, <= 2^-24 / ln 2 absolute in log2 u, + the
+    // hardware log2's error, ~2^-22 absolute near 1) + |gf| x (its relative error and two
+    // roundings, ~2^-22) — bounded here by 2^-17 x |il2| + 2^-20 x |gf| (16x and 4x
+    // margins).  The margin is kept tight on purpose: a lane that falls back makes its whole
+    // wave run the double log, so at p = 0.01 a 1 % per-lane fallback rate (a 2^-13 x |il2|
+    // bound) left most iterations of a 64-lane wave on the slow path; this one is ~0.1 %.
+    const float err = fabsf(gf) * 0x1.0p-20f + fabsf(c.il2) * 0x1.0p-17f;
+    // decided when both ends of [gf - err, gf + err] have the same floor, or both lie past the
+    // block (a walk only needs to know the gap ends it: at p <= 0.001 most draws)
+    const float flo = fminf(floorf(gf - err), (float)kFlipBlock), fhi = fminf(floorf(gf + err), (float)kFlipBlock);
+    if (c.il2 != 0.0f && flo == fhi) {
+        gap = (double)fhi;
+    } else {
+        gap = floor(log(u) / c.lq);
+        if (fb) *fb = true;
+    }
+    return gap;
+}
+
 // Next flip of a block's walk inside [lo, hi): false when the block is exhausted.
 struct FlipCursor {
     uint64_t stream, k;
@@ -86,23 +116,7 @@ __device__ __forceinline__ bool next_flip(FlipCursor& cur, uint64_t b, uint64_t 
         if (c.always) {
             cur.pos += 1;
         } else {
-            const double u = (double)((h >> 11) + 1ull) * 0x1.0p-53;  // (0, 1]
-            // gap = floor(ln u / lq) in double.  First in single precision (the hardware log2):
-            // its error bound is tiny next to the distance from the nearest integer except in a
-            // fraction ~1e-4 of draws, which take the double path — so the result is always
-            // the double one (the flips, hence the states, do not change).
-            double gap;
-            const float gf = __log2f((float)u) * c.il2;
-            const float fl = floorf(gf);
-            // error of gf: |il2| x (rounding of u, <= 2^-24 / ln 2 absolute in log2 u, + the
-            // hardware log2's error, ~2^-22 absolute near 1) + |gf| x (its relative error and two
-            // roundings, ~2^-22) — bounded here by 2^-17 x |il2| + 2^-20 x |gf| (16x and 4x
-            // margins).  The margin is kept tight on purpose: a lane that falls back makes its whole
-            // wave run the double log, so at p = 0.01 a 1 % per-lane fallback rate (a 2^-13 x |il2|
-            // bound) left most iterations of a 64-lane wave on the slow path; this one is ~0.1 %.
-            const float err = fabsf(gf) * 0x1.0p-20f + fabsf(c.il2) * 0x1.0p-17f;
-            if (c.il2 != 0.0f && gf - fl > err && fl + 1.0f - gf > err && gf < 4.0e6f) gap = (double)fl;
-            else gap = floor(log(u) / c.lq);
+            const double gap = flip_gap(h, c);
             if (gap >= (double)kFlipBlock) {
                 cur.done = true;
                 break;
@@ -1336,6 +1350,52 @@ void launch_pull_noise_step(const double2* src, double2* dst, int n, uint64_t ba
 }
 
 }  // namespace qsim_hip
+
+namespace qsim_hip {
+// draws single-precision-first gaps (flip_gap) against the double formula: out[0] mismatches,
+// out[1] draws that fell back to the double log
+__global__ __launch_bounds__(256) void k_gap_check(FlipChan c, uint64_t key, uint64_t draws,
+                                                   unsigned long long* out) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    unsigned long long mm = 0, fb = 0;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < draws; i += stride) {
+        const uint64_t h = nz_mix(key + i * 0x9e3779b97f4a7c15ull);
+        bool f = false;
+        const double g = flip_gap(h, c, &f);
+        const double u = (double)((h >> 11) + 1ull) * 0x1.0p-53;
+        const double ref = floor(log(u) / c.lq), blk = (double)kFlipBlock;
+        if (!((g < blk ? g : blk) == (ref < blk ? ref : blk))) ++mm;
+        fb += f ? 1ull : 0ull;
+    }
+    if (mm) atomicAdd(&out[0], mm);
+    if (fb) atomicAdd(&out[1], fb);
+}
+}  // namespace qsim_hip
+
+extern "C" int qsim_noise_gap_check(double p, uint64_t draws, uint64_t key, uint64_t* mismatches,
+                                    uint64_t* fallbacks) {
+    using namespace qsim_hip;
+    if (!mismatches || !fallbacks || !(p > 0.0) || p > 1.0) return QSIM_ERR_INVALID_ARGUMENT;
+    FlipChan c{};
+    if (!flip_channel(0, 0, p, key, c) || c.always) {  // (nothing to draw: no gaps)
+        *mismatches = *fallbacks = 0;
+        return QSIM_OK;
+    }
+    unsigned long long* d = nullptr;
+    if (hipMalloc(&d, 2 * sizeof(unsigned long long)) != hipSuccess) return QSIM_ERR_DEVICE;
+    unsigned long long hcnt[2] = {0, 0};
+    bool ok = hipMemset(d, 0, sizeof(hcnt)) == hipSuccess;
+    if (ok) {
+        hipLaunchKernelGGL(k_gap_check, dim3(1024), dim3(256), 0, 0, c, key, draws, d);
+        ok = hipGetLastError() == hipSuccess && hipDeviceSynchronize() == hipSuccess &&
+             hipMemcpy(hcnt, d, sizeof(hcnt), hipMemcpyDeviceToHost) == hipSuccess;
+    }
+    (void)hipFree(d);
+    if (!ok) return QSIM_ERR_DEVICE;
+    *mismatches = hcnt[0];
+    *fallbacks = hcnt[1];
+    return QSIM_OK;
+}
 
 extern "C" int qsim_noise_check_flips(uint64_t* flips) {
     if (!flips) return QSIM_ERR_INVALID_ARGUMENT;

@@ -329,6 +329,11 @@ int qsim_noise_apply(qsim_state* s, int type, int qubit, double probability, uin
  * reference noise kernel counts every access outside its work-group's pairs on the device and
  * fails the call if there is one; tests read this to see the check had work to do). */
 int qsim_noise_check_flips(uint64_t* flips);
+/* Tests: `draws` geometric gaps of a flip channel of probability p (keyed by `key`) taken the
+ * engine's way (single precision first, the double log where that cannot decide) against
+ * floor(ln u / ln(1 - P)) in double, both capped at one 256-pair block (a walk only needs to know
+ * a gap is past its block): *mismatches (0 expected) and *fallbacks. */
+int qsim_noise_gap_check(double p, uint64_t draws, uint64_t key, uint64_t* mismatches, uint64_t* fallbacks);
 /* NoisySimulator::run (src/NoiseModel.cu:369-382): each gate, then every channel entry in order,
  * one noise pass each; *counter advances by one per pass.  With no channel entries the circuit
  * runs as fused passes (flags = QSIM_RUN_*), else one kernel per gate (the noise interleaves). */

@@ -399,3 +399,18 @@ def test_single_precision_gap_draws_equal_double(qsim, gpu_ready, monkeypatch, p
         got.append(sim.getStateVector())
         del sim
     assert np.array_equal(got[0], got[1])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("p", [0.01, 0.001, 1e-5, 0.05, 0.3, 0.75, 0.99])
+def test_single_precision_gaps_never_differ(qsim, gpu_ready, p):
+    """noise.hip flip_gap over 2^26 draws per probability: the single-precision-first gap equals
+    floor(ln u / ln(1 - P)) in double every time (its error bound holds), and the double fallback
+    stays rare (< 1 % of draws)."""
+    import ctypes
+    from qsim_amd import _lib
+    mm, fb = ctypes.c_uint64(), ctypes.c_uint64()
+    draws = 1 << 26
+    _lib.check(_lib.hip.qsim_noise_gap_check(p, draws, 0x5eed + int(p * 1e6), ctypes.byref(mm), ctypes.byref(fb)))
+    assert mm.value == 0
+    assert fb.value < draws // 100
