@@ -332,10 +332,12 @@ uint64_t noise_check_flips = 0;  // flips applied by range-checked launches (qsi
 void launch_noise_after_gate(double2* st, int n, const std::vector<NoiseChan>& chans, uint64_t seed,
                              uint64_t& counter, hipStream_t s, Timer* tm, uint64_t batch, uint64_t traj0) {
     const int log_ppt = n - 1;
-    // whole trajectories, >= 256 blocks of 256 pairs (QSIM_NOISE_UNIT_LOG: experiments, >= n - 1)
+    // whole trajectories, >= 128 blocks of 256 pairs (QSIM_NOISE_UNIT_LOG: experiments, >= n - 1;
+    // W-BATCH config 4: one trajectory per work-group, 2^15 pairs, suffix push 0.140 -> 0.137 ms
+    // against two, profiles/r05/batch_unit/)
     static const int unit_log_env = [] {
         const char* e = std::getenv("QSIM_NOISE_UNIT_LOG");
-        return e ? std::atoi(e) : 16;
+        return e ? std::atoi(e) : 15;
     }();
     const int log_unit = std::max(log_ppt, unit_log_env);
     const uint64_t pairs = batch << log_ppt, idx0 = traj0 << log_ppt;
