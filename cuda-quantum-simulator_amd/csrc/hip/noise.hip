@@ -538,6 +538,40 @@ __device__ __forceinline__ void gn_walk(const GnArgs& a, int c, int jb, uint64_t
 // and writes the first cap flips in walk order, then the count (> cap: the tile kernel ignores the
 // list and walks the channel itself).  (One thread per block with atomic slot reservation measured
 // slower: 67.3 vs 58.2 ms per W-BATCH step.)
+// The same lists with one lane per (tile, channel, block): the 8 lanes of a (tile, channel) count
+// their blocks' flips, place them by a prefix sum over those lanes, and walk again to write —
+// twice the draws, but chains of one block instead of eight (the walks are latency-bound), and
+// the entries land in the same order as the one-lane form's, so the lists are identical.
+__global__ __launch_bounds__(256) void k_gn_lists8(GnArgs a, uint16_t* list, uint32_t* cnt, uint64_t tiles) {
+    const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t grp = tid >> 3;  // (tile, channel); 8 lanes each, aligned within a wave
+    const int jb = (int)(tid & 7);
+    const bool live = grp < tiles * (uint64_t)a.np;
+    const uint64_t b = live ? grp / (uint64_t)a.np : 0;
+    const int c = live ? (int)(grp - b * (uint64_t)a.np) : 0;
+    uint64_t traj = 0, loc = 0;
+    const uint64_t gbase = gn_tile_base(b, a.n, a.u, &traj, &loc);
+    uint32_t k = 0;
+    if (live) gn_walk(a, c, jb, traj, gbase, [&](int, uint32_t) { ++k; });
+    // exclusive prefix of k over the 8 lanes of the group (every lane takes part: shuffles)
+    uint32_t incl = k;
+#pragma unroll
+    for (int d = 1; d < 8; d <<= 1) {
+        const uint32_t o = __shfl_up(incl, d, 8);
+        if (jb >= d) incl += o;
+    }
+    const uint32_t total = __shfl(incl, 7, 8);
+    if (!live) return;
+    uint32_t pos = incl - k;
+    uint16_t* out = list + (b * kGnMaxPrefix + (uint64_t)c) * (uint64_t)a.cap;
+    if (pos < (uint32_t)a.cap)
+        gn_walk(a, c, jb, traj, gbase, [&](int x, uint32_t code) {
+            if (pos < (uint32_t)a.cap) out[pos] = (uint16_t)((x << 2) | (int)code);
+            ++pos;
+        });
+    if (jb == 0) cnt[b * kGnMaxPrefix + (uint64_t)c] = total;
+}
+
 __global__ __launch_bounds__(256) void k_gn_lists(GnArgs a, uint16_t* list, uint32_t* cnt, uint64_t tiles) {
     const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (tid >= tiles * (uint64_t)a.np) return;
@@ -865,10 +899,18 @@ void launch_gate_noise_run(double2* st, int n, uint64_t batch, uint64_t traj0, c
         uint32_t* cnt = nullptr;
         set_of(i, &list, &cnt);
         if (b.np) {
-            const uint64_t threads = tiles * (uint64_t)b.np;
+            // QSIM_NOISE_LISTS8 (default 1): one lane per (tile, channel, block), k_gn_lists8;
+            // 0: one lane per (tile, channel)
+            const char* l8e = std::getenv("QSIM_NOISE_LISTS8");
+            const bool l8 = l8e == nullptr || std::atoi(l8e) != 0;
+            const uint64_t threads = tiles * (uint64_t)b.np * (l8 ? 8u : 1u);
             TimedLaunch tl(tm, "noise_lists", 0.0, L->ms);
-            hipLaunchKernelGGL(k_gn_lists, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, L->ms, b, list, cnt,
-                               tiles);
+            if (l8)
+                hipLaunchKernelGGL(k_gn_lists8, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, L->ms, b, list,
+                                   cnt, tiles);
+            else
+                hipLaunchKernelGGL(k_gn_lists, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, L->ms, b, list,
+                                   cnt, tiles);
             QSIM_HIPCHK(hipGetLastError());
         }
         QSIM_HIPCHK(hipEventRecord(L->built[i & 1], L->ms));
