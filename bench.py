@@ -114,7 +114,7 @@ def parse():
     p.add_argument("--pmc-json", default=None,
                    help="per-launch HBM traffic measured by rocprofv3 --pmc (see profiles/)")
     p.add_argument("--profile-region", default="none",
-                   choices=["none", "hc", "1q28", "batch16ref", "noisy26", "dm14"],
+                   choices=["none", "hc", "hc28", "1q28", "batch16ref", "noisy26", "dm14"],
                    help="bracket that timed region (only) with roctxProfilerResume / Pause, for "
                         "rocprofv3 --selected-regions: the profile then holds exactly the launches "
                         "the line's roofline averages (scripts/roofline_check.py recomputes it)")
@@ -203,6 +203,125 @@ def cpu_baseline(circuit, n, budget, q=None, args=None):
                       f"({', '.join(str(d) for d, _ in runs_n)} gates in "
                       f"{', '.join(f'{s:.1f}' for _, s in runs_n)} s), single thread ({cpu_model}; host "
                       f"has {os.cpu_count()} logical CPUs); value = median of prefix gates / prefix time"}
+
+
+def batch_cpu_baseline(args, trajectories=4):
+    """W-BATCH CPU baseline (kind "port"): the oracle's restatement of the reference batched noise
+    process (oracle/numpy_oracle.py batched_reference_run: per gate the C++ CPUSimulator
+    restatement on every trajectory, then one per-pair depolarizing pass per channel entry,
+    src/NoiseModel.cu:815-892) on `trajectories` trajectories of the same circuit and noise, gate by
+    gate until --cpu-budget seconds; value = trajectories x gates done / seconds."""
+    if args.cpu_budget <= 0:
+        return None
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import numpy_oracle as orc  # test infrastructure: the CPU baseline leg only
+    from qsim_amd import circuit as qc
+    n = args.qubits
+    gates = orc.gates_of(qc.createRandomHCCircuit(n, args.depth, args.seed))
+    chans = [(0, qq, args.noise) for qq in range(n)]
+    st, counter, done = None, 0, 0
+    t0 = time.perf_counter()
+    while done < len(gates) and time.perf_counter() - t0 < args.cpu_budget:
+        st, counter = orc.batched_reference_run(n, trajectories, [gates[done]], chans, args.seed,
+                                                states=st, counter=counter)
+        done += 1
+    secs = time.perf_counter() - t0
+    return {"value": round(trajectories * done / secs, 2), "unit": "trajectory-gates/s", "cores": 1,
+            "kind": "port",
+            "sample": f"{trajectories} trajectories x the first {done} of {len(gates)} gates at {n} qubits "
+                      f"with depolarizing {args.noise} on all qubits after every gate, {secs:.1f} s, single "
+                      f"thread (numpy + the C++ oracle; same process and draws as the engine's reference "
+                      f"noise path)"}
+
+
+H_SINGLE_REF_MS = {20: 0.035, 24: 2.7, 26: 9.9}  # README.md:373-377 (benchmark_custatevec.cu)
+
+
+def h_single_synced(q, sizes=(12, 16, 18, 20, 22, 24, 26), warmup=3, iterations=10):
+    """The reference's Hadamard scaling benchmark (benchmarks/benchmark_custatevec.cu:60-78 timing
+    helper, :233-290 loop): one H on target 0 of an n-qubit |0..0> state, `warmup` synchronised
+    launches, then `iterations` launches back to back between two device synchronisations, the
+    mean per launch; here through the per-gate kernel entry (StateVector.applyGate, the
+    applyH<<<>>> analogue), beside the published times (README.md:373-377, RTX 4070 laptop)."""
+    rows = []
+    for n in sizes:
+        sv = q.StateVector(n)
+        op = q.GateOp(q.GateType.H, [0])
+        for _ in range(warmup):
+            sv.applyGate(op)
+            sv.synchronize()
+        sv.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(iterations):
+            sv.applyGate(op)
+        sv.synchronize()
+        ms = (time.perf_counter() - t0) / iterations * 1e3
+        sv.close()
+        rows.append({"qubits": n, "ms": round(ms, 4), "GBps": round(32.0 * (1 << n) / (ms / 1e3) / 1e9, 1),
+                     "reference_readme_ms": H_SINGLE_REF_MS.get(n),
+                     "speedup_vs_reference": round(H_SINGLE_REF_MS[n] / ms, 1) if n in H_SINGLE_REF_MS else None})
+    return {"workload": "one H on target 0, mean of 10 back-to-back launches between synchronisations "
+                        "(benchmark_custatevec.cu benchmarkScaling)", "rows": rows}
+
+
+def w_hc_28q(q, args, steps=10):
+    """BASELINE config 3 in the default line: createRandomHCCircuit(28, depth, seed) in the line's
+    mode (calibrated first run, specialised pass kernels), gates / median synchronised step, and
+    the pass kernels' roofline from per-launch HIP events on every timed step (the launches a
+    --profile-region hc28 rocprof profile records), PMC traffic from profiles/pmc_hc_28q.json."""
+    from qsim_amd.plan import set_jit
+    set_jit(args.jit, -1)
+    n = 28
+    c = q.createRandomHCCircuit(n, args.depth, args.seed)
+    sim = q.Simulator(n)
+    tf = time.perf_counter()
+    sim.run(c)
+    sim.synchronize()
+    first = time.perf_counter() - tf
+    sim.run(c)
+    sim.synchronize()
+    sim.state.profileReset()
+    sim.state.profile(True)
+    ts_ = []
+    with region("hc28"):
+        for _ in range(steps):
+            t0 = time.perf_counter()
+            sim.run(c)
+            sim.synchronize()
+            ts_.append(time.perf_counter() - t0)
+    stats = sim.state.profileStats()
+    sim.state.profile(False)
+    info = sim.state.layoutInfo()
+    passes = sim.state.lastRunInfo()[0]
+    del sim
+    med = _median(ts_)
+    # the pass kernels together (every launch moves 32 B x 2^28 whatever its name)
+    pk = [s_ for s_ in stats if s_["alg_bytes"] > 0 and s_["launches"]]
+    launches = sum(s_["launches"] for s_ in pk)
+    ms = sum(s_["ms"] for s_ in pk)
+    by = sum(s_["alg_bytes"] for s_ in pk)
+    roof = None
+    if launches:
+        ach = by / (ms / 1e3) / 1e9
+        traffic, tsrc = None, None
+        pmc_path = os.path.join(ROOT, "profiles", "pmc_hc_28q.json")
+        if os.path.exists(pmc_path):
+            with open(pmc_path) as f:
+                kern = json.load(f).get("kernels", {})
+            ents = [kern[s_["name"]] for s_ in pk if s_["name"] in kern]
+            tl = sum(e["launches"] for e in ents)
+            if ents and tl:
+                traffic = sum(e["hbm_bytes_per_launch"] * e["launches"] for e in ents) / tl
+                tsrc = os.path.relpath(pmc_path, ROOT)
+        roof = {"bound": "hbm", "kernels": sorted(s_["name"] for s_ in pk), "achieved": round(ach, 1),
+                "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBPS, 4),
+                "traffic": traffic, "traffic_source": tsrc, "alg_bytes_per_launch": by / launches,
+                "avg_launch_ms": round(ms / launches, 4), "launches": launches}
+    return {"workload": f"W-HC createRandomHCCircuit(28, {args.depth}, {args.seed}) (BASELINE config 3)",
+            "value": round(c.getGateCount() / med, 1), "unit": "gates/s", "ms_per_step": round(med * 1e3, 3),
+            "steps": steps, "passes": passes, "tile_qubits": info["tile_qubits"], "relayout": info["relayout"],
+            "calibrated": info["calibrated"], "first_run_ms": round(first * 1e3, 1), "roofline": roof,
+            "kernels": stats}
 
 
 def run_single(args):
@@ -311,6 +430,8 @@ def run_single(args):
         out["seeds"] = hc_seeds(q, args)
         out["default_mode"] = default_mode(q, args, circuit)
         out["w_ref"] = w_ref(q, args)
+        out["w_hc_28q"] = w_hc_28q(q, args)
+        out["h_single_synced"] = h_single_synced(q)
         out["gate_table_20q"] = gate_table_20q(q)
         out["dm_14q"] = measure_dm(q, 14, 3, 1, args.jit, args.seed, args.depth, 0.01)
         out["noisy_26q"] = measure_noisy(q, 26, 3, 1, args.seed, args.depth, 0.01)
@@ -723,7 +844,10 @@ def measure_batch(q, n, B, steps, warmup, jit, seed, depth, p_noise, process, pm
                 "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBPS, 4), "traffic": traffic,
                 "traffic_source": traffic_src,
                 "alg_bytes_per_launch": per, "avg_launch_ms": round(avg_s * 1e3, 4),
-                "launches": dom["launches"]}
+                "launches": dom["launches"],
+                "source": ("as many steps more with one part on one stream after the timed ones "
+                           "(QSIM_NOISE_SPLIT=1, same states): each kernel's own duration; the timed "
+                           "steps run two parts on two streams") if split else "the timed steps"}
     del sim
     return {"value": round(gates * B * steps / wall, 1), "ms_per_step": round(wall / steps * 1e3, 3),
             "gates": gates, "tile_passes": passes, "jit_passes": jit_passes, "roofline": roof,
@@ -775,7 +899,7 @@ def run_batch(args):
                    "noise_process": m["noise_process"],
                    "qubits": n, "trajectories": B, "gates": m["gates"], "state_bytes": (16 << n) * B,
                    "tile_passes": m["tile_passes"], "jit_passes": m["jit_passes"]},
-        "roofline": m["roofline"], "kernels": m["kernels"], "cpu_baseline": None,
+        "roofline": m["roofline"], "kernels": m["kernels"], "cpu_baseline": batch_cpu_baseline(args),
         **{k: m[k] for k in ("kernels_note", "kernels_overlapped") if k in m},
     }
     print(json.dumps(out))
@@ -823,7 +947,7 @@ def main():
         if world > 1 or args.dry_run:
             from qsim_amd import dist_bench  # trajectory-sharded replicas
             dist_bench.run_batch(args, "trajectory-gates/s, W-HC circuit on noisy trajectories "
-                                       "(BatchedSimulator)", HBM_PEAK_GBPS)
+                                       "(BatchedSimulator)", HBM_PEAK_GBPS, batch_cpu_baseline)
         else:
             run_batch(args)
         return

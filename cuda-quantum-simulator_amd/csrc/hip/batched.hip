@@ -391,8 +391,11 @@ bool ensure_list_buffers(qsim_batch* b, size_t bytes) {
 }
 // The in-tile run over k trajectory parts on k streams (QSIM_NOISE_SPLIT, default 2): part 0 on the object's
 // stream with its list sets, part j > 0 on a stream of its own with its own side stream and lists;
-// every part draws with the global pair index, so the states are the one-part run's.
-void split_tile_run(qsim_batch* b, const std::vector<Op>& ops, const std::vector<NoiseChan>& dep, int k,
+// every part draws with the global pair index, so the states are the one-part run's.  false (nothing
+// launched): a part's list buffers do not fit beside the margin ensure_list_buffers keeps — the
+// caller runs the ensemble as one part instead (a near-full device must not turn a run
+// that fits as one part into an error).
+bool split_tile_run(qsim_batch* b, const std::vector<Op>& ops, const std::vector<NoiseChan>& dep, int k,
                     const GnLists& L0) {
     const uint64_t B = (uint64_t)b->batch;
     if ((int)b->split.size() < k - 1) b->split.resize(k - 1);
@@ -402,6 +405,30 @@ void split_tile_run(qsim_batch* b, const std::vector<Op>& ops, const std::vector
     std::vector<uint64_t> first(k + 1);
     for (int j = 0; j <= k; ++j) first[j] = B * (uint64_t)j / (uint64_t)k;
     Ls[0] = L0;
+    for (int j = 1; j < k; ++j) {  // every part's list buffers first, so a refusal launches nothing
+        qsim_batch::SplitPart& p = b->split[j - 1];
+        const size_t lb = gate_noise_lists_bytes(b->n, first[j + 1] - first[j], dep);
+        if (lb <= p.cap) continue;
+        if (p.lists) {
+            QSIM_HIPCHK(hipStreamSynchronize(p.s));
+            QSIM_HIPCHK(hipStreamSynchronize(p.ms));
+            (void)hipFree(p.lists);
+            p.lists = nullptr;
+            p.cap = 0;
+        }
+        size_t free_b = 0, total_b = 0;
+        if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) {
+            (void)hipGetLastError();
+            return false;
+        }
+        if (free_b < 2 * lb + (256ull << 20)) return false;
+        if (hipMalloc((void**)&p.lists, 2 * lb) != hipSuccess) {
+            (void)hipGetLastError();
+            p.lists = nullptr;
+            return false;
+        }
+        p.cap = lb;
+    }
     for (int j = 1; j < k; ++j) {
         qsim_batch::SplitPart& p = b->split[j - 1];
         if (!p.s) {
@@ -409,18 +436,6 @@ void split_tile_run(qsim_batch* b, const std::vector<Op>& ops, const std::vector
             QSIM_HIPCHK(hipStreamCreateWithFlags(&p.ms, hipStreamNonBlocking));
             for (hipEvent_t* e : {&p.built[0], &p.built[1], &p.used[0], &p.used[1], &p.start, &p.fork, &p.join})
                 QSIM_HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
-        }
-        const size_t lb = gate_noise_lists_bytes(b->n, first[j + 1] - first[j], dep);
-        if (lb > p.cap) {
-            if (p.lists) {
-                QSIM_HIPCHK(hipStreamSynchronize(p.s));
-                QSIM_HIPCHK(hipStreamSynchronize(p.ms));
-                (void)hipFree(p.lists);
-                p.lists = nullptr;
-                p.cap = 0;
-            }
-            QSIM_HIPCHK(hipMalloc((void**)&p.lists, 2 * lb));
-            p.cap = lb;
         }
         GnLists& L = Ls[j];
         L.buf[0] = p.lists;
@@ -447,6 +462,7 @@ void split_tile_run(qsim_batch* b, const std::vector<Op>& ops, const std::vector
         QSIM_HIPCHK(hipStreamWaitEvent(b->stream, b->split[j - 1].join, 0));
     }
     b->ncounter = c_end;
+    return true;
 }
 // Buffers of the pulled noise path (second ensemble buffer, flip codes, touched bits), allocated
 // when the device has room for them beside a margin; false: run the push kernels instead.
@@ -746,10 +762,7 @@ int qsim_batch_run(qsim_batch* b, const qsim_gate* gates, size_t count,
                 // 57.8 -> 54.1 ms per step (3 parts 62.5, 4 parts 58.6)
                 const char* se = std::getenv("QSIM_NOISE_SPLIT");
                 const int k = se ? std::max(1, std::min(4, std::atoi(se))) : 2;
-                if (k > 1 && b->batch >= k && lists) {
-                    split_tile_run(b, ops, dep, k, L);
-                    return;
-                }
+                if (k > 1 && b->batch >= k && lists && split_tile_run(b, ops, dep, k, L)) return;
                 launch_gate_noise_run(b->d, b->n, (uint64_t)b->batch, b->traj0, ops, dep, b->seed, b->ncounter,
                                       b->stream, &b->timer, lists ? &L : nullptr);
                 return;

@@ -303,6 +303,19 @@ static void ensure_noise_stream(qsim_state* s) {
 // Buffers of the pulled noise path: the second state buffer, two sets of per-step code words.
 static bool ensure_noise_buffers(qsim_state* s, size_t nch) {
     const size_t codes_b = pull_noise_codes_bytes(s->n, 1, nch);
+    // Allocate only when the device keeps room for another state of this size beside the new
+    // buffers — the rule trim_noise_buffers keeps them by — so a device with between one and two
+    // states of room runs the push kernels instead of allocating and freeing a second state on
+    // every run.
+    const size_t need = (s->alt ? 0 : (sizeof(double2) << s->n)) + (codes_b > s->noise_codes_cap ? 2 * codes_b : 0);
+    if (need) {
+        size_t free_b = 0, total_b = 0;
+        if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) {
+            (void)hipGetLastError();
+            return false;
+        }
+        if (free_b < need + (sizeof(double2) << s->n) + kAltMarginBytes) return false;
+    }
     if (!ensure_alt(s)) return false;
     auto grab = [&](unsigned char** p, size_t bytes) {
         if (hipMalloc((void**)p, bytes) != hipSuccess) {
@@ -794,12 +807,26 @@ static Op permute_op(Op o, const std::vector<int>& pi) {
 // QSIM_DM_RELABEL_TRIES labelings (default 48, about 1 s of host planning at 14 qubits; 256 when
 // the candidates are timed on the device — more fewest-pass candidates to time: 14q 9.19k ->
 // 9.52k gates/s); 0 turns it off.
-static int dm_relabel_tries(bool timed = false) {
+// Below 24 index bits (rho of <= 11 qubits: ~1 ms passes) a quarter of that (the search
+// is paid on the first run of every new circuit structure).
+static int dm_relabel_tries(int nbits, bool timed = false) {
     static const int v = [] {
         const char* e = std::getenv("QSIM_DM_RELABEL_TRIES");
         return e ? std::max(0, std::atoi(e)) : -1;
     }();
-    return v >= 0 ? v : timed ? 256 : 48;
+    if (v >= 0) return v;
+    const int full = timed ? 256 : 48;
+    return nbits >= 24 ? full : full / 4;
+}
+// The DM relabeling follows the state-vector relabel policy (qsim_set_relabel / QSIM_RELABEL: mode
+// 0 turns it off) with its own size floor in index bits (QSIM_DM_RELABEL_MIN_BITS, default 16:
+// rho of 8 qubits).
+static bool dm_relabel_enabled(int nbits) {
+    static const int min_bits = [] {
+        const char* e = std::getenv("QSIM_DM_RELABEL_MIN_BITS");
+        return e ? std::max(2, std::atoi(e)) : 16;
+    }();
+    return relabel_mode_on() && nbits >= min_bits && dm_relabel_tries(nbits) > 0;
 }
 static LayoutChoice dm_choose_layout(int nbits, const std::vector<Op>& ops, size_t want_alts = 0) {
     auto lower = [&](const std::vector<int>& pi) {
@@ -808,7 +835,7 @@ static LayoutChoice dm_choose_layout(int nbits, const std::vector<Op>& ops, size
         for (const Op& o : ops) out.push_back(permute_op(o, pi));
         return out;
     };
-    return choose_layout(nbits, lower, dm_relabel_tries(want_alts > 0), want_alts);
+    return choose_layout(nbits, lower, dm_relabel_tries(nbits, want_alts > 0), want_alts);
 }
 
 static qsim_gate map_gate(const qsim_state* s, const qsim_gate& g) {
@@ -1678,15 +1705,26 @@ int qsim_dm_run(qsim_state* s, int n, const qsim_gate* gates, size_t count,
         // through them; readers restore the identity first (prep).  A pinned state (handed-out
         // device pointer) is never relabeled.
         const bool fresh = (flags & QSIM_RUN_FUSED) && !s->pinned && s->basis && s->basis_idx == 0 &&
-                           s->perm.empty() && count > 0 && s->n >= 16 && dm_relabel_tries() > 0;
+                           s->perm.empty() && count > 0 && dm_relabel_enabled(s->n);
         if (fresh) {
-            std::vector<unsigned char> key(count * sizeof(qsim_gate) + n_channels * sizeof(qsim_noise_channel) +
-                                           sizeof(int));
-            std::memcpy(key.data(), gates, count * sizeof(qsim_gate));
-            if (n_channels) std::memcpy(key.data() + count * sizeof(qsim_gate), channels, n_channels * sizeof(qsim_noise_channel));
-            std::memcpy(key.data() + key.size() - sizeof(int), &flags, sizeof(int));
+            // memo key: the circuit's STRUCTURE (gate types and qubits, channel types and qubits,
+            // flags) — not rotation angles or probabilities, so a parameter sweep (reset + run with
+            // new angles) reuses the labels instead of searching again; any labels are exact, the
+            // structure is what they were chosen for
+            std::vector<int32_t> key;
+            key.reserve(4 * count + 2 * n_channels + 2);
+            for (size_t i = 0; i < count; ++i) {
+                key.push_back(gates[i].type);
+                for (int j = 0; j < 3; ++j) key.push_back(j < gates[i].nqubits ? gates[i].qubits[j] : -1);
+            }
+            for (size_t i = 0; i < n_channels; ++i) {
+                key.push_back(channels[i].type);
+                key.push_back(channels[i].qubit);
+            }
+            key.push_back((int32_t)count);
+            key.push_back(flags);
             std::vector<int> memo;
-            if (layout_memo_get(s->n, 3, key.data(), key.size(), memo, nullptr)) {
+            if (layout_memo_get(s->n, 3, key.data(), key.size() * sizeof(int32_t), memo, nullptr)) {
                 s->perm = memo;
             } else {
                 // with layout calibration (inline compilation, >= 26 index bits by default) the
@@ -1710,7 +1748,7 @@ int qsim_dm_run(qsim_state* s, int n, const qsim_gate* gates, size_t count,
                     s->plans.put(lc.ops, s->n, std::move(lc.plan), s->stream);
                     s->perm = lc.perm;
                 }
-                layout_memo_put(s->n, 3, key.data(), key.size(), s->perm, -1);
+                layout_memo_put(s->n, 3, key.data(), key.size() * sizeof(int32_t), s->perm, -1);
             }
         } else if (s->pinned || s->relayout) {
             prep(s, true);  // (identity labels; a relayout-plan layout is the state vector's own)

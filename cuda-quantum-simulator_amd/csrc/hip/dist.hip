@@ -1895,6 +1895,22 @@ int qsim_dist_sync(qsim_dist* d) {
     });
 }
 
+// Every rank's engine idle, then a one-double all-reduce on the communicator: the ranks leave it
+// within the collective's latency of one another (the timing barrier of bench.py's N > 1 steps —
+// a host-file barrier releases its pollers milliseconds apart).
+int qsim_dist_barrier(qsim_dist* d) {
+    return dguard_comm(d, [&] {
+        need(d);
+        QSIM_HIPCHK(hipSetDevice(d->device));
+        flush_carry(d);  // (the previous run's last step, if it was left pending)
+        QSIM_HIPCHK(hipSetDevice(d->device));
+        stream_wait(d, d->comm_stream);
+        stream_wait(d, d->copy_stream);
+        stream_wait(d, d->stream);
+        (void)allreduce_sum(d, 0.0);
+    });
+}
+
 int qsim_dist_perm(qsim_dist* d, int32_t* perm) {
     return dguard([&] {
         need(d);

@@ -86,7 +86,12 @@ __device__ __forceinline__ double flip_gap(uint64_t h, const FlipChan& c, bool* 
     // error of gf: |il2| x (rounding of u, <= 2^-24 / ln 2 absolute in log2 u, + the
     // hardware log2's error, ~2^-22 absolute near 1) + |gf| x (its relative error and two
     // roundings, ~2^-22) — bounded here by 2^-17 x |il2| + 2^-20 x |gf| (16x and 4x
-    // margins).  The margin is kept tight on purpose: a lane that falls back makes its whole
+    // margins).  The hardware figures are assumptions (v_log_f32 is taken to be within ~1 ulp
+    // of log2 of its float input; no ISA accuracy table ships with this image), so the bound is
+    // checked, not trusted: random draws (qsim_noise_gap_check, 2^26 per p) and a targeted sweep
+    // of every integer boundary of the gap up to the block and of the float-rounding interval
+    // around it (qsim_noise_gap_check_edges) must give the double result for every draw
+    // (tests/test_batched_refnoise_gpu.py).  The margin is kept tight on purpose: a lane that falls back makes its whole
     // wave run the double log, so at p = 0.01 a 1 % per-lane fallback rate (a 2^-13 x |il2|
     // bound) left most iterations of a 64-lane wave on the slow path; this one is ~0.1 %.
     const float err = fabsf(gf) * 0x1.0p-20f + fabsf(c.il2) * 0x1.0p-17f;
@@ -1414,7 +1419,84 @@ __global__ __launch_bounds__(256) void k_gap_check(FlipChan c, uint64_t key, uin
     if (mm) atomicAdd(&out[0], mm);
     if (fb) atomicAdd(&out[1], fb);
 }
+// The same comparison on targeted draws: every u index K in [center - half, center + half) of each
+// center (the host's boundary candidates, qsim_noise_gap_check_edges), u = (K + 1) 2^-53.
+__global__ __launch_bounds__(256) void k_gap_edges(FlipChan c, const uint64_t* centers, uint64_t ncent,
+                                                   uint64_t half, unsigned long long* out) {
+    const uint64_t per = 2 * half, total = ncent * per;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    unsigned long long mm = 0, fb = 0;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+        const uint64_t ctr = centers[i / per];
+        const uint64_t off = i % per;
+        const uint64_t K = ctr + off >= half ? ctr + off - half : 0;
+        if (K >= (1ull << 53)) continue;
+        const uint64_t h = K << 11;
+        bool f = false;
+        const double g = flip_gap(h, c, &f);
+        const double u = (double)((h >> 11) + 1ull) * 0x1.0p-53;
+        const double ref = floor(log(u) / c.lq), blk = (double)kFlipBlock;
+        if (!((g < blk ? g : blk) == (ref < blk ? ref : blk))) ++mm;
+        fb += f ? 1ull : 0ull;
+    }
+    if (mm) atomicAdd(&out[0], mm);
+    if (fb) atomicAdd(&out[1], fb);
+}
 }  // namespace qsim_hip
+
+// Targeted boundary sweep: the single-precision first try of flip_gap can only be wrong
+// where ln u / lq lies within its error of an integer m.  For every m in [0, 256] the centers are the
+// double boundary u_m = exp(m lq) and both ends of the interval of doubles that round to the float
+// nearest u_m (where the float path's input is fixed while the double answer changes), each swept
+// over 2 x half consecutive u indices.
+extern "C" int qsim_noise_gap_check_edges(double p, uint64_t half, uint64_t* mismatches, uint64_t* fallbacks,
+                                          uint64_t* draws) {
+    using namespace qsim_hip;
+    if (!mismatches || !fallbacks || !draws || !(p > 0.0) || p > 1.0 || half == 0 || half > (1ull << 24))
+        return QSIM_ERR_INVALID_ARGUMENT;
+    FlipChan c{};
+    if (!flip_channel(0, 0, p, 0, c) || c.always) {
+        *mismatches = *fallbacks = *draws = 0;
+        return QSIM_OK;
+    }
+    std::vector<uint64_t> cent;
+    auto kof = [](double u) -> uint64_t {  // u index K with (K + 1) 2^-53 nearest u
+        const double k = std::floor(u * 0x1.0p53) - 1.0;
+        return k < 0.0 ? 0ull : (k >= 0x1.0p53 ? (1ull << 53) - 1 : (uint64_t)k);
+    };
+    for (int m = 0; m <= (int)kFlipBlock; ++m) {
+        const double um = std::exp((double)m * c.lq);
+        if (!(um > 0.0)) break;
+        cent.push_back(kof(um));
+        const float uf = (float)um;
+        const double lo = 0.5 * ((double)std::nextafter(uf, 0.0f) + (double)uf);
+        const double hi = 0.5 * ((double)uf + (double)std::nextafter(uf, 2.0f));
+        cent.push_back(kof(lo));
+        cent.push_back(kof(std::min(hi, 1.0)));
+    }
+    uint64_t* d_c = nullptr;
+    unsigned long long* d = nullptr;
+    if (hipMalloc((void**)&d_c, cent.size() * sizeof(uint64_t)) != hipSuccess) return QSIM_ERR_DEVICE;
+    if (hipMalloc((void**)&d, 2 * sizeof(unsigned long long)) != hipSuccess) {
+        (void)hipFree(d_c);
+        return QSIM_ERR_DEVICE;
+    }
+    unsigned long long hcnt[2] = {0, 0};
+    bool ok = hipMemcpy(d_c, cent.data(), cent.size() * sizeof(uint64_t), hipMemcpyHostToDevice) == hipSuccess &&
+              hipMemset(d, 0, sizeof(hcnt)) == hipSuccess;
+    if (ok) {
+        hipLaunchKernelGGL(k_gap_edges, dim3(1024), dim3(256), 0, 0, c, d_c, (uint64_t)cent.size(), half, d);
+        ok = hipGetLastError() == hipSuccess && hipDeviceSynchronize() == hipSuccess &&
+             hipMemcpy(hcnt, d, sizeof(hcnt), hipMemcpyDeviceToHost) == hipSuccess;
+    }
+    (void)hipFree(d);
+    (void)hipFree(d_c);
+    if (!ok) return QSIM_ERR_DEVICE;
+    *mismatches = hcnt[0];
+    *fallbacks = hcnt[1];
+    *draws = (uint64_t)cent.size() * 2 * half;
+    return QSIM_OK;
+}
 
 extern "C" int qsim_noise_gap_check(double p, uint64_t draws, uint64_t key, uint64_t* mismatches,
                                     uint64_t* fallbacks) {

@@ -156,6 +156,8 @@ _sig(hip, "qsim_batch_profile_get", [_P, c_int, c_char_p, c_size_t, POINTER(c_do
 _sig(hip, "qsim_noise_apply", [_P, c_int, c_int, c_double, c_uint64, c_uint64])
 _sig(hip, "qsim_noise_check_flips", [POINTER(c_uint64)])
 _sig(hip, "qsim_noise_gap_check", [c_double, c_uint64, c_uint64, POINTER(c_uint64), POINTER(c_uint64)])
+_sig(hip, "qsim_noise_gap_check_edges", [c_double, c_uint64, POINTER(c_uint64), POINTER(c_uint64),
+                                         POINTER(c_uint64)])
 _sig(hip, "qsim_noisy_run", [_P, POINTER(qsim_gate), c_size_t, POINTER(qsim_noise_channel), c_size_t,
                              c_uint64, POINTER(c_uint64), c_int])
 
@@ -199,6 +201,7 @@ _sig(hip, "qsim_dist_virtual_rccl", [_P, c_char_p])
 _sig(hip, "qsim_dist_destroy", [_P])
 _sig(hip, "qsim_dist_run", [_P, POINTER(qsim_gate), c_size_t, c_int])
 _sig(hip, "qsim_dist_sync", [_P])
+_sig(hip, "qsim_dist_barrier", [_P])
 _sig(hip, "qsim_dist_overlapped", [_P, POINTER(c_int)])
 _sig(hip, "qsim_dist_fused_remaps", [_P, POINTER(c_int)])
 _sig(hip, "qsim_dist_carried_runs", [_P, POINTER(c_int)])

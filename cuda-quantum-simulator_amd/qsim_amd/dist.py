@@ -111,6 +111,11 @@ class DistributedSimulator:
 
     def synchronize(self) -> None: _lib.check(_lib.hip.qsim_dist_sync(self._h))
 
+    def barrier(self) -> None:
+        """Collective: this rank's engine idle, then a one-value all-reduce over the communicator
+        (the ranks leave within its latency of one another: bench.py's per-step timing barrier)."""
+        _lib.check(_lib.hip.qsim_dist_barrier(self._h))
+
     def overlappedRemaps(self) -> int:
         """Remaps of the last run that were split in halves overlapping local work."""
         v = _c.c_int(0)

@@ -39,6 +39,34 @@ def _circuit(args):
     return qc.createScalingBenchmarkCircuit(n), "W-REF benchmark_scaling.cu:69-76 (100 H + 20 CNOT)"
 
 
+def _median(xs):
+    xs = sorted(xs)
+    m = len(xs) // 2
+    return xs[m] if len(xs) % 2 else 0.5 * (xs[m - 1] + xs[m])
+
+
+def _step_max(grp, step_s):
+    """Per-step max over ranks of each rank's synchronised step times (one all-gather after the
+    timed region): the statistic of the N = 1 line (bench.py: gates / median step) at every N."""
+    import struct
+    parts = grp.all_gather(struct.pack(f"{len(step_s)}d", *step_s))
+    per_rank = [struct.unpack(f"{len(step_s)}d", p) for p in parts]
+    return [max(col) for col in zip(*per_rank)]
+
+
+def _pmc_traffic(name: str, kernel: str):
+    """HBM bytes per launch of `kernel` from profiles/<name> (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE,
+    corrected as profiles/ README says), or (None, None) when no such measurement is committed."""
+    root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    path = os.path.join(root, "profiles", name)
+    if not os.path.exists(path):
+        return None, None
+    with open(path) as f:
+        ent = json.load(f).get("kernels", {}).get(kernel, {})
+    t = ent.get("hbm_bytes_per_launch")
+    return t, (os.path.relpath(path, root) if t is not None else None)
+
+
 def _cpu_baseline(cpu_fn, circuit, n):
     """Rank 0, after the timed region and its max-over-ranks reduction (so it cannot disturb the
     measurement): bench.py's cpu_baseline leg (the oracle's single-thread restatement of the
@@ -61,16 +89,22 @@ def run_dry(args, metric: str, peak_gbps: float = 8000.0, cpu_fn=None) -> None:
     for _ in range(args.warmup):
         steps, perm = plan(circuit, world, rank, perm)
     grp.barrier()
+    step_s = []
     t0 = time.perf_counter()
     for _ in range(args.steps):
+        grp.barrier()  # (the GPU run's per-step device barrier)
+        ts = time.perf_counter()
         steps, perm = plan(circuit, world, rank, perm)
         xs = [s for s in steps if s["kind"] == "exchange"]
         remaps += len(xs)
         # each exchange of k global qubits sends (1 - 2^-k) of this rank's 16 B x 2^L shard
         sent += sum(16.0 * (1 << L) * (1.0 - 2.0 ** -s["k"]) for s in xs)
+        step_s.append(time.perf_counter() - ts)
     t1 = time.perf_counter()
     grp.barrier()
     wall = max(grp.all_reduce_max(t1 - t0), 1e-9)
+    step_max = [max(x, 1e-9) for x in _step_max(grp, step_s)]
+    med = _median(step_max)
     # every rank must plan the same exchange skeleton (the lockstep contract of qsim_dist_run)
     if grp.all_reduce_min(remaps) != grp.all_reduce_max(remaps):
         raise RuntimeError("ranks planned different numbers of remaps")
@@ -78,18 +112,20 @@ def run_dry(args, metric: str, peak_gbps: float = 8000.0, cpu_fn=None) -> None:
         gates = circuit.getGateCount()
         # the line's full shape; what only the GPU run measures is null (dry_run: true)
         roof = {"bound": "hbm", "kernel": "fused_tile", "achieved": None, "peak": peak_gbps, "unit": "GB/s",
-                "frac": None, "traffic": None, "alg_bytes_per_launch": 32.0 * (1 << L),
+                "frac": None, "traffic": None, "traffic_source": None, "alg_bytes_per_launch": 32.0 * (1 << L),
                 "avg_launch_ms": None, "launches": None}
         comm = {"bytes_sent_per_step": sent / max(1, args.steps), "bytes_sent_last_run": None,
                 "transfer_ms_per_step": None, "transfer_parts_per_step": None, "sent_GBps": None,
                 "local_kernel_ms_per_step": None, "exposed_ms_per_step": None,
                 "overlapped_ms_per_step": None, "source": "host planner (bytes); times need the GPU run"}
         print(json.dumps({
-            "metric": metric, "value": round(gates * args.steps / wall, 2), "unit": "gates/s",
+            "metric": metric, "value": round(gates / med, 2), "unit": "gates/s",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": round(wall / args.steps * 1e3, 3), "higher_is_better": True,
+            "ms_per_step": round(med * 1e3, 3), "higher_is_better": True,
             "scaling": "strong", "vs_baseline": None, "dtype": "c128 (complex<double>)",
             "data": "synthetic", "dry_run": True,
+            "value_is": "gates / median over steps of the max-over-ranks step time",
+            "value_mean": round(gates * args.steps / sum(step_max), 2), "wall_s": round(wall, 4),
             "config": {"workload": wl, "qubits": n, "gates": gates,
                        "remaps_per_step": remaps / max(1, args.steps),
                        "parallelism": f"dry run: host planner on {world} ranks, no GPU"},
@@ -128,16 +164,25 @@ def run(args, metric: str, peak_gbps: float, cpu_fn=None) -> None:
     sim.synchronize()
     sim.profile(True)
     grp.barrier()
+    # Every step synchronised and timed on its own between device barriers (an all-reduce on the
+    # communicator: the ranks leave it within its latency), value = gates / the median over steps
+    # of the max-over-ranks step time — the N = 1 line's statistic (bench.py run_single).
+    step_s = []
     t0 = time.perf_counter()
     for _ in range(args.steps):
+        sim.barrier()
+        ts = time.perf_counter()
         sim.run(circuit, fused=fused)
-    sim.synchronize()
+        sim.synchronize()
+        step_s.append(time.perf_counter() - ts)
     t1 = time.perf_counter()
     grp.barrier()
     wall = grp.all_reduce_max(t1 - t0)
+    step_max = _step_max(grp, step_s)
+    med = _median(step_max)
     stats = sim.profileStats()
     gates = circuit.getGateCount()
-    comm = comm_summary(stats, args.steps, wall, sim.remapBytes())
+    comm = comm_summary(stats, args.steps, sum(step_max), sim.remapBytes())
     comm["fused_remaps_last_run"] = sim.fusedRemaps()
     comm["remap_path"] = ("fused: the last pass before the remap stores into the send buffer's slab "
                           "layout, the step after loads from the receive buffer (no pack / unpack "
@@ -150,17 +195,26 @@ def run(args, metric: str, peak_gbps: float, cpu_fn=None) -> None:
         if dom and dom["launches"]:
             per = dom["alg_bytes"] / dom["launches"]
             avg_s = dom["ms"] / dom["launches"] / 1e3
+            # per-launch HBM bytes of this kernel at the shard's size (rocprofv3 --pmc of the
+            # same sharded run on virtual shards, profiles/pmc_dist_<wl>_<n>q_<G>.json)
+            traffic, tsrc = _pmc_traffic(f"pmc_dist_{args.workload}_{n}q_{world}.json", dom["name"])
             roof = {"bound": "hbm", "kernel": dom["name"], "achieved": round(per / avg_s / 1e9, 1),
                     "peak": peak_gbps, "unit": "GB/s",
-                    "frac": round(per / avg_s / 1e9 / peak_gbps, 4), "traffic": None,
+                    "frac": round(per / avg_s / 1e9 / peak_gbps, 4), "traffic": traffic,
+                    "traffic_source": tsrc,
                     "alg_bytes_per_launch": per, "avg_launch_ms": round(dom["ms"] / dom["launches"], 4),
                     "launches": dom["launches"]}
         out = {
-            "metric": metric, "value": round(gates * args.steps / wall, 2), "unit": "gates/s",
+            "metric": metric, "value": round(gates / med, 2), "unit": "gates/s",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": round(wall / args.steps * 1e3, 3), "higher_is_better": True,
+            "ms_per_step": round(med * 1e3, 3), "higher_is_better": True,
             "scaling": "strong", "vs_baseline": None, "dtype": "c128 (complex<double>)",
             "data": "synthetic",
+            "value_is": "gates / median over steps of the max-over-ranks synchronised step time "
+                        "(device barrier before each step); value_mean = gates x steps / sum of them",
+            "value_mean": round(gates * args.steps / sum(step_max), 2),
+            "ms_per_step_min_max": [round(min(step_max) * 1e3, 3), round(max(step_max) * 1e3, 3)],
+            "wall_s": round(wall, 4),
             "config": {"workload": wl, "qubits": n, "gates": gates,
                        "mode": "Fused" if fused else "PerGate", "state_bytes": 16 << n,
                        "pass_kernels": "jit" if jit else "interpreter",
@@ -208,7 +262,7 @@ def split_trajectories(total: int, world: int, rank: int):
     return rank * base + min(rank, extra), base + (1 if rank < extra else 0)
 
 
-def run_batch(args, metric: str, peak_gbps: float) -> None:
+def run_batch(args, metric: str, peak_gbps: float, cpu_fn=None) -> None:
     """W-BATCH over N GPUs (SURVEY §8(e) "BatchedSimulator shards trivially by trajectory"): each
     rank runs its contiguous share of the --trajectories total (replicas, no data-path exchange;
     strong scaling: the ensemble is fixed), and the ensemble's average probabilities are the
@@ -224,9 +278,14 @@ def run_batch(args, metric: str, peak_gbps: float) -> None:
     from . import circuit as qc
     circuit = qc.createRandomHCCircuit(n, args.depth, args.seed)
     gates = circuit.getGateCount()
+    step_s = []
     if dry:  # skeleton only: split, barriers, max-over-ranks timing, the weighted reduction
         grp.barrier()
         t0 = time.perf_counter()
+        for _ in range(args.steps):
+            grp.barrier()
+            ts = time.perf_counter()
+            step_s.append(time.perf_counter() - ts)
         t1 = time.perf_counter()
         avg = np.full(1 << n, 1.0 / (1 << n))
         stats, roof = [], None
@@ -251,10 +310,15 @@ def run_batch(args, metric: str, peak_gbps: float) -> None:
         sim.synchronize()
         sim.profile(True)
         grp.barrier()
+        # replicas exchange nothing, so a host barrier's release skew cannot enter a rank's own
+        # step time: each step synchronised and timed per rank, max over ranks per step, median
         t0 = time.perf_counter()
         for _ in range(args.steps):
+            grp.barrier()
+            ts = time.perf_counter()
             sim.run(circuit)
-        sim.synchronize()
+            sim.synchronize()
+            step_s.append(time.perf_counter() - ts)
         t1 = time.perf_counter()
         stats = sim.profileStats()
         gate_stats = [s for s in stats if s["alg_bytes"] > 0]
@@ -263,29 +327,40 @@ def run_batch(args, metric: str, peak_gbps: float) -> None:
         if dom and dom["launches"]:
             per = dom["alg_bytes"] / dom["launches"]
             avg_s = dom["ms"] / dom["launches"] / 1e3
+            # per-launch HBM bytes: the same kernels at the same per-rank shape would need a PMC
+            # pass per shard size; the committed one is the 1-GPU ensemble's (16q x 1024), used
+            # only when this rank runs that shape
+            pmc = "pmc_batch_ref_16q.json" if args.batch_noise == "reference" else "pmc_batch_16q.json"
+            traffic, tsrc = _pmc_traffic(pmc, dom["name"]) if (n, count) == (16, 1024) else (None, None)
             roof = {"bound": "hbm", "kernel": dom["name"], "achieved": round(per / avg_s / 1e9, 1),
                     "peak": peak_gbps, "unit": "GB/s", "frac": round(per / avg_s / 1e9 / peak_gbps, 4),
-                    "traffic": None, "alg_bytes_per_launch": per,
+                    "traffic": traffic, "traffic_source": tsrc, "alg_bytes_per_launch": per,
                     "avg_launch_ms": round(avg_s * 1e3, 4), "launches": dom["launches"]}
         avg = sim.getAverageProbabilities()
     grp.barrier()
     wall = max(grp.all_reduce_max(t1 - t0), 1e-9)
+    step_max = [max(x, 1e-9) for x in _step_max(grp, step_s)]
+    med = _median(step_max)
     # ensemble average: sum over ranks of (count_r / total) * average_r (after the timed region)
     parts = grp.all_gather((avg * (count / args.trajectories)).astype(np.float64).tobytes())
     ens = np.sum([np.frombuffer(p, dtype=np.float64) for p in parts], axis=0)
     if rank == 0:
         total = args.trajectories
         print(json.dumps({
-            "metric": metric, "value": round(gates * total * args.steps / wall, 1),
+            "metric": metric, "value": round(gates * total / med, 1),
             "unit": "trajectory-gates/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": round(wall / args.steps * 1e3, 3), "higher_is_better": True,
+            "ms_per_step": round(med * 1e3, 3), "higher_is_better": True,
             "scaling": "strong", "vs_baseline": None, "dtype": "c128 (complex<double>)",
             "data": "synthetic", "dry_run": bool(dry),
+            "value_is": "trajectory-gates / median over steps of the max-over-ranks synchronised step time",
+            "value_mean": round(gates * total * args.steps / sum(step_max), 1), "wall_s": round(wall, 4),
             "config": {"workload": f"W-BATCH {n}q x {total} trajectories, depolarizing {args.noise} "
                                    f"on all qubits after every gate, W-HC depth {args.depth} seed {args.seed}",
                        "qubits": n, "trajectories": total, "gates": gates,
                        "trajectories_per_rank": [split_trajectories(total, world, r)[1] for r in range(world)],
                        "ensemble_probability_sum": float(ens.sum()),
                        "parallelism": f"trajectories sharded over {world} GPUs (replicas, no exchange)"},
-            "roofline": roof, "kernels_rank0": stats, "cpu_baseline": None}), flush=True)
+            "roofline": roof, "kernels_rank0": stats,
+            # rank 0, after the timed region and the reductions
+            "cpu_baseline": cpu_fn(args) if cpu_fn is not None else None}), flush=True)
     grp.close()

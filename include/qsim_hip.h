@@ -334,6 +334,11 @@ int qsim_noise_check_flips(uint64_t* flips);
  * floor(ln u / ln(1 - P)) in double, both capped at one 256-pair block (a walk only needs to know
  * a gap is past its block): *mismatches (0 expected) and *fallbacks. */
 int qsim_noise_gap_check(double p, uint64_t draws, uint64_t key, uint64_t* mismatches, uint64_t* fallbacks);
+/* Tests: the same comparison on TARGETED draws — for every gap boundary m in [0, 256] (u_m =
+ * exp(m ln(1 - P))) and both ends of the interval of doubles that round to the float nearest u_m,
+ * 2 x half consecutive u values around each; *draws = how many were checked. */
+int qsim_noise_gap_check_edges(double p, uint64_t half, uint64_t* mismatches, uint64_t* fallbacks,
+                               uint64_t* draws);
 /* NoisySimulator::run (src/NoiseModel.cu:369-382): each gate, then every channel entry in order,
  * one noise pass each; *counter advances by one per pass.  With no channel entries the circuit
  * runs as fused passes (flags = QSIM_RUN_*), else one kernel per gate (the noise interleaves). */
@@ -441,6 +446,10 @@ int qsim_dist_create_hosted(int n_qubits, int rank, int world, int device, qsim_
 int qsim_dist_destroy(qsim_dist* d);
 int qsim_dist_run(qsim_dist* d, const qsim_gate* gates, size_t count, int flags);
 int qsim_dist_sync(qsim_dist* d);
+/* Collective: qsim_dist_sync, then a one-value all-reduce on the communicator, so every rank
+ * returns within the collective's latency of the others (the per-step timing barrier of the
+ * N > 1 bench; no reference counterpart: the reference is single-GPU, README.md:361-367). */
+int qsim_dist_barrier(qsim_dist* d);
 int qsim_dist_overlapped(qsim_dist* d, int* remaps); /* remaps of the last run that overlapped local work */
 /* Runs of this object whose first step merged the previous run's carried last step (the
  * EXPERIMENTAL cross-run overlap, QSIM_DIST_CARRY=1, off by default; read per run). */

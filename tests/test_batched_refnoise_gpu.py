@@ -414,3 +414,19 @@ def test_single_precision_gaps_never_differ(qsim, gpu_ready, p):
     _lib.check(_lib.hip.qsim_noise_gap_check(p, draws, 0x5eed + int(p * 1e6), ctypes.byref(mm), ctypes.byref(fb)))
     assert mm.value == 0
     assert fb.value < draws // 100
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("p", [0.01, 0.001, 1e-5, 0.05, 0.3, 0.75, 0.99])
+def test_single_precision_gaps_at_every_boundary(qsim, gpu_ready, p):
+    """the targeted form of the check above — 2 x 4096 consecutive u values around every
+    integer boundary of the gap up to the block (u_m = exp(m ln(1 - P)), m = 0..256) and around both
+    ends of the float-rounding interval of u_m, where the single-precision try sees one input while
+    the double answer changes: no draw may differ from the double formula."""
+    import ctypes
+    from qsim_amd import _lib
+    mm, fb, dr = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+    _lib.check(_lib.hip.qsim_noise_gap_check_edges(p, 4096, ctypes.byref(mm), ctypes.byref(fb), ctypes.byref(dr)))
+    assert dr.value >= 3 * 8192  # (at least the m = 0 boundary; small p has all 257)
+    assert mm.value == 0, (mm.value, fb.value, dr.value)
+    assert fb.value > 0  # (the sweep reaches the undecidable draws: it is where the bound matters)

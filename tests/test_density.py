@@ -299,6 +299,41 @@ def _relabeled_runs(qsim, oracle, n, depth, seed):
 
 
 @pytest.mark.gpu
+def test_relabel_policy_governs_dm_relabeling(qsim, oracle, gpu_ready):
+    """the DM first-run relabeling follows qsim_set_relabel — mode 0 keeps the
+    identity labels (no host search); the default relabels from 16 index bits; a parameter sweep
+    (same structure, new angles) reuses the memoised labels; every result equals the oracle."""
+    from qsim_amd.plan import set_relabel
+    n = 8
+    channels = [(0, -1, 0.02)]
+
+    def circ(theta):
+        c = _circuit(qsim, n, 20, 41)
+        c.rz(2, theta)
+        c.ry(5, 0.5 * theta)
+        return c
+    set_relabel(0, -1)
+    try:
+        sim = qsim.DensityMatrixSimulator(n, _noise(qsim, channels))
+        sim.run(circ(0.3))
+        assert not sim.density.state.layoutInfo()["relabeled"]
+        np.testing.assert_allclose(sim.getDensityMatrix(), oracle.dm_run(n, oracle.gates_of(circ(0.3)), channels),
+                                   atol=1e-12, rtol=0)
+    finally:
+        set_relabel(1, 26)
+    sim = qsim.DensityMatrixSimulator(n, _noise(qsim, channels))
+    sim.run(circ(0.3))
+    assert sim.density.state.layoutInfo()["relabeled"]
+    perm0 = sim.density.state.perm()
+    for theta in (0.7, 1.1):
+        sim.reset()
+        sim.run(circ(theta))
+        assert sim.density.state.perm() == perm0  # (memo keyed on structure, not angles)
+        np.testing.assert_allclose(sim.getDensityMatrix(), oracle.dm_run(n, oracle.gates_of(circ(theta)), channels),
+                                   atol=1e-12, rtol=0)
+
+
+@pytest.mark.gpu
 def test_relabeled_run_reference_y_and_pinned_pointer(qsim, oracle, gpu_ready):
     """18 index bits: the relabeled first run with the reference's Y sign (its global -1 op moves
     with the labels), and a rho whose device pointer was handed out before the run (never

@@ -49,6 +49,11 @@ def test_dry_run_launch_prints_one_json_line(world):
     cb = out["cpu_baseline"]
     assert cb["kind"] == "port" and cb["cores"] == 1 and cb["value"] > 0 and "prefix" in cb["sample"]
     assert cb["w_hc_20q"]["value"] > 0
+    # the N = 1 line's statistic (gates / median synchronised step) at every N,
+    # and the PMC traffic field with its source
+    assert "median" in out["value_is"] and out["value_mean"] > 0
+    assert abs(out["value"] - out["config"]["gates"] / (out["ms_per_step"] / 1e3)) <= 0.01 * out["value"]
+    assert "traffic_source" in roof
 
 
 def test_launcher_parent_does_not_load_the_engine():
@@ -126,7 +131,8 @@ def test_batch_dry_run_shards_trajectories(world, total):
     (sizes differ by at most one, covering the ensemble), the trajectory-weighted reduction of the
     ranks' averages is a probability vector, one JSON line."""
     r = subprocess.run([sys.executable, BENCH, "--workload", "batch", "--gpus", str(world), "--dry-run",
-                        "--steps", "2", "--warmup", "1", "--qubits", "10", "--trajectories", str(total)],
+                        "--steps", "2", "--warmup", "1", "--qubits", "10", "--trajectories", str(total),
+                        "--cpu-budget", "1"],
                        capture_output=True, text=True, timeout=300, env=_env())
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
@@ -136,6 +142,11 @@ def test_batch_dry_run_shards_trajectories(world, total):
     assert out["n_gpus"] == world and out["dry_run"] is True and out["unit"] == "trajectory-gates/s"
     assert sum(per) == total and max(per) - min(per) <= 1
     assert abs(out["config"]["ensemble_probability_sum"] - 1.0) < 1e-12
+    # median statistic and the CPU baseline on rank 0 (the oracle's batched
+    # reference-process restatement on a bounded sample)
+    assert "median" in out["value_is"]
+    cb = out["cpu_baseline"]
+    assert cb["kind"] == "port" and cb["unit"] == "trajectory-gates/s" and cb["value"] > 0
 
 
 def test_split_trajectories_covers_the_ensemble():
