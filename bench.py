@@ -102,6 +102,9 @@ def parse():
     p.add_argument("--no-extras", action="store_true",
                    help="skip the default line's extra objects (seeds, default_mode, w_ref, "
                         "gate_table_20q, dm_14q, noisy_26q)")
+    p.add_argument("--extras", default="seeds,default_mode,w_ref,w_hc_28q,h_single,gate_table,dm,noisy",
+                   help="which extra objects of the default W-HC line to measure (comma list; "
+                        "--no-extras: none)")
     p.add_argument("--noise", type=float, default=0.01)
     p.add_argument("--cpu-budget", type=float, default=12.0,
                    help="seconds of single-thread CPU oracle work for cpu_baseline (0 = skip)")
@@ -426,15 +429,24 @@ def run_single(args):
         "kernels": stats,
     }
     del sim
-    if args.workload == "hc" and not args.no_extras:
-        out["seeds"] = hc_seeds(q, args)
-        out["default_mode"] = default_mode(q, args, circuit)
-        out["w_ref"] = w_ref(q, args)
-        out["w_hc_28q"] = w_hc_28q(q, args)
-        out["h_single_synced"] = h_single_synced(q)
-        out["gate_table_20q"] = gate_table_20q(q)
-        out["dm_14q"] = measure_dm(q, 14, 3, 1, args.jit, args.seed, args.depth, 0.01)
-        out["noisy_26q"] = measure_noisy(q, 26, 3, 1, args.seed, args.depth, 0.01)
+    ex = set() if args.no_extras else set(args.extras.split(","))
+    if args.workload == "hc":
+        if "seeds" in ex:
+            out["seeds"] = hc_seeds(q, args)
+        if "default_mode" in ex:
+            out["default_mode"] = default_mode(q, args, circuit)
+        if "w_ref" in ex:
+            out["w_ref"] = w_ref(q, args)
+        if "w_hc_28q" in ex:
+            out["w_hc_28q"] = w_hc_28q(q, args)
+        if "h_single" in ex:
+            out["h_single_synced"] = h_single_synced(q)
+        if "gate_table" in ex:
+            out["gate_table_20q"] = gate_table_20q(q)
+        if "dm" in ex:
+            out["dm_14q"] = measure_dm(q, 14, 3, 1, args.jit, args.seed, args.depth, 0.01)
+        if "noisy" in ex:
+            out["noisy_26q"] = measure_noisy(q, 26, 3, 1, args.seed, args.depth, 0.01)
     if args.workload == "hc" and not args.no_1q28:
         out["roofline_1q28"] = roofline_1q28(q)
     if args.workload == "hc" and not args.no_batch16:

@@ -29,6 +29,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <tuple>
 #include <vector>
 
 #include "device_ops.hpp"
@@ -590,6 +591,401 @@ std::vector<PivotMemo> g_pivots;
 uint64_t g_pivot_clock = 0;
 }  // namespace
 
+// ---- steady-state cycle pivots (the cross-run carry, QSIM_DIST_CARRY) ---------------------
+// A benchmark or trajectory loop re-runs one circuit, and the runs' start maps soon cycle (the remap
+// planner is deterministic; W-HC 30q on 8 ranks: two maps).  With the carry on, run j's last step B_j
+// and run j+1's leading passes run per part of run j's exchange X_j, so X_j's pivots P_j shape TWO
+// runs: run j (A_j's tail and B_j avoid P_j) and run j+1 (A_{j+1}'s head avoids P_j).  mark_overlap
+// chooses P_j for run j alone (at most one pass of the next run credited), and on the alternate
+// runs of seed 42 A's first pass then touches the carried pivots and runs whole and exposed.  Here
+// the pivots of every exchange of the cycle are chosen together: coordinate descent over the
+// cycle, each P_j by the beam search of mark_overlap on the cost T_j + T_{j+1} (the run-time model
+// of mark_overlap with the carry: per-part passes of both neighbouring runs, whole passes exposed),
+// every plan from rank 0's lowering (rank-independent), plans memoised by (step, avoid sets).
+namespace {
+struct CycleMemo {
+    int n, g;
+    std::vector<qsim_gate> gates;
+    std::vector<std::vector<int>> maps;  // start map of each run of the cycle
+    std::vector<uint64_t> piv;           // pivots of each run's exchange
+    uint64_t used;
+};
+std::vector<CycleMemo> g_cycles;  // (under g_pivot_mu)
+}  // namespace
+
+// The pass touch masks of step `ops` planned with tail avoid set `pa` and head avoid set `pb`
+// (all ones for a pass that never runs per part).
+static std::vector<uint64_t> pass_masks(const std::vector<Op>& ops, int L, uint64_t pa, uint64_t pb) {
+    const Plan pl = plan_fused(ops, L, -1, pa, pb);
+    std::vector<uint64_t> m;
+    for (const FusedPass& fp : pl.passes) {
+        if (fp.single >= 0 || fp.h < 4) {
+            m.push_back(~0ull);
+            continue;
+        }
+        uint64_t t = 0;
+        for (int i = 0; i < 6 + fp.h - fp.r0; ++i) t |= 1ull << fp.hpos[i];
+        m.push_back(t);
+    }
+    return m;
+}
+
+// Per pass of the unconstrained plan of `ops`: the positions its gates act on (targets and
+// controls; padding excluded — a tile may be padded elsewhere), all ones for a per-gate pass.
+static std::vector<uint64_t> pass_forced(const std::vector<Op>& ops, int L) {
+    const Plan pl = plan_fused(ops, L);
+    std::vector<uint64_t> m;
+    for (const FusedPass& fp : pl.passes) {
+        if (fp.single >= 0 || fp.h < 4) {
+            m.push_back(~0ull);
+            continue;
+        }
+        int b = fp.op_begin, e = fp.op_end;
+        if (fp.stage_end > fp.stage_begin) {
+            b = pl.stages[fp.stage_begin].op_begin;
+            e = pl.stages[fp.stage_end - 1].op_end;
+        }
+        uint64_t f = 0;
+        for (int i = b; i < e; ++i) {
+            const Op& o = ops[pl.order[i]];
+            f |= (1ull << o.t0) | o.cmask;
+            if (o.t1 >= 0) f |= 1ull << o.t1;
+        }
+        m.push_back(f);
+    }
+    return m;
+}
+
+static bool cycle_pivots(const qsim_gate* gates, size_t count, int n, int g, const std::vector<int>& perm_in,
+                         uint64_t* piv_out) {
+    const int L = n - g;
+    auto same_gates = [&](const CycleMemo& m) {
+        return m.n == n && m.g == g && m.gates.size() == count &&
+               (count == 0 || std::memcmp(m.gates.data(), gates, count * sizeof(qsim_gate)) == 0);
+    };
+    {
+        std::lock_guard<std::mutex> l(g_pivot_mu);
+        for (CycleMemo& m : g_cycles)
+            if (same_gates(m))
+                for (size_t j = 0; j < m.maps.size(); ++j)
+                    if (m.maps[j] == perm_in) {
+                        m.used = ++g_pivot_clock;
+                        *piv_out = m.piv[j];
+                        return true;
+                    }
+    }
+    // the runs from perm_in (rank 0's lowering), until a start map repeats
+    std::vector<std::vector<int>> maps;
+    std::vector<std::vector<DStep>> runs;
+    std::vector<int> p = perm_in;
+    int cyc = -1;
+    for (int r = 0; r < 8 && cyc < 0; ++r) {
+        maps.push_back(p);
+        runs.push_back(plan_dist_core(gates, count, n, g, 0, p));
+        for (size_t j = 0; j < maps.size(); ++j)
+            if (maps[j] == p) cyc = (int)j;
+    }
+    if (cyc != 0) return false;  // (perm_in is a transient map, or no cycle within 8 runs)
+    const int C = (int)runs.size();
+    for (const std::vector<DStep>& st : runs)
+        if (st.size() != 3 || st[0].kind != 0 || st[1].kind != 1 || st[2].kind != 0 || st[0].ops.empty() ||
+            st[2].ops.empty())
+            return false;  // (one remap per run between two ops steps: the case the model prices)
+    static const double r_scale = [] {  // (mark_overlap's QSIM_DIST_MODEL_R)
+        const char* e = std::getenv("QSIM_DIST_MODEL_R");
+        return e ? std::atof(e) : 50.0;
+    }();
+    // a pass run per part (sub-space launches) costs rP whole-shard passes (virtual 30q / 8:
+    // 5.15 vs 6.4 TB/s, profiles/r04/dist_virtual/)
+    static const double rP = [] {
+        const char* e = std::getenv("QSIM_DIST_MODEL_PART");
+        return e ? std::atof(e) : 1.243;
+    }();
+    const double R = r_scale / std::max(2, 1 << g);
+    std::mutex mu;
+    std::map<std::tuple<int, int, uint64_t, uint64_t>, std::vector<uint64_t>> cache;
+    auto masks = [&](int j, int which, uint64_t pa, uint64_t pb) {
+        const auto key = std::make_tuple(j, which, pa, pb);
+        {
+            std::lock_guard<std::mutex> l(mu);
+            auto it = cache.find(key);
+            if (it != cache.end()) return it->second;
+        }
+        std::vector<uint64_t> m = pass_masks(runs[j][which].ops, L, pa, pb);
+        std::lock_guard<std::mutex> l(mu);
+        cache.emplace(key, m);
+        return m;
+    };
+    // B_j's (passes, leading passes avoiding P_j, parts)
+    struct BInfo {
+        int nb, h;
+        double K;
+    };
+    auto binfo = [&](int j, uint64_t P) {
+        const std::vector<uint64_t> mb = masks(j, 2, 0, P);
+        int h = 0;
+        if (P)
+            while (h < (int)mb.size() && !(mb[h] & P)) ++h;
+        return BInfo{(int)mb.size(), h, (double)(1 << __builtin_popcountll(P))};
+    };
+    // T of a run from its A's pass masks, the previous run's B info, carried pivots Pp, own P
+    auto t_of = [&](const std::vector<uint64_t>& ma, const BInfo& bp, uint64_t Pp, uint64_t P) {
+        const int na = (int)ma.size();
+        int hA = 0, t = 0;
+        if (Pp)
+            while (hA < na && !(ma[hA] & Pp)) ++hA;
+        if (P)
+            while (t < na - hA && !(ma[na - 1 - t] & P)) ++t;
+        int c = 0;
+        uint64_t cb = 0;
+        if (P && coarse_enabled()) {  // (coarse_split on the masks)
+            double best = (double)(na - t - hA);
+            uint64_t U = 0;
+            for (int cc = 1; cc <= na - t - hA; ++cc) {
+                U |= ma[na - t - cc] & P;
+                const uint64_t b = P & ~U;
+                if (!b) break;
+                const double e = (double)(na - t - hA - cc) + (double)cc / (double)(1 << __builtin_popcountll(b));
+                if (e < best - 1e-9) {
+                    best = e;
+                    c = cc;
+                    cb = b;
+                }
+            }
+        }
+        const double K = (double)(1 << __builtin_popcountll(P)), Kc = (double)(1 << __builtin_popcountll(cb));
+        const int whole = (na - hA - t - c) + (bp.nb - bp.h);
+        const double exposed = (bp.h + hA) * rP / bp.K + (na - hA - t - c) + c * rP / Kc + t * rP / K + (bp.nb - bp.h);
+        return std::max(R + exposed, whole + (hA + t + c + bp.h) * rP + R / K);
+    };
+    // T_j: run j with carried pivots Pp (of X_{j-1}) and its own P, from the plans under those sets
+    auto tj = [&](int j, uint64_t Pp, uint64_t P) {
+        const int jp = (j + C - 1) % C;
+        return t_of(masks(j, 0, P, Pp), binfo(jp, Pp), Pp, P);
+    };
+    std::vector<uint64_t> P(C, 0);
+    auto cost_j = [&](int j, uint64_t Pj) {  // the terms P_j enters
+        std::vector<uint64_t> Q = P;
+        Q[j] = Pj;
+        const int jn = (j + 1) % C;
+        if (jn == j) return tj(j, Pj, Pj);
+        return tj(j, Q[(j + C - 1) % C], Pj) + tj(jn, Pj, Q[jn]);
+    };
+    auto optimise = [&](int j) {
+        uint64_t lmask = 0;
+        for (int i = 0; i < runs[j][1].k; ++i) lmask |= 1ull << runs[j][1].lpos[i];
+        std::vector<int> cand;
+        for (int q = 6; q < L; ++q)
+            if (!((lmask >> q) & 1ull)) cand.push_back(q);
+        auto score = [&](const std::vector<uint64_t>& sets) {
+            std::vector<double> sc(sets.size(), 1e30);
+            std::vector<std::thread> th;
+            const size_t nt = std::min<size_t>(sets.size(), 16);
+            for (size_t w = 0; w < nt; ++w)
+                th.emplace_back([&, w] {
+                    for (size_t c = w; c < sets.size(); c += nt) try {
+                            sc[c] = cost_j(j, sets[c]);
+                        } catch (...) {
+                        }
+                });
+            for (auto& t : th) t.join();
+            return sc;
+        };
+        std::vector<uint64_t> singles;
+        for (int q : cand) singles.push_back(1ull << q);
+        std::vector<double> s1 = score(singles);
+        double bestT = cost_j(j, 0);
+        uint64_t best = 0;
+        std::vector<size_t> o(singles.size());
+        for (size_t c = 0; c < o.size(); ++c) o[c] = c;
+        std::sort(o.begin(), o.end(), [&](size_t a, size_t b) { return s1[a] != s1[b] ? s1[a] < s1[b] : a < b; });
+        constexpr size_t kBeam = 4, kPool = 10;
+        std::vector<int> pool;
+        std::vector<uint64_t> beam;
+        for (size_t c = 0; c < o.size() && pool.size() < kPool; ++c)
+            if (s1[o[c]] < 1e29) {
+                pool.push_back(cand[o[c]]);
+                if (beam.size() < kBeam) beam.push_back(singles[o[c]]);
+                if (s1[o[c]] < bestT - 1e-9) {
+                    bestT = s1[o[c]];
+                    best = singles[o[c]];
+                }
+            }
+        // (the current choice competes too: a sweep never makes P_j worse)
+        if (P[j]) {
+            const double cur = cost_j(j, P[j]);
+            if (cur < bestT - 1e-9) {
+                bestT = cur;
+                best = P[j];
+            }
+        }
+        for (int m = 1; m < kMaxPivots && !beam.empty(); ++m) {
+            std::vector<uint64_t> sets;
+            for (uint64_t b : beam)
+                for (int q : pool) {
+                    const uint64_t s2 = b | (1ull << q);
+                    if (s2 != b && std::find(sets.begin(), sets.end(), s2) == sets.end()) sets.push_back(s2);
+                }
+            std::vector<double> sc = score(sets);
+            std::vector<size_t> o2(sets.size());
+            for (size_t c = 0; c < o2.size(); ++c) o2[c] = c;
+            std::sort(o2.begin(), o2.end(),
+                      [&](size_t a, size_t b) { return sc[a] != sc[b] ? sc[a] < sc[b] : sets[a] < sets[b]; });
+            beam.clear();
+            for (size_t c = 0; c < o2.size() && beam.size() < kBeam; ++c)
+                if (sc[o2[c]] < 1e29) beam.push_back(sets[o2[c]]);
+            if (!o2.empty() && sc[o2[0]] < bestT - 1e-9) {
+                bestT = sc[o2[0]];
+                best = sets[o2[0]];
+            }
+        }
+        P[j] = best;
+    };
+    // Constructive start: every split of each run's A into a head (avoids the carried pivots) and a
+    // tail (avoids its own), the passes between them whole or coarse.  Under fixed splits P_j may
+    // take any position outside the exchanged ones, B_j's passes, A_j's tail and A_{j+1}'s head
+    // (masks of the unconstrained plans); the up-to-4 such positions used by the fewest passes of
+    // the cycle form P_j.  Splits are ranked by the model on the unconstrained masks, the best few
+    // re-priced on the plans under their sets, and the best becomes the descent's start.
+    static const bool construct = [] {
+        const char* e = std::getenv("QSIM_DIST_CYCLE_CONSTRUCT");
+        return e == nullptr || std::atoi(e) != 0;
+    }();
+    if (C <= 3 && construct) {
+        std::vector<std::vector<uint64_t>> mA(C), mB(C);
+        std::vector<int> use(64, 0);
+        for (int j = 0; j < C; ++j) {
+            mA[j] = pass_forced(runs[j][0].ops, L);
+            mB[j] = pass_forced(runs[j][2].ops, L);
+            for (const auto* v : {&mA[j], &mB[j]})
+                for (uint64_t x : *v)
+                    for (int q = 0; q < L; ++q) use[q] += (int)((x >> q) & 1ull);
+        }
+        uint64_t all = 0;
+        for (int q = 6; q < L; ++q) all |= 1ull << q;
+        std::vector<std::vector<std::pair<int, int>>> splits(C);
+        for (int j = 0; j < C; ++j)
+            for (int h = 0; h <= std::min(1, (int)mA[j].size()); ++h)  // (the planner steers the first pass only)
+                for (int t = 0; h + t <= (int)mA[j].size(); ++t) splits[j].push_back({h, t});
+        struct Combo {
+            double pred;
+            std::vector<uint64_t> P;
+        };
+        std::vector<Combo> combos;
+        std::vector<size_t> idx(C, 0);
+        for (;;) {
+            std::vector<uint64_t> Q(C, 0);
+            for (int j = 0; j < C; ++j) {
+                const int jn = (j + 1) % C;
+                const int t = splits[j][idx[j]].second, hn = splits[jn][idx[jn]].first;
+                uint64_t forbid = 0;
+                for (int i = 0; i < runs[j][1].k; ++i) forbid |= 1ull << runs[j][1].lpos[i];
+                for (uint64_t x : mB[j]) forbid |= x;
+                for (int i = 0; i < t; ++i) forbid |= mA[j][mA[j].size() - 1 - i];
+                for (int i = 0; i < hn; ++i) forbid |= mA[jn][i];
+                std::vector<int> ok;
+                for (int q = 6; q < L; ++q)
+                    if (((all & ~forbid) >> q) & 1ull) ok.push_back(q);
+                std::stable_sort(ok.begin(), ok.end(), [&](int a, int b) { return use[a] < use[b]; });
+                for (size_t i = 0; i < ok.size() && i < (size_t)kMaxPivots; ++i) Q[j] |= 1ull << ok[i];
+            }
+            double pred = 0.0;
+            for (int j = 0; j < C; ++j) {
+                const int jp = (j + C - 1) % C;
+                int hb = 0;
+                if (Q[jp])
+                    while (hb < (int)mB[jp].size() && !(mB[jp][hb] & Q[jp])) ++hb;
+                pred += t_of(mA[j], BInfo{(int)mB[jp].size(), hb, (double)(1 << __builtin_popcountll(Q[jp]))},
+                             Q[jp], Q[j]);
+            }
+            combos.push_back({pred, Q});
+            int j = 0;
+            while (j < C && ++idx[j] == splits[j].size()) idx[j++] = 0;
+            if (j == C) break;
+        }
+        std::sort(combos.begin(), combos.end(), [](const Combo& a, const Combo& b) {
+            return a.pred != b.pred ? a.pred < b.pred : a.P < b.P;
+        });
+        std::vector<std::vector<uint64_t>> tops;
+        for (const Combo& cb : combos) {
+            if (tops.size() >= 12) break;
+            if (std::find(tops.begin(), tops.end(), cb.P) == tops.end()) tops.push_back(cb.P);
+        }
+        std::vector<double> sc(tops.size(), 1e30);
+        {
+            std::vector<std::thread> th;
+            for (size_t c = 0; c < tops.size(); ++c)
+                th.emplace_back([&, c] {
+                    try {
+                        double tot = 0.0;
+                        for (int j = 0; j < C; ++j) tot += tj(j, tops[c][(j + C - 1) % C], tops[c][j]);
+                        sc[c] = tot;
+                    } catch (...) {
+                    }
+                });
+            for (auto& t : th) t.join();
+        }
+        size_t bi = 0;
+        for (size_t c = 1; c < tops.size(); ++c)
+            if (sc[c] < sc[bi] - 1e-9) bi = c;
+        if (std::getenv("QSIM_DIST_DEBUG_CYCLE"))
+            for (size_t c = 0; c < tops.size(); ++c) {
+                double pr = 0;
+                for (const Combo& cb : combos)
+                    if (cb.P == tops[c]) {
+                        pr = cb.pred;
+                        break;
+                    }
+                std::fprintf(stderr, "[cycle] combo %zu pred %.3f real %.3f:", c, pr, sc[c]);
+                for (uint64_t x : tops[c]) std::fprintf(stderr, " %#llx", (unsigned long long)x);
+                for (int j = 0; j < C; ++j) {
+                    std::fprintf(stderr, " | A%d", j);
+                    for (uint64_t x : masks(j, 0, tops[c][j], tops[c][(j + C - 1) % C]))
+                        std::fprintf(stderr, " %#llx", (unsigned long long)x);
+                    std::fprintf(stderr, " B%d", j);
+                    for (uint64_t x : masks(j, 2, 0, tops[c][j])) std::fprintf(stderr, " %#llx", (unsigned long long)x);
+                }
+                std::fprintf(stderr, "\n");
+            }
+        if (!tops.empty() && sc[bi] < 1e29) P = tops[bi];
+    }
+    static const int sweeps = [] {
+        const char* e = std::getenv("QSIM_DIST_CYCLE_SWEEPS");
+        return e ? std::max(0, std::atoi(e)) : 1;
+    }();
+    for (int sw = 0; sw < sweeps; ++sw)
+        for (int j = 0; j < C; ++j) optimise(j);
+    static const bool dbg = std::getenv("QSIM_DIST_DEBUG_CYCLE") != nullptr;
+    if (dbg) {
+        double tot = 0.0;
+        for (int j = 0; j < C; ++j) tot += tj(j, P[(j + C - 1) % C], P[j]);
+        std::fprintf(stderr, "[cycle] %d runs, model %.3f passes per run, pivots", C, tot / C);
+        for (uint64_t x : P) std::fprintf(stderr, " %#llx", (unsigned long long)x);
+        std::fprintf(stderr, "\n");
+        for (int j = 0; j < C; ++j) {
+            const uint64_t Pp = P[(j + C - 1) % C];
+            std::fprintf(stderr, "[cycle] run %d T %.3f | A (head %#llx, tail %#llx):", j, tj(j, Pp, P[j]),
+                         (unsigned long long)Pp, (unsigned long long)P[j]);
+            for (uint64_t x : masks(j, 0, P[j], Pp)) std::fprintf(stderr, " %#llx", (unsigned long long)x);
+            std::fprintf(stderr, " | A free:");
+            for (uint64_t x : masks(j, 0, 0, 0)) std::fprintf(stderr, " %#llx", (unsigned long long)x);
+            std::fprintf(stderr, " | B:");
+            for (uint64_t x : masks(j, 2, 0, P[j])) std::fprintf(stderr, " %#llx", (unsigned long long)x);
+            std::fprintf(stderr, " | X lpos");
+            for (int i = 0; i < runs[j][1].k; ++i) std::fprintf(stderr, " %d", runs[j][1].lpos[i]);
+            std::fprintf(stderr, "\n");
+        }
+    }
+    *piv_out = P[0];
+    std::lock_guard<std::mutex> l(g_pivot_mu);
+    CycleMemo m{n, g, std::vector<qsim_gate>(gates, gates + count), maps, P, ++g_pivot_clock};
+    if (g_cycles.size() >= 8)
+        g_cycles.erase(std::min_element(g_cycles.begin(), g_cycles.end(),
+                                        [](const CycleMemo& a, const CycleMemo& b) { return a.used < b.used; }));
+    g_cycles.push_back(std::move(m));
+    return true;
+}
+
 static std::vector<DStep> plan_dist(const qsim_gate* gates, size_t count, int n, int g, int rank,
                                     std::vector<int>& perm, uint64_t carry = 0) {
     const std::vector<int> perm_in = perm;
@@ -620,6 +1016,45 @@ static std::vector<DStep> plan_dist(const qsim_gate* gates, size_t count, int n,
                     }
                 return steps;
             }
+    }
+    // carry on and the start map on a cycle of one-remap runs: the cycle's jointly chosen pivots
+    uint64_t cyc_piv = 0;
+    if (carry_enabled() && overlap && L >= 8 && steps.size() == 3 && steps[0].kind == 0 && steps[1].kind == 1 &&
+        steps[2].kind == 0 && cycle_pivots(gates, count, n, g, perm_in, &cyc_piv) && cyc_piv) {
+        DStep& A = steps[0];
+        DStep& ex = steps[1];
+        ex.pmask = cyc_piv;
+        ex.pivot = __builtin_ctzll(cyc_piv);
+        A.role |= 1;
+        steps[2].role |= 2;
+        if (carry) A.role |= 2;
+        // coarse bits for this run's actual carry, on rank 0's lowering (rank-independent)
+        ex.coarse = 0;
+        if (coarse_enabled()) {
+            std::vector<int> p0 = perm_in;
+            const std::vector<DStep> ref = plan_dist_core(gates, count, n, g, 0, p0);
+            if (ref.size() == 3 && !ref[0].ops.empty()) {
+                const Plan pA = plan_fused(ref[0].ops, L, -1, cyc_piv, carry);
+                const int na = (int)pA.passes.size();
+                int ha = 0, t = 0;
+                if (carry)
+                    while (ha < na && pass_avoids(pA.passes[ha], carry)) ++ha;
+                while (t < na - ha && pass_avoids(pA.passes[na - 1 - t], cyc_piv)) ++t;
+                (void)coarse_split(pA, ha, na - t, cyc_piv, &ex.coarse);
+            }
+        }
+        PivotMemo m{n, g, carry, std::vector<qsim_gate>(gates, gates + count), perm_in, {}, {}, 0};
+        for (const DStep& st : steps) {
+            m.pmask.push_back(st.kind == 1 ? st.pmask : 0ull);
+            m.coarse.push_back(st.kind == 1 ? st.coarse : 0ull);
+        }
+        std::lock_guard<std::mutex> l(g_pivot_mu);
+        m.used = ++g_pivot_clock;
+        if (g_pivots.size() >= 16)
+            g_pivots.erase(std::min_element(g_pivots.begin(), g_pivots.end(),
+                                            [](const PivotMemo& a, const PivotMemo& b) { return a.used < b.used; }));
+        g_pivots.push_back(std::move(m));
+        return steps;
     }
     // the next run's first ops step (rank 0's lowering, from this run's end map: the same on every
     // rank), for scoring the last remap's pivots by the passes it can carry
@@ -1449,6 +1884,8 @@ qsim_dist::RunPlan& run_plan(qsim_dist* d, const qsim_gate* gates, size_t count,
 }
 // Run the carried step (the per-part head of the previous run's last remap) now, part by part as
 // each part lands; every entry that touches the state, or a run that cannot merge it, calls this.
+// A shard whose carried step has passes that touch the pivots (j1 < np: its lowering differs from
+// rank 0's, e.g. gates dropped by a global control) runs those whole once every part has landed.
 void flush_carry(qsim_dist* d) {
     qsim_dist::Carry& c = d->carry;
     if (!c.active) return;
@@ -1461,6 +1898,10 @@ void flush_carry(qsim_dist* d) {
                 run_part(d, d->shards[i], c.rp->steps[i][c.step].ops, c.runs[i], 0, c.runs[i].j1, c.pbs[i], h,
                          c.homes[i], c.alts[i]);
     }
+    for (size_t i = 0; i < d->shards.size(); ++i)
+        if (c.runs[i].plan && c.runs[i].j1 < c.runs[i].np)
+            run_part(d, d->shards[i], c.rp->steps[i][c.step].ops, c.runs[i], c.runs[i].j1, c.runs[i].np, 0, -1,
+                     c.homes[i], c.alts[i]);
     c.active = false;
     c.rp->in_use = false;
     c.rp = nullptr;
@@ -1763,12 +2204,18 @@ int qsim_dist_run(qsim_dist* d, const qsim_gate* gates, size_t count, int flags)
                 }
             }
             const bool head = pb && pending;
-            // the run's last step, every pass of it in the per-part head: leave it pending (the next
-            // run merges it into its first step's head; anything else flushes it)
+            // the run's last step, the per-part head of the run's last remap: leave it pending (the
+            // next run merges it into its first step's head; anything else flushes it).  Decided on
+            // the step skeleton alone (roles, pivots: the same on every rank), never on this rank's
+            // own passes — the next run plans its pivots with the carried ones (carry_in), so ranks
+            // that decided differently would plan different part counts for the same exchange
+            // (round 5 required every shard's step to lie wholly in the head; at world 8 / 20 qubits
+            // some shards' lowerings differ from rank 0's — gates dropped by a global control — so
+            // no run ever carried, and separate rank processes could have disagreed).  A shard whose
+            // step has passes that touch the pivots runs them whole after the last part (flush_carry
+            // and the merged head below).
             if (head && carry_on && k + 1 == plans[0].size() && !pa && (flags & QSIM_RUN_FUSED) && !(k == 0 && merge)) {
-                bool all = true;
-                for (size_t i = 0; i < S; ++i) all = all && runs[i].plan && runs[i].j1 == runs[i].np;
-                if (all) {
+                {
                     qsim_dist::Carry& c = d->carry;
                     c.active = true;
                     c.pmask = pb;
@@ -1786,23 +2233,34 @@ int qsim_dist_run(qsim_dist* d, const qsim_gate* gates, size_t count, int flags)
             }
             if (head) {
                 const bool carried = k == 0 && merge;
+                const qsim_dist::Carry& c = d->carry;
+                // a shard whose carried step is partial (see flush_carry) interleaves nothing: its
+                // carried head per part, then after the last part the rest of that step whole and
+                // this step's head whole
+                auto partial = [&](size_t i) { return carried && c.runs[i].plan && c.runs[i].j1 < c.runs[i].np; };
                 if (pending > kMaxParts) fail(QSIM_ERR_RUNTIME, "pending remap with too many parts");
                 for (int oi = 0; oi < pending; ++oi) {
                     const int h = d->order[oi];
                     QSIM_HIPCHK(hipStreamWaitEvent(d->stream, d->pev[3 * kMaxParts + h], 0));
-                    if (carried) {  // part h of the previous run's last step, then part h of this one
-                        const qsim_dist::Carry& c = d->carry;
+                    if (carried)  // part h of the previous run's last step, then part h of this one
                         for (size_t i = 0; i < S; ++i)
                             if (c.runs[i].plan)
                                 run_part(d, d->shards[i], c.rp->steps[i][c.step].ops, c.runs[i], 0, c.runs[i].j1,
                                          c.pbs[i], h, c.homes[i], c.alts[i]);
-                    }
                     for (size_t i = 0; i < S; ++i)
-                        if (runs[i].plan)
+                        if (runs[i].plan && !partial(i))
                             run_part(d, d->shards[i], plans[i][k].ops, runs[i], 0, runs[i].j1, pbs[i], h, homes[i],
                                      alts[i]);
                 }
                 if (carried) {
+                    for (size_t i = 0; i < S; ++i)
+                        if (partial(i)) {
+                            run_part(d, d->shards[i], c.rp->steps[i][c.step].ops, c.runs[i], c.runs[i].j1,
+                                     c.runs[i].np, 0, -1, c.homes[i], c.alts[i]);
+                            if (runs[i].plan)
+                                run_part(d, d->shards[i], plans[i][k].ops, runs[i], 0, runs[i].j1, 0, -1, homes[i],
+                                         alts[i]);
+                        }
                     d->carry.active = false;
                     d->carry.rp->in_use = false;
                     d->carry.rp = nullptr;
@@ -2153,9 +2611,10 @@ static int plan_passes_impl(int n, int world, int rank, const qsim_gate* gates, 
                     passes[width * k + 4] = coarse_bits;
                 }
             }
-            // a last step run wholly per part is carried into the next run (qsim_dist_run)
-            if (k + 1 == st.size() && k > 0 && st[k].kind == 0 && (st[k].role & 2) && !(st[k].role & 1) && np > 0 &&
-                head == np)
+            // the per-part head of the run's last remap is carried into the next run (qsim_dist_run:
+            // decided on the skeleton alone, the same on every rank)
+            if (k + 1 == st.size() && k > 0 && st[k].kind == 0 && (st[k].role & 2) && !(st[k].role & 1) &&
+                st[k - 1].pmask)
                 carry_out = st[k - 1].pmask;
         }
         if (n_steps) *n_steps = st.size();
@@ -2186,6 +2645,7 @@ int qsim_dist_plan_memo_clear(void) {
     return dguard([&] {
         std::lock_guard<std::mutex> l(g_pivot_mu);
         g_pivots.clear();
+        g_cycles.clear();
     });
 }
 

@@ -34,6 +34,9 @@ run_pmc() {  # name, command...
 for rg in $REGIONS; do
   case $rg in
     hc) prof hc --steps 20 --warmup 2 --no-1q28 --no-batch16 --no-extras || exit 1 ;;
+    hc28) prof hc28 --steps 3 --warmup 1 --no-1q28 --no-batch16 --extras w_hc_28q || exit 1 ;;
+    pmchc28)
+      run_pmc hc_28q python3 $R/bench.py --qubits 28 --cpu-budget 0 --steps 3 --warmup 1 --no-1q28 --no-batch16 --no-extras || exit 1 ;;
     1q28) prof 1q28 --steps 3 --warmup 1 --no-batch16 --no-extras || exit 1 ;;
     batch16ref) prof batch16ref --steps 3 --warmup 1 --no-1q28 --no-extras || exit 1 ;;
     noisy26) prof noisy26 --workload noisy --steps 3 || exit 1 ;;

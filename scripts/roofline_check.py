@@ -23,6 +23,7 @@ PEAK = 8000.0  # GB/s, MI355X HBM3E (MI355X_MICROARCH.md)
 # region -> (how to find the line's roofline object, rocprof kernel-name pattern)
 REGIONS = {
     "hc": (lambda o: o["roofline"], r"^(qk\d+|.*k_fused_(staged|tile).*)"),
+    "hc28": (lambda o: o["w_hc_28q"]["roofline"], r"^(qk\d+|.*k_fused_(staged|tile).*)"),
     "1q28": (lambda o: o["roofline_1q28"], r".*k_m1_(slice|lane).*"),
     "batch16ref": (lambda o: o["roofline_batch16"]["reference"]["roofline"], None),
     # (the default line's nested objects, or the --workload noisy / dm line itself)

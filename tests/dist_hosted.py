@@ -142,7 +142,7 @@ def main(argv) -> int:
                 "total": d.getTotalProbability(),
                 "p0": [d.probBitZero(b) for b in range(n)],
                 "perm": d.perm(), "perms_in": perms, "overlapped": overlapped,
-                "remap_bytes": sent}
+                "remap_bytes": sent, "carried": d.carriedRuns()}
             st = d.getStateVector()
             if rank == 0:
                 np.save(os.path.join(out, f"{key}.npy"), st)

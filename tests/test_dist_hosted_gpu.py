@@ -34,6 +34,62 @@ def _ports(k):
     return ports
 
 
+def _launch(world, n, tmp_path, carry=False):
+    sys.path.insert(0, HERE)
+    ports = _ports(world)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    if carry:
+        env["QSIM_DIST_CARRY"] = "1"
+    procs = [subprocess.Popen([sys.executable, "-u", os.path.join(HERE, "dist_hosted.py"), str(r), str(world),
+                               ",".join(map(str, ports)), str(n), str(tmp_path)], env=env,
+                              stdout=subprocess.PIPE, stderr=subprocess.STDOUT)
+             for r in range(world)]
+    outs = []
+    try:
+        for p in procs:
+            out, _ = p.communicate(timeout=100)
+            outs.append(out.decode(errors="replace")[-3000:])
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    for r, p in enumerate(procs):
+        assert p.returncode == 0, f"rank {r} failed:\n{outs[r]}"
+    return [json.load(open(tmp_path / f"rank{r}.json")) for r in range(world)]
+
+
+@pytest.mark.subprocess  # started before this process initialises the GPU (pool rule)
+@pytest.mark.parametrize("world,n", [(8, 16), (4, 16)])
+def test_rank_processes_with_cross_run_carry(qsim, oracle, tmp_path, world, n):
+    """The cross-run carry (QSIM_DIST_CARRY=1) with one process per rank: each rank decides to
+    carry its run's last step from the step skeleton alone (roles and pivots, the same on every
+    rank) — not from its own passes, whose lowering differs per rank — so every rank carries the
+    same runs and plans the next run's pivots with the same carried ones.  States equal the oracle
+    at 1e-12, every rank reports the same carried-run count and collective values, and the carry
+    merged at least once."""
+    sys.path.insert(0, HERE)
+    import dist_hosted
+    recs = _launch(world, n, tmp_path, carry=True)
+    merged = 0
+    for name, c in dist_hosted.circuits(qsim, n):
+        g = oracle.gates_of(c)
+        ref = oracle.run_cpu(n, g + g + g)
+        for mode in ("fused", "pergate"):
+            key = f"{name}_{mode}"
+            if key not in recs[0]["runs"]:
+                continue
+            np.testing.assert_allclose(np.load(tmp_path / f"{key}.npy"), ref, atol=1e-12, rtol=0, err_msg=key)
+            for rec in recs:
+                run = rec["runs"][key]
+                assert run["carried"] == recs[0]["runs"][key]["carried"], key
+                assert run["perm"] == recs[0]["runs"][key]["perm"]
+                assert abs(run["total"] - 1.0) < 1e-12
+            merged += recs[0]["runs"][key]["carried"]
+    assert merged >= 1
+
+
 @pytest.mark.subprocess  # started before this process initialises the GPU (pool rule)
 @pytest.mark.parametrize("world,n", [(2, 14), (4, 16), (8, 16), (8, 10)])
 def test_rank_processes_match_oracle(qsim, oracle, tmp_path, world, n):
