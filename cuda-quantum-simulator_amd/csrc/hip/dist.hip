@@ -847,9 +847,13 @@ static bool cycle_pivots(const qsim_gate* gates, size_t count, int n, int g, con
     // (masks of the unconstrained plans); the up-to-4 such positions used by the fewest passes of
     // the cycle form P_j.  Splits are ranked by the model on the unconstrained masks, the best few
     // re-priced on the plans under their sets, and the best becomes the descent's start.
+    // (QSIM_DIST_CYCLE_CONSTRUCT=1, measured not kept: W-HC 30q / 8, the carry model over seeds
+    // 42 / 1-3 gives 4.03 / 3.98 / 4.11 / 3.97x with it against 4.18 / 4.00 / 4.11 / 4.22x from the
+    // descent alone — W-HC tiles are dense, a split's free positions number one or two, and the
+    // plans re-padded under the chosen sets lose the split anyway)
     static const bool construct = [] {
         const char* e = std::getenv("QSIM_DIST_CYCLE_CONSTRUCT");
-        return e == nullptr || std::atoi(e) != 0;
+        return e != nullptr && std::atoi(e) != 0;
     }();
     if (C <= 3 && construct) {
         std::vector<std::vector<uint64_t>> mA(C), mB(C);
@@ -951,7 +955,7 @@ static bool cycle_pivots(const qsim_gate* gates, size_t count, int n, int g, con
     }
     static const int sweeps = [] {
         const char* e = std::getenv("QSIM_DIST_CYCLE_SWEEPS");
-        return e ? std::max(0, std::atoi(e)) : 1;
+        return e ? std::max(0, std::atoi(e)) : 2;
     }();
     for (int sw = 0; sw < sweeps; ++sw)
         for (int j = 0; j < C; ++j) optimise(j);
