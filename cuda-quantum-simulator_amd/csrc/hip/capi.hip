@@ -835,7 +835,14 @@ static LayoutChoice dm_choose_layout(int nbits, const std::vector<Op>& ops, size
         for (const Op& o : ops) out.push_back(permute_op(o, pi));
         return out;
     };
-    return choose_layout(nbits, lower, dm_relabel_tries(nbits, want_alts > 0), want_alts);
+    // QSIM_DM_STAGE_US (default 1000, layout-cost units per register stage; 0: cost alone): the
+    // round-5 timed candidates at 14 qubits ran ~0.1 ms longer per stage and per 1 000 units of
+    // predicted cost (profiles/r05/dm_relabel/sweep, stage counts from QSIM_DM_CAND_DEBUG)
+    static const double stage_us = [] {
+        const char* e = std::getenv("QSIM_DM_STAGE_US");
+        return e ? std::max(0.0, std::atof(e)) : 1000.0;
+    }();
+    return choose_layout(nbits, lower, dm_relabel_tries(nbits, want_alts > 0), want_alts, stage_us);
 }
 
 static qsim_gate map_gate(const qsim_state* s, const qsim_gate& g) {
@@ -1773,7 +1780,30 @@ int qsim_dm_plan_info(int n, const qsim_gate* gates, size_t count, const qsim_no
         const TileHeightScope tile_h(th, tile_rb_for(2 * n, th));
         Plan plan;
         LayoutChoice lc;
-        if (flags & QSIM_DM_PLAN_RELABELED) lc = dm_choose_layout(2 * n, ops);
+        if (flags & QSIM_DM_PLAN_RELABELED) {
+            // (QSIM_DM_CAND_DEBUG: every candidate the timed first run would time, in its order:
+            // passes, register stages per pass, layout cost)
+            static const bool dbg = std::getenv("QSIM_DM_CAND_DEBUG") != nullptr;
+            static const size_t nalt = [] {
+                const char* e = std::getenv("QSIM_DM_CAND_DEBUG");
+                return e ? (size_t)std::max(1, std::atoi(e)) : (size_t)1;
+            }();
+            lc = dm_choose_layout(2 * n, ops, dbg ? nalt - 1 : 0);
+            if (dbg && !lc.perm.empty()) {
+                auto show = [&](size_t k, const Plan& pl) {
+                    int st = 0;
+                    std::string per;
+                    for (const FusedPass& fp : pl.passes) {
+                        st += fp.stage_end - fp.stage_begin;
+                        per += " " + std::to_string(fp.stage_end - fp.stage_begin);
+                    }
+                    std::fprintf(stderr, "[dmcand] %zu passes %zu stages %d (%s ) cost %.1f\n", k, pl.passes.size(), st,
+                                 per.c_str(), plan_layout_cost_us(pl));
+                };
+                show(0, lc.plan);
+                for (size_t a = 0; a < lc.alts.size(); ++a) show(a + 1, lc.alts[a].plan);
+            }
+        }
         if (!lc.perm.empty()) plan = std::move(lc.plan);
         else plan = plan_fused(ops, 2 * n);  // (as qsim_dm_run's run_fused plans it)
         for (size_t p = 0; p < plan.passes.size() && p < cap && info; ++p) {

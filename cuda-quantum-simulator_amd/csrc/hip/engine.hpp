@@ -279,8 +279,11 @@ struct LayoutChoice {
     };
     std::vector<Alt> alts;
 };
+// stage_us > 0: the fewest-pass candidates are ranked by their plans' layout cost plus stage_us per
+// register stage (density-matrix passes spend their time in their stages) instead of by the
+// annealed layout cost alone.
 LayoutChoice choose_layout(int n, const std::function<std::vector<Op>(const std::vector<int>&)>& lower,
-                           int tries, size_t want_alts = 0);
+                           int tries, size_t want_alts = 0, double stage_us = 0.0);
 // QSIM_RELABEL_CALIBRATE (default 1) / QSIM_RELABEL_CALIBRATE_MIN_QUBITS (default 26): with
 // inline compilation (QSIM_JIT=2) the first run of a basis state times the model's choice and
 // its alternatives with their circuit-specialised kernels and keeps the fastest (capi.hip).

@@ -242,14 +242,151 @@ static void plan_stages(std::vector<TileOp>& pass_ops, std::vector<int>& pass_sr
             if ((allowed >> b) & 1u) sbits |= 1u << b;
         return sbits;
     };
+    // The ops an in-order scan takes with register bits fixed to S (an op is taken when its target
+    // bit is in S and no earlier deferred op touches its bits; diagonal ops need no register bit).
+    auto take_fixed = [&](const std::vector<int>& from, uint32_t S) {
+        Taken t;
+        uint32_t blocked = 0;
+        for (int i : from) {
+            const TileOp& o = ops[i];
+            const uint32_t need = o.kind == K_M1 ? (1u << o.b0) : 0u;
+            const uint32_t touch = o.cmask | (1u << o.b0);
+            if ((touch & blocked) == 0 && (need & ~S) == 0) {
+                t.sbits |= need;
+                t.in.push_back(i);
+            } else {
+                t.deferred.push_back(i);
+                blocked |= touch;
+            }
+        }
+        return t;
+    };
+    // One stage: the first-fit scan (register bits claimed in program order), or — when it takes
+    // more ops — register bits grown greedily from the best PAIR of allowed bits, one bit at a time,
+    // each time the bit that lets the scan take the most ops (QSIM_STAGE_SEARCH=0: first fit
+    // only).  Fewer LDS round trips per pass: the density-matrix passes spend their time in their
+    // stages, W-HC 14q DM 39-47 stages per 6-pass plan with first fit.
+    static const bool search = [] {
+        const char* e = std::getenv("QSIM_STAGE_SEARCH");
+        return e == nullptr || std::atoi(e) != 0;
+    }();
+    auto stage = [&](const std::vector<int>& from, uint32_t allowed) {
+        Taken ff = take(from, allowed);
+        if (!search || ff.deferred.empty() || rb < 2) return ff;
+        std::vector<int> bits;
+        for (int b = 0; b < tile_bits; ++b)
+            if ((allowed >> b) & 1u) bits.push_back(b);
+        uint32_t S = 0;
+        size_t got = 0;
+        for (size_t i = 0; i < bits.size(); ++i)
+            for (size_t j = i + 1; j < bits.size(); ++j) {
+                const uint32_t s2 = (1u << bits[i]) | (1u << bits[j]);
+                const size_t c = take_fixed(from, s2).in.size();
+                if (c > got) {
+                    got = c;
+                    S = s2;
+                }
+            }
+        while (__builtin_popcount(S) < rb) {
+            int bb = -1;
+            for (int b : bits) {
+                if ((S >> b) & 1u) continue;
+                const size_t c = take_fixed(from, S | (1u << b)).in.size();
+                if (c > got) {
+                    got = c;
+                    bb = b;
+                }
+            }
+            if (bb < 0) break;
+            S |= 1u << bb;
+        }
+        if (got <= ff.in.size()) return ff;
+        return take_fixed(from, S);
+    };
+    // Candidate register-bit sets of one stage for the beam below: first fit, and the best few
+    // pairs of allowed bits each grown greedily to rb bits.
+    auto stage_cands = [&](const std::vector<int>& from, uint32_t allowed) {
+        std::vector<Taken> out;
+        out.push_back(take(from, allowed));
+        if (out[0].deferred.empty() || rb < 2) return out;
+        std::vector<int> bits;
+        for (int b = 0; b < tile_bits; ++b)
+            if ((allowed >> b) & 1u) bits.push_back(b);
+        std::vector<std::pair<size_t, uint32_t>> pairs;
+        for (size_t i = 0; i < bits.size(); ++i)
+            for (size_t j = i + 1; j < bits.size(); ++j) {
+                const uint32_t s2 = (1u << bits[i]) | (1u << bits[j]);
+                pairs.push_back({take_fixed(from, s2).in.size(), s2});
+            }
+        std::sort(pairs.begin(), pairs.end(), [](const auto& a, const auto& b) {
+            return a.first != b.first ? a.first > b.first : a.second < b.second;
+        });
+        for (size_t k = 0; k < pairs.size() && k < 4; ++k) {
+            uint32_t S = pairs[k].second;
+            size_t got = pairs[k].first;
+            while (__builtin_popcount(S) < rb) {
+                int bb = -1;
+                for (int b : bits) {
+                    if ((S >> b) & 1u) continue;
+                    const size_t c = take_fixed(from, S | (1u << b)).in.size();
+                    if (c > got) {
+                        got = c;
+                        bb = b;
+                    }
+                }
+                if (bb < 0) break;
+                S |= 1u << bb;
+            }
+            Taken t = take_fixed(from, S);
+            bool dup = false;
+            for (const Taken& o : out) dup = dup || o.in == t.in;
+            if (!dup) out.push_back(std::move(t));
+        }
+        return out;
+    };
     std::vector<int> rem(ops.size());
     for (size_t i = 0; i < rem.size(); ++i) rem[i] = (int)i;
     std::vector<std::pair<uint32_t, std::vector<int>>> seq;  // (register bits, ops) per stage
-    Taken first = take(rem, high_bits);
-    seq.push_back({pad(first.sbits, high_bits, first.in), first.in});
-    rem.swap(first.deferred);
+    static const int beam_w = [] {  // QSIM_STAGE_BEAM: beam width over stage sequences (0: greedy)
+        const char* e = std::getenv("QSIM_STAGE_BEAM");
+        return e ? std::max(0, std::atoi(e)) : 0;
+    }();
+    if (search && beam_w > 0) {
+        // Beam over stage sequences: states ranked by the ops still to place (then by stages so
+        // far, equal at a level); the first state with none left wins (fewest stages found).
+        struct St {
+            std::vector<int> rem;
+            std::vector<std::pair<uint32_t, std::vector<int>>> seq;
+        };
+        std::vector<St> beam(1);
+        beam[0].rem = rem;
+        for (int level = 0; !beam.empty(); ++level) {
+            std::vector<St> next;
+            for (const St& st : beam)
+                for (Taken& t : stage_cands(st.rem, level == 0 ? high_bits : all_bits)) {
+                    St ns;
+                    ns.seq = st.seq;
+                    ns.seq.push_back({level == 0 ? pad(t.sbits, high_bits, t.in) : t.sbits, t.in});
+                    ns.rem = std::move(t.deferred);
+                    next.push_back(std::move(ns));
+                }
+            std::stable_sort(next.begin(), next.end(), [](const St& a, const St& b) { return a.rem.size() < b.rem.size(); });
+            if (next.empty()) break;
+            if (next[0].rem.empty()) {
+                seq = std::move(next[0].seq);
+                rem.clear();
+                break;
+            }
+            next.resize(std::min<size_t>(next.size(), (size_t)beam_w));
+            beam.swap(next);
+        }
+    } else {
+        Taken first = stage(rem, high_bits);
+        seq.push_back({pad(first.sbits, high_bits, first.in), first.in});
+        rem.swap(first.deferred);
+    }
     while (!rem.empty()) {
-        Taken t = take(rem, all_bits);
+        Taken t = stage(rem, all_bits);
         seq.push_back({t.sbits, t.in});
         rem.swap(t.deferred);
     }

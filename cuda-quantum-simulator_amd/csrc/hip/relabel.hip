@@ -249,7 +249,7 @@ std::vector<int> choose_relabel(const std::vector<uint64_t>& tiles, int n, doubl
 // >= 3 % cheaper.  `lower` maps the caller's gates through a permutation and lowers them exactly
 // as the caller will (so the returned plan can be cached under the same key).
 LayoutChoice choose_layout(int n, const std::function<std::vector<Op>(const std::vector<int>&)>& lower,
-                           int tries, size_t want_alts) {
+                           int tries, size_t want_alts, double stage_us) {
     const int h = tile_height_default();  // the calling thread's height, for the worker threads too
     const double t13 = layout_t13();      // and its 13-qubit tile cost factor
     const bool ctrl_out = tile_ctrl_out();  // (CtrlOutOff is per thread: carried into the workers)
@@ -323,9 +323,27 @@ LayoutChoice choose_layout(int n, const std::function<std::vector<Op>(const std:
             });
         for (auto& t : th) t.join();
     }
+    if (stage_us > 0.0) {  // rank by the annealed plans' cost + stages (see the declaration)
+        std::vector<std::thread> th;
+        for (size_t i = 0; i < pool.size(); ++i)
+            th.emplace_back([&, i] {
+                const LayoutT13Scope sc(t13);
+                std::unique_ptr<CtrlOutOff> off;
+                if (!ctrl_out) off = std::make_unique<CtrlOutOff>();
+                try {
+                    const Plan p = plan_fused(lower(total[i]), n, h);
+                    int st = 0;
+                    for (const FusedPass& fp : p.passes) st += fp.stage_end - fp.stage_begin;
+                    pred[i] = plan_layout_cost_us(p) + stage_us * st;
+                } catch (...) {
+                    pred[i] = 1e300;
+                }
+            });
+        for (auto& t : th) t.join();
+    }
     std::vector<size_t> order(pool.size());
     for (size_t i = 0; i < order.size(); ++i) order[i] = i;
-    std::sort(order.begin(), order.end(), [&](size_t a, size_t b) { return pred[a] < pred[b]; });
+    std::stable_sort(order.begin(), order.end(), [&](size_t a, size_t b) { return pred[a] < pred[b]; });
     bool chosen = false;  // the first acceptable candidate; then up to want_alts alternatives
     for (size_t i : order) {
         // the annealed labels may steer the planner differently: verify, else the candidate as is
