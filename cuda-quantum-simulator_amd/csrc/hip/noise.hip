@@ -25,6 +25,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <string>
+#include <type_traits>
 
 #include "device_ops.hpp"
 #include "engine.hpp"
@@ -999,6 +1000,52 @@ struct MapArgs {
     FlipChan ch[kMaxPullChannels];
 };
 
+// Sparse code words (QSIM_NOISE_SPARSE, default on): 16 bits per amplitude instead of 32 / 64.  At
+// p = 0.01 a code word holds at most two non-zero fields for all but ~0.2 % of the amplitudes
+// (26 channels), so the word of amplitude k is stored as up to two (channel, code) entries —
+// bits 0-4 channel and 5-6 code of the highest flipping channel, 7-11 / 12-13 of the next, 14-15
+// the entry count — and a word with three or more non-zero fields as count 3, its full 64-bit
+// word at ovf[k] (a second array of the same index space, touched only at those amplitudes).  The
+// pull pass then streams 2 B of words per amplitude instead of 8 (26 channels) or 4 (<= 16).
+// (32-bit halves throughout: the map encodes every word of the state once per step)
+__device__ __forceinline__ uint32_t top_field(uint32_t nzl, uint32_t nzh) {  // highest non-zero field
+    return nzh ? 16u + ((31u - (uint32_t)__clz((int)nzh)) >> 1) : (31u - (uint32_t)__clz((int)nzl)) >> 1;
+}
+__device__ __forceinline__ uint16_t sparse_encode(unsigned long long w, bool* over) {
+    const uint32_t lo = (uint32_t)w, hi = (uint32_t)(w >> 32);
+    uint32_t nzl = (lo | (lo >> 1)) & 0x55555555u, nzh = (hi | (hi >> 1)) & 0x55555555u;  // bit 2c: field c != 0
+    const uint32_t cnt = (uint32_t)(__popc(nzl) + __popc(nzh));
+    *over = cnt > 2;
+    if (cnt == 0) return 0;
+    if (cnt > 2) return (uint16_t)0xC000u;
+    auto code_of = [&](uint32_t c) { return c >= 16 ? (hi >> (2 * (c - 16))) & 3u : (lo >> (2 * c)) & 3u; };
+    const uint32_t c1 = top_field(nzl, nzh);
+    uint32_t r = c1 | (code_of(c1) << 5) | (cnt << 14);
+    if (cnt == 2) {
+        if (c1 >= 16) nzh &= ~(1u << (2 * (c1 - 16)));
+        else nzl &= ~(1u << (2 * c1));
+        const uint32_t c2 = top_field(nzl, nzh);
+        r |= (c2 << 7) | (code_of(c2) << 12);
+    }
+    return (uint16_t)r;
+}
+// The full word of amplitude k from its sparse entry r (ovf: the overflow words).
+template <class W>
+__device__ __forceinline__ W sparse_decode(uint16_t r, const unsigned long long* ovf, uint64_t k) {
+    const uint32_t cnt = (uint32_t)r >> 14;
+    if (cnt == 3) return (W)ovf[k];
+    W f = 0;
+    if (cnt >= 1) f |= (W)((r >> 5) & 3u) << (2 * (r & 31u));
+    if (cnt == 2) f |= (W)((r >> 12) & 3u) << (2 * ((r >> 7) & 31u));
+    return f;
+}
+bool noise_sparse_words() {
+    const char* e = std::getenv("QSIM_NOISE_SPARSE");  // (read per launch: tests switch it)
+    return e == nullptr || std::atoi(e) != 0;
+}
+// Byte offset of the overflow words behind the 16-bit entries of `amps` amplitudes.
+__host__ __device__ inline uint64_t sparse_ovf_offset(uint64_t amps) { return (amps * sizeof(uint16_t) + 255) & ~255ull; }
+
 // One block's walk: flips (local pair l in [0, 256) of block gb) handed to `f(l, code)`.
 template <class F>
 __device__ __forceinline__ void walk_block(uint64_t gb, const FlipChan& c, F&& f) {
@@ -1049,7 +1096,7 @@ __device__ __forceinline__ void map_task(const MapArgs& a, const FlipChan* chs, 
     });
 }
 
-template <class W>
+template <class W, bool SPARSE = false>
 __global__ __launch_bounds__(kWordThreads) void k_noise_words(MapArgs a) {
     __shared__ W w[1 << kRegionLogMax];
     __shared__ FlipChan chs[kMaxPullChannels];
@@ -1064,15 +1111,36 @@ __global__ __launch_bounds__(kWordThreads) void k_noise_words(MapArgs a) {
     if (!(a.skip & 1))
         for (int task = t; task < toff[a.nch]; task += kWordThreads) map_task(a, chs, toff, w, K0, task);
     __syncthreads();
-    W* out = static_cast<W*>(a.words) + K0;
-    if (!(a.skip & 2))
-        for (int i = t; i < R; i += kWordThreads) out[i] = w[i];
+    if constexpr (SPARSE) {
+        // four consecutive words per lane: one 8-byte store of their entries (R >= 512: n >= 9)
+        uint16_t* out = static_cast<uint16_t*>(a.words) + K0;
+        unsigned long long* ovf =
+            reinterpret_cast<unsigned long long*>(static_cast<char*>(a.words) + sparse_ovf_offset(a.amps)) + K0;
+        if (!(a.skip & 2))
+            for (int i = 4 * t; i < R; i += 4 * kWordThreads) {
+                uint16_t e[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const unsigned long long wj = (unsigned long long)w[i + j];
+                    bool over = false;
+                    e[j] = wj ? sparse_encode(wj, &over) : (uint16_t)0;
+                    if (over) ovf[i + j] = wj;
+                }
+                *reinterpret_cast<ushort4*>(out + i) = make_ushort4(e[0], e[1], e[2], e[3]);
+            }
+    } else {
+        W* out = static_cast<W*>(a.words) + K0;
+        if (!(a.skip & 2))
+            for (int i = t; i < R; i += kWordThreads) out[i] = w[i];
+    }
 }
 
 struct PullArgs {
     const double2* src;
     double2* dst;
     const void* words;
+    uint64_t amps;       // amplitudes of this object (where sparse words keep their overflow words)
+    int lockstep;        // walks of a thread's amplitudes in lockstep (pull_walks) or one by one
     uint64_t items;      // pairs (2x2 / diagonal) or amplitudes (SWAP / identity)
     int nch;
     int q[kMaxPullChannels];
@@ -1084,8 +1152,24 @@ struct PullArgs {
 
 // (P psi)[k] for a non-zero code word w of k: the fields from the highest down; a move (X / Y)
 // re-reads the word at the new index, restricted to the channels below the one that moved it.
+// The code word of amplitude k: dense (W per amplitude) or sparse (16-bit entries + overflow words).
+template <class W, bool SPARSE>
+struct WordSrc {
+    const W* w;
+    __device__ __forceinline__ W raw(uint64_t k) const { return w[k]; }
+    __device__ __forceinline__ W full(uint64_t, W r) const { return r; }
+    __device__ __forceinline__ W at(uint64_t k) const { return w[k]; }
+};
 template <class W>
-__device__ __forceinline__ double2 pull_walk(const PullArgs& a, const int* sq, const W* words, uint64_t k, W w,
+struct WordSrc<W, true> {
+    const uint16_t* w;
+    const unsigned long long* ovf;
+    __device__ __forceinline__ uint16_t raw(uint64_t k) const { return w[k]; }
+    __device__ __forceinline__ W full(uint64_t k, uint16_t r) const { return sparse_decode<W>(r, ovf, k); }
+    __device__ __forceinline__ W at(uint64_t k) const { return sparse_decode<W>(w[k], ovf, k); }
+};
+template <class W, class WS>
+__device__ __forceinline__ double2 pull_walk(const PullArgs& a, const int* sq, const WS& words, uint64_t k, W w,
                                              double2 v) {
     int e = 0;  // phase i^e
     bool moved = false;
@@ -1105,7 +1189,7 @@ __device__ __forceinline__ double2 pull_walk(const PullArgs& a, const int* sq, c
         if (code == 2) e += bit ? 1 : 3;  // Y: |0> <- -i v[k1], |1> <- +i v[k0]
         k ^= 1ull << q;                  // X / Y: the partner's amplitude
         moved = true;
-        w = words[k];
+        w = words.at(k);
     }
     if (moved) v = a.src[k];
     switch (e & 3) {
@@ -1113,6 +1197,76 @@ __device__ __forceinline__ double2 pull_walk(const PullArgs& a, const int* sq, c
         case 2: return make_double2(-v.x, -v.y);
         case 3: return make_double2(v.y, -v.x);
         default: return v;
+    }
+}
+
+// The walks of one thread's S amplitudes in lockstep (QSIM_PULL_LOCKSTEP, default 1): each round
+// advances every unfinished walk to its next X / Y field (Z fields add their phase without a
+// load), then issues the word loads of all walks that moved, together; the moved amplitudes are
+// loaded together at the end.  The per-item walk (pull_walk) serialises the dependent random loads
+// of a thread's walks one after another — at 26 channels most threads hold a non-zero word.
+// Same result as pull_walk per amplitude (the same fields in the same order).
+template <int S, class W, class WS>
+__device__ __forceinline__ void pull_walks(const PullArgs& a, const int* sq, const WS& words, const uint64_t (&k0)[S],
+                                           W (&w)[S], double2 (&v)[S], int nvalid) {
+    uint64_t k[S];
+    int e[S], hi[S];
+    bool mv[S];
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+        k[s] = k0[s];
+        e[s] = 0;
+        hi[s] = a.nch;
+        mv[s] = false;
+        if (s >= nvalid) w[s] = 0;
+    }
+    for (;;) {
+        bool need[S], any = false;
+#pragma unroll
+        for (int s = 0; s < S; ++s) {
+            need[s] = false;
+            // apply fields from the top until an X / Y moves the index (or none is left)
+            while (w[s]) {
+                const W m = hi[s] >= (int)(4 * sizeof(W)) ? w[s] : (w[s] & (((W)1 << (2 * hi[s])) - 1));
+                if (!m) {
+                    w[s] = 0;
+                    break;
+                }
+                const int c =
+                    (int)(8 * sizeof(W) - 1 - (sizeof(W) == 8 ? __clzll((long long)m) : __clz((int)m))) >> 1;
+                const int code = (int)((w[s] >> (2 * c)) & 3);
+                const int q = sq[c];
+                const int bit = (int)((k[s] >> q) & 1ull);
+                hi[s] = c;
+                if (code == 3) {  // Z: |1> <- -v[k1] (the index stays)
+                    if (bit) e[s] += 2;
+                    continue;
+                }
+                if (code == 2) e[s] += bit ? 1 : 3;  // Y: |0> <- -i v[k1], |1> <- +i v[k0]
+                k[s] ^= 1ull << q;                   // X / Y: the partner's amplitude
+                mv[s] = true;
+                need[s] = true;
+                any = true;
+                break;
+            }
+        }
+        if (!any) break;
+#pragma unroll
+        for (int s = 0; s < S; ++s)
+            if (need[s]) w[s] = words.at(k[s]);
+    }
+#pragma unroll
+    for (int s = 0; s < S; ++s)
+        if (mv[s]) v[s] = a.src[k[s]];
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+        const double2 x = v[s];
+        switch (e[s] & 3) {
+            case 1: v[s] = make_double2(-x.y, x.x); break;
+            case 2: v[s] = make_double2(-x.x, -x.y); break;
+            case 3: v[s] = make_double2(x.y, -x.x); break;
+            default: break;
+        }
     }
 }
 
@@ -1133,7 +1287,7 @@ template <class W>
 struct PullMapLds<W, false> {
     W w[1];
 };
-template <class W, bool PAIR, int kPullU, bool NT, bool MAP = false>
+template <class W, bool PAIR, int kPullU, bool NT, bool MAP = false, bool SPARSE = false>
 __global__ __launch_bounds__(256) void k_pull_gate(PullArgs a, MapArgs m) {
     __shared__ int sq[kMaxPullChannels];
     __shared__ PullMapLds<W, MAP> lds;
@@ -1162,7 +1316,15 @@ __global__ __launch_bounds__(256) void k_pull_gate(PullArgs a, MapArgs m) {
             for (int i = threadIdx.x; i < (m.rpw << m.rl); i += 256) out[i] = lds.w[i];
         }
     };
-    const W* words = static_cast<const W*>(a.words);
+    using Raw = std::conditional_t<SPARSE, uint16_t, W>;
+    WordSrc<W, SPARSE> words;
+    if constexpr (SPARSE) {
+        words.w = static_cast<const uint16_t*>(a.words);
+        words.ovf = reinterpret_cast<const unsigned long long*>(static_cast<const char*>(a.words) +
+                                                                sparse_ovf_offset(a.amps));
+    } else {
+        words.w = static_cast<const W*>(a.words);
+    }
     const uint64_t base = ((uint64_t)blockIdx.x * kPullU) << 8;
     // items is a multiple of 256, so each item group u (256 consecutive items) is wholly in or
     // wholly out of range for the whole work-group; groups past the end do nothing (a 9- or
@@ -1174,7 +1336,7 @@ __global__ __launch_bounds__(256) void k_pull_gate(PullArgs a, MapArgs m) {
     }
     if constexpr (PAIR) {
         uint64_t j0[kPullU];
-        W w0[kPullU], w1[kPullU];
+        Raw w0[kPullU], w1[kPullU];
         double2 x0[kPullU], x1[kPullU];
 #pragma unroll
         for (int u = 0; u < kPullU; ++u) {
@@ -1183,24 +1345,49 @@ __global__ __launch_bounds__(256) void k_pull_gate(PullArgs a, MapArgs m) {
             const uint64_t lo = i & ((1ull << a.t0) - 1ull);
             j0[u] = ((i ^ lo) << 1) | lo;
             const uint64_t j1 = j0[u] | (1ull << a.t0);
-            w0[u] = words[j0[u]];
-            w1[u] = words[j1];
+            w0[u] = words.raw(j0[u]);
+            w1[u] = words.raw(j1);
             x0[u] = ld<NT>(a.src + j0[u]);
             x1[u] = ld<NT>(a.src + j1);
         }
         build_map();
+        if (a.lockstep) {  // both members of every pair: 2U walks in lockstep
+            uint64_t ks[2 * kPullU];
+            W ws[2 * kPullU];
+            double2 vs[2 * kPullU];
+#pragma unroll
+            for (int u = 0; u < kPullU; ++u) {
+                ks[2 * u] = j0[u];
+                ks[2 * u + 1] = j0[u] | (1ull << a.t0);
+                ws[2 * u] = u < nu && w0[u] ? words.full(ks[2 * u], w0[u]) : (W)0;
+                ws[2 * u + 1] = u < nu && w1[u] ? words.full(ks[2 * u + 1], w1[u]) : (W)0;
+                vs[2 * u] = x0[u];
+                vs[2 * u + 1] = x1[u];
+            }
+            pull_walks<2 * kPullU>(a, sq, words, ks, ws, vs, 2 * nu);
+#pragma unroll
+            for (int u = 0; u < kPullU; ++u) {
+                x0[u] = vs[2 * u];
+                x1[u] = vs[2 * u + 1];
+            }
+        }
 #pragma unroll
         for (int u = 0; u < kPullU; ++u) {
             if (u >= nu) break;
-            if (w0[u]) x0[u] = pull_walk(a, sq, words, j0[u], w0[u], x0[u]);
-            if (w1[u]) x1[u] = pull_walk(a, sq, words, j0[u] | (1ull << a.t0), w1[u], x1[u]);
+            if (!a.lockstep) {
+                if (w0[u]) x0[u] = pull_walk<W>(a, sq, words, j0[u], words.full(j0[u], w0[u]), x0[u]);
+                if (w1[u]) {
+                    const uint64_t j1 = j0[u] | (1ull << a.t0);
+                    x1[u] = pull_walk<W>(a, sq, words, j1, words.full(j1, w1[u]), x1[u]);
+                }
+            }
             if ((j0[u] & a.cmask) == a.cmask) m1_pair(a.sub, a.m[0], a.m[1], a.m[2], a.m[3], x0[u], x1[u]);
             st<NT>(a.dst + j0[u], x0[u]);
             st<NT>(a.dst + (j0[u] | (1ull << a.t0)), x1[u]);
         }
     } else {
         uint64_t sk[kPullU];
-        W w[kPullU];
+        Raw w[kPullU];
         double2 x[kPullU];
 #pragma unroll
         for (int u = 0; u < kPullU; ++u) {
@@ -1212,15 +1399,21 @@ __global__ __launch_bounds__(256) void k_pull_gate(PullArgs a, MapArgs m) {
                 if (b0 != b1) s = k ^ ((1ull << a.t0) | (1ull << a.t1));
             }
             sk[u] = s;
-            w[u] = words[s];
+            w[u] = words.raw(s);
             x[u] = ld<NT>(a.src + s);
         }
         build_map();
+        if (a.lockstep) {
+            W ws[kPullU];
+#pragma unroll
+            for (int u = 0; u < kPullU; ++u) ws[u] = u < nu && w[u] ? words.full(sk[u], w[u]) : (W)0;
+            pull_walks<kPullU>(a, sq, words, sk, ws, x, nu);
+        }
 #pragma unroll
         for (int u = 0; u < kPullU; ++u) {
             if (u >= nu) break;
             const uint64_t k = base + ((uint64_t)u << 8) + threadIdx.x;
-            if (w[u]) x[u] = pull_walk(a, sq, words, sk[u], w[u], x[u]);
+            if (!a.lockstep && w[u]) x[u] = pull_walk<W>(a, sq, words, sk[u], words.full(sk[u], w[u]), x[u]);
             double2 y = x[u];
             const bool on = (k & a.cmask) == a.cmask;
             const int bit = (int)((k >> a.t0) & 1ull);
@@ -1251,7 +1444,10 @@ bool pull_noise_supported(int n, const std::vector<NoiseChan>& chans, bool defau
 
 // Bytes of one step's code words: 4 per amplitude up to 16 channel entries, else 8.
 size_t pull_noise_codes_bytes(int n, uint64_t batch, size_t nch) {
-    return (batch << n) * (nch <= 16 ? sizeof(uint32_t) : sizeof(uint64_t));
+    const uint64_t amps = batch << n;
+    const size_t dense = amps * (nch <= 16 ? sizeof(uint32_t) : sizeof(uint64_t));
+    const size_t sparse = sparse_ovf_offset(amps) + amps * sizeof(unsigned long long);
+    return std::max(dense, sparse);  // (either layout fits: QSIM_NOISE_SPARSE may change between runs)
 }
 
 // The live (can-fire) channels of one noise step, keyed like the push kernels' passes.
@@ -1284,7 +1480,8 @@ void launch_noise_map(int n, uint64_t batch, uint64_t traj0, const std::vector<N
     pull_channels(n, chans, seed, counter0, m, a);
     const char* ske = std::getenv("QSIM_MAP_SKIP");
     m.skip = ske ? std::atoi(ske) : 0;
-    const size_t wb = chans.size() <= 16 ? sizeof(uint32_t) : sizeof(uint64_t);
+    const bool sparse = noise_sparse_words();
+    const size_t wb = sparse ? sizeof(uint16_t) : chans.size() <= 16 ? sizeof(uint32_t) : sizeof(uint64_t);
     if (!m.nch) {  // no channel can fire: every word zero
         QSIM_HIPCHK(hipMemsetAsync(words, 0, amps * wb, s));
         return;
@@ -1296,8 +1493,14 @@ void launch_noise_map(int n, uint64_t batch, uint64_t traj0, const std::vector<N
     // (256-thread work-groups: one round of 320 threads for the 320 walks of a 26-qubit region
     // shortens the map alone, 0.240 -> 0.218 ms, but the overlapped step loses: 1 112 -> 1 067
     // gates/s, profiles/r05/fast_log/)
-    if (wb == sizeof(uint32_t)) hipLaunchKernelGGL(k_noise_words<uint32_t>, grid, dim3(kWordThreads), 0, s, m);
-    else hipLaunchKernelGGL(k_noise_words<unsigned long long>, grid, dim3(kWordThreads), 0, s, m);
+    if (sparse) {
+        if (chans.size() <= 16) hipLaunchKernelGGL((k_noise_words<uint32_t, true>), grid, dim3(kWordThreads), 0, s, m);
+        else hipLaunchKernelGGL((k_noise_words<unsigned long long, true>), grid, dim3(kWordThreads), 0, s, m);
+    } else if (wb == sizeof(uint32_t)) {
+        hipLaunchKernelGGL(k_noise_words<uint32_t>, grid, dim3(kWordThreads), 0, s, m);
+    } else {
+        hipLaunchKernelGGL(k_noise_words<unsigned long long>, grid, dim3(kWordThreads), 0, s, m);
+    }
     QSIM_HIPCHK(hipGetLastError());
 }
 
@@ -1326,6 +1529,11 @@ void launch_pull_gate(const double2* src, double2* dst, int n, uint64_t batch, c
     a.src = src;
     a.dst = dst;
     a.words = words;
+    a.amps = amps;
+    {
+        const char* le = std::getenv("QSIM_PULL_LOCKSTEP");  // (read per launch: measurements)
+        a.lockstep = le == nullptr || std::atoi(le) != 0;
+    }
     a.kind = op ? op->kind : -1;
     if (op) {
         a.sub = op->sub;
@@ -1343,11 +1551,16 @@ void launch_pull_gate(const double2* src, double2* dst, int n, uint64_t batch, c
     // traffic, default 1): read per launch (measurement sweeps)
     const char* ue = std::getenv("QSIM_PULL_U");
     const char* ne = std::getenv("QSIM_PULL_NT");
-    const int U = ue ? std::atoi(ue) : 4;
-    const bool nt = ne == nullptr || std::atoi(ne) != 0;
+    const bool sparse = noise_sparse_words();  // (sparse words: the defaults, 4 items, non-temporal)
+    const int U = ue && !sparse ? std::atoi(ue) : 4;
+    const bool nt = sparse || ne == nullptr || std::atoi(ne) != 0;
     const int Uc = U <= 2 ? 2 : (U >= 8 ? 8 : 4);
     const dim3 grid((unsigned)((a.items + 256 * Uc - 1) / (256 * Uc)));
     const bool w32 = chans.size() <= 16;
+    if (fuse && sparse) {  // (the fused map writes dense words: build them apart instead)
+        fuse = false;
+        launch_noise_map(n, batch, next->traj0, chans, next->seed, next->counter0, next->words, s, tm);
+    }
     if (fuse) {  // the fused form: 4 items per thread, non-temporal, 1 or 2 whole regions per group
         const uint64_t regions = amps >> nm.rl;
         nm.rpw = (int)(regions / grid.x);
@@ -1379,7 +1592,17 @@ void launch_pull_gate(const double2* src, double2* dst, int n, uint64_t batch, c
         else if (Uc == 8) QSIM_PULL_LAUNCH(W_, 8, NTT); \
         else QSIM_PULL_LAUNCH(W_, 4, NTT);         \
     } while (0)
-    if (w32) {
+    if (sparse) {  // (4 items per thread, non-temporal amplitude traffic: the defaults)
+        if (w32) {
+            if (pair) hipLaunchKernelGGL((k_pull_gate<uint32_t, true, 4, true, false, true>), grid, dim3(256), 0, s, a, m);
+            else hipLaunchKernelGGL((k_pull_gate<uint32_t, false, 4, true, false, true>), grid, dim3(256), 0, s, a, m);
+        } else {
+            if (pair)
+                hipLaunchKernelGGL((k_pull_gate<unsigned long long, true, 4, true, false, true>), grid, dim3(256), 0, s, a, m);
+            else
+                hipLaunchKernelGGL((k_pull_gate<unsigned long long, false, 4, true, false, true>), grid, dim3(256), 0, s, a, m);
+        }
+    } else if (w32) {
         if (nt) QSIM_PULL_LAUNCH_U(uint32_t, true);
         else QSIM_PULL_LAUNCH_U(uint32_t, false);
     } else {

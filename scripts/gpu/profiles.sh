@@ -41,6 +41,8 @@ for rg in $REGIONS; do
     batch16ref) prof batch16ref --steps 3 --warmup 1 --no-1q28 --no-extras || exit 1 ;;
     noisy26) prof noisy26 --workload noisy --steps 3 || exit 1 ;;
     dm14) prof dm14 --workload dm --steps 5 || exit 1 ;;
+    pmcnoisy)
+      run_pmc noisy_26q python3 $R/bench.py --workload noisy --cpu-budget 0 --steps 2 --warmup 1 || exit 1 ;;
     pmcbatch)
       ( export QSIM_NOISE_SPLIT=1; run_pmc batch_ref_16q python3 $R/bench.py --workload batch --cpu-budget 0 --steps 2 --warmup 1 ) || exit 1 ;;
     pmc)

@@ -27,8 +27,10 @@ LABELS = [("k_fused_staged", "fused_tile"), ("k_fused_tile", "fused_tile"),
 
 
 def label_of(name):
-    if "k_pull_gate<" in name and name.split("(")[0].replace(" ", "").endswith(",true>"):
-        return "pull_gate_map"  # (the word map fused in: k_pull_gate<W, PAIR, U, NT, MAP = true>)
+    if "k_pull_gate<" in name:
+        # k_pull_gate<W, PAIR, U, NT, MAP[, SPARSE]>: MAP = true is the word map fused in
+        args = name.split("(")[0].split("<", 1)[1].rstrip(">").replace(" ", "").split(",")
+        return "pull_gate_map" if len(args) >= 5 and args[4] == "true" else "pull_gate"
     for key, lab in LABELS:
         if key in name:
             return lab

@@ -35,8 +35,9 @@ ENGINE_NAMES = {
     "noise_units": r".*k_noise_units.*",
     "noise": r".*k_noise_(units|flips).*",
     "gate_noise": r".*k_gate_noise_tile.*",
-    "pull_gate": r".*k_pull_gate.*",
-    "pull_gate_map": r".*k_pull_gate<.*, *true>\(.*",
+    # k_pull_gate<W, PAIR, U, NT, MAP[, SPARSE]>: the fifth argument says whether the map is fused in
+    "pull_gate": r".*k_pull_gate<[^,]+, *[a-z]+, *\d+, *[a-z]+(, *false(, *[a-z]+)?)?>\(.*",
+    "pull_gate_map": r".*k_pull_gate<[^,]+, *[a-z]+, *\d+, *[a-z]+, *true(, *[a-z]+)?>\(.*",
     "noise_map": r".*k_noise_words.*",
     "fused_tile": r"^(qk\d+|.*k_fused_(staged|tile).*)",
 }
