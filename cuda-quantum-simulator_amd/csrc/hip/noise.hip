@@ -1007,25 +1007,18 @@ struct MapArgs {
 // the entry count — and a word with three or more non-zero fields as count 3, its full 64-bit
 // word at ovf[k] (a second array of the same index space, touched only at those amplitudes).  The
 // pull pass then streams 2 B of words per amplitude instead of 8 (26 channels) or 4 (<= 16).
-// (32-bit halves throughout: the map encodes every word of the state once per step)
-__device__ __forceinline__ uint32_t top_field(uint32_t nzl, uint32_t nzh) {  // highest non-zero field
-    return nzh ? 16u + ((31u - (uint32_t)__clz((int)nzh)) >> 1) : (31u - (uint32_t)__clz((int)nzl)) >> 1;
-}
 __device__ __forceinline__ uint16_t sparse_encode(unsigned long long w, bool* over) {
-    const uint32_t lo = (uint32_t)w, hi = (uint32_t)(w >> 32);
-    uint32_t nzl = (lo | (lo >> 1)) & 0x55555555u, nzh = (hi | (hi >> 1)) & 0x55555555u;  // bit 2c: field c != 0
-    const uint32_t cnt = (uint32_t)(__popc(nzl) + __popc(nzh));
+    const unsigned long long nz = (w | (w >> 1)) & 0x5555555555555555ull;  // bit 2c: field c != 0
+    const int cnt = __popcll(nz);
     *over = cnt > 2;
     if (cnt == 0) return 0;
     if (cnt > 2) return (uint16_t)0xC000u;
-    auto code_of = [&](uint32_t c) { return c >= 16 ? (hi >> (2 * (c - 16))) & 3u : (lo >> (2 * c)) & 3u; };
-    const uint32_t c1 = top_field(nzl, nzh);
-    uint32_t r = c1 | (code_of(c1) << 5) | (cnt << 14);
+    const int c1 = (63 - __clzll((long long)nz)) >> 1;
+    uint32_t r = (uint32_t)c1 | ((uint32_t)((w >> (2 * c1)) & 3ull) << 5) | ((uint32_t)cnt << 14);
     if (cnt == 2) {
-        if (c1 >= 16) nzh &= ~(1u << (2 * (c1 - 16)));
-        else nzl &= ~(1u << (2 * c1));
-        const uint32_t c2 = top_field(nzl, nzh);
-        r |= (c2 << 7) | (code_of(c2) << 12);
+        const unsigned long long rest = nz & ~(1ull << (2 * c1));
+        const int c2 = (63 - __clzll((long long)rest)) >> 1;
+        r |= ((uint32_t)c2 << 7) | ((uint32_t)((w >> (2 * c2)) & 3ull) << 12);
     }
     return (uint16_t)r;
 }
@@ -1112,21 +1105,17 @@ __global__ __launch_bounds__(kWordThreads) void k_noise_words(MapArgs a) {
         for (int task = t; task < toff[a.nch]; task += kWordThreads) map_task(a, chs, toff, w, K0, task);
     __syncthreads();
     if constexpr (SPARSE) {
-        // four consecutive words per lane: one 8-byte store of their entries (R >= 512: n >= 9)
+        // (measured and not kept, 26 qubits / 26 channels: the encode in 32-bit halves 0.266 ms,
+        // four words per lane with one 8-byte store 0.267, zeros first and then only the touched
+        // words from an LDS list 0.307 (its one append counter serialises) — against 0.247 ms)
         uint16_t* out = static_cast<uint16_t*>(a.words) + K0;
         unsigned long long* ovf =
             reinterpret_cast<unsigned long long*>(static_cast<char*>(a.words) + sparse_ovf_offset(a.amps)) + K0;
         if (!(a.skip & 2))
-            for (int i = 4 * t; i < R; i += 4 * kWordThreads) {
-                uint16_t e[4];
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const unsigned long long wj = (unsigned long long)w[i + j];
-                    bool over = false;
-                    e[j] = wj ? sparse_encode(wj, &over) : (uint16_t)0;
-                    if (over) ovf[i + j] = wj;
-                }
-                *reinterpret_cast<ushort4*>(out + i) = make_ushort4(e[0], e[1], e[2], e[3]);
+            for (int i = t; i < R; i += kWordThreads) {
+                bool over = false;
+                out[i] = sparse_encode((unsigned long long)w[i], &over);
+                if (over) ovf[i] = (unsigned long long)w[i];
             }
     } else {
         W* out = static_cast<W*>(a.words) + K0;
@@ -1140,7 +1129,6 @@ struct PullArgs {
     double2* dst;
     const void* words;
     uint64_t amps;       // amplitudes of this object (where sparse words keep their overflow words)
-    int lockstep;        // walks of a thread's amplitudes in lockstep (pull_walks) or one by one
     uint64_t items;      // pairs (2x2 / diagonal) or amplitudes (SWAP / identity)
     int nch;
     int q[kMaxPullChannels];
@@ -1197,76 +1185,6 @@ __device__ __forceinline__ double2 pull_walk(const PullArgs& a, const int* sq, c
         case 2: return make_double2(-v.x, -v.y);
         case 3: return make_double2(v.y, -v.x);
         default: return v;
-    }
-}
-
-// The walks of one thread's S amplitudes in lockstep (QSIM_PULL_LOCKSTEP, default 1): each round
-// advances every unfinished walk to its next X / Y field (Z fields add their phase without a
-// load), then issues the word loads of all walks that moved, together; the moved amplitudes are
-// loaded together at the end.  The per-item walk (pull_walk) serialises the dependent random loads
-// of a thread's walks one after another — at 26 channels most threads hold a non-zero word.
-// Same result as pull_walk per amplitude (the same fields in the same order).
-template <int S, class W, class WS>
-__device__ __forceinline__ void pull_walks(const PullArgs& a, const int* sq, const WS& words, const uint64_t (&k0)[S],
-                                           W (&w)[S], double2 (&v)[S], int nvalid) {
-    uint64_t k[S];
-    int e[S], hi[S];
-    bool mv[S];
-#pragma unroll
-    for (int s = 0; s < S; ++s) {
-        k[s] = k0[s];
-        e[s] = 0;
-        hi[s] = a.nch;
-        mv[s] = false;
-        if (s >= nvalid) w[s] = 0;
-    }
-    for (;;) {
-        bool need[S], any = false;
-#pragma unroll
-        for (int s = 0; s < S; ++s) {
-            need[s] = false;
-            // apply fields from the top until an X / Y moves the index (or none is left)
-            while (w[s]) {
-                const W m = hi[s] >= (int)(4 * sizeof(W)) ? w[s] : (w[s] & (((W)1 << (2 * hi[s])) - 1));
-                if (!m) {
-                    w[s] = 0;
-                    break;
-                }
-                const int c =
-                    (int)(8 * sizeof(W) - 1 - (sizeof(W) == 8 ? __clzll((long long)m) : __clz((int)m))) >> 1;
-                const int code = (int)((w[s] >> (2 * c)) & 3);
-                const int q = sq[c];
-                const int bit = (int)((k[s] >> q) & 1ull);
-                hi[s] = c;
-                if (code == 3) {  // Z: |1> <- -v[k1] (the index stays)
-                    if (bit) e[s] += 2;
-                    continue;
-                }
-                if (code == 2) e[s] += bit ? 1 : 3;  // Y: |0> <- -i v[k1], |1> <- +i v[k0]
-                k[s] ^= 1ull << q;                   // X / Y: the partner's amplitude
-                mv[s] = true;
-                need[s] = true;
-                any = true;
-                break;
-            }
-        }
-        if (!any) break;
-#pragma unroll
-        for (int s = 0; s < S; ++s)
-            if (need[s]) w[s] = words.at(k[s]);
-    }
-#pragma unroll
-    for (int s = 0; s < S; ++s)
-        if (mv[s]) v[s] = a.src[k[s]];
-#pragma unroll
-    for (int s = 0; s < S; ++s) {
-        const double2 x = v[s];
-        switch (e[s] & 3) {
-            case 1: v[s] = make_double2(-x.y, x.x); break;
-            case 2: v[s] = make_double2(-x.x, -x.y); break;
-            case 3: v[s] = make_double2(x.y, -x.x); break;
-            default: break;
-        }
     }
 }
 
@@ -1351,35 +1269,13 @@ __global__ __launch_bounds__(256) void k_pull_gate(PullArgs a, MapArgs m) {
             x1[u] = ld<NT>(a.src + j1);
         }
         build_map();
-        if (a.lockstep) {  // both members of every pair: 2U walks in lockstep
-            uint64_t ks[2 * kPullU];
-            W ws[2 * kPullU];
-            double2 vs[2 * kPullU];
-#pragma unroll
-            for (int u = 0; u < kPullU; ++u) {
-                ks[2 * u] = j0[u];
-                ks[2 * u + 1] = j0[u] | (1ull << a.t0);
-                ws[2 * u] = u < nu && w0[u] ? words.full(ks[2 * u], w0[u]) : (W)0;
-                ws[2 * u + 1] = u < nu && w1[u] ? words.full(ks[2 * u + 1], w1[u]) : (W)0;
-                vs[2 * u] = x0[u];
-                vs[2 * u + 1] = x1[u];
-            }
-            pull_walks<2 * kPullU>(a, sq, words, ks, ws, vs, 2 * nu);
-#pragma unroll
-            for (int u = 0; u < kPullU; ++u) {
-                x0[u] = vs[2 * u];
-                x1[u] = vs[2 * u + 1];
-            }
-        }
 #pragma unroll
         for (int u = 0; u < kPullU; ++u) {
             if (u >= nu) break;
-            if (!a.lockstep) {
-                if (w0[u]) x0[u] = pull_walk<W>(a, sq, words, j0[u], words.full(j0[u], w0[u]), x0[u]);
-                if (w1[u]) {
-                    const uint64_t j1 = j0[u] | (1ull << a.t0);
-                    x1[u] = pull_walk<W>(a, sq, words, j1, words.full(j1, w1[u]), x1[u]);
-                }
+            if (w0[u]) x0[u] = pull_walk<W>(a, sq, words, j0[u], words.full(j0[u], w0[u]), x0[u]);
+            if (w1[u]) {
+                const uint64_t j1 = j0[u] | (1ull << a.t0);
+                x1[u] = pull_walk<W>(a, sq, words, j1, words.full(j1, w1[u]), x1[u]);
             }
             if ((j0[u] & a.cmask) == a.cmask) m1_pair(a.sub, a.m[0], a.m[1], a.m[2], a.m[3], x0[u], x1[u]);
             st<NT>(a.dst + j0[u], x0[u]);
@@ -1403,17 +1299,11 @@ __global__ __launch_bounds__(256) void k_pull_gate(PullArgs a, MapArgs m) {
             x[u] = ld<NT>(a.src + s);
         }
         build_map();
-        if (a.lockstep) {
-            W ws[kPullU];
-#pragma unroll
-            for (int u = 0; u < kPullU; ++u) ws[u] = u < nu && w[u] ? words.full(sk[u], w[u]) : (W)0;
-            pull_walks<kPullU>(a, sq, words, sk, ws, x, nu);
-        }
 #pragma unroll
         for (int u = 0; u < kPullU; ++u) {
             if (u >= nu) break;
             const uint64_t k = base + ((uint64_t)u << 8) + threadIdx.x;
-            if (!a.lockstep && w[u]) x[u] = pull_walk<W>(a, sq, words, sk[u], words.full(sk[u], w[u]), x[u]);
+            if (w[u]) x[u] = pull_walk<W>(a, sq, words, sk[u], words.full(sk[u], w[u]), x[u]);
             double2 y = x[u];
             const bool on = (k & a.cmask) == a.cmask;
             const int bit = (int)((k >> a.t0) & 1ull);
@@ -1530,10 +1420,6 @@ void launch_pull_gate(const double2* src, double2* dst, int n, uint64_t batch, c
     a.dst = dst;
     a.words = words;
     a.amps = amps;
-    {
-        const char* le = std::getenv("QSIM_PULL_LOCKSTEP");  // (read per launch: measurements)
-        a.lockstep = le == nullptr || std::atoi(le) != 0;
-    }
     a.kind = op ? op->kind : -1;
     if (op) {
         a.sub = op->sub;
