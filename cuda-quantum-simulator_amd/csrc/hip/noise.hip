@@ -1366,7 +1366,11 @@ void launch_noise_map(int n, uint64_t batch, uint64_t traj0, const std::vector<N
     m.amps = amps;
     m.idx0 = traj0 << (n - 1);
     m.n = n;
-    m.rl = std::min(n, kRegionLogMax);
+    {  // QSIM_NOISE_REGION_LOG (9..12, default 12): amplitudes per word-map work-group (measurements)
+        const char* re = std::getenv("QSIM_NOISE_REGION_LOG");
+        const int rl = re ? std::max(9, std::min(kRegionLogMax, std::atoi(re))) : kRegionLogMax;
+        m.rl = std::min(n, rl);
+    }
     pull_channels(n, chans, seed, counter0, m, a);
     const char* ske = std::getenv("QSIM_MAP_SKIP");
     m.skip = ske ? std::atoi(ske) : 0;
@@ -1433,14 +1437,17 @@ void launch_pull_gate(const double2* src, double2* dst, int n, uint64_t batch, c
     a.items = pair ? pairs : amps;  // (multiples of 256: n >= 9)
     if (n < kMinPullQubits || a.items % 256 != 0) fail(QSIM_ERR_RUNTIME, "pulled noise pass: bad shape");
     if (!pair && a.kind == K_M1 && a.t0 >= 6) fail(QSIM_ERR_RUNTIME, "pulled noise pass: lane partner");
-    // QSIM_PULL_U (items per thread, 2 / 4 / 8, default 4), QSIM_PULL_NT (non-temporal amplitude
+    // QSIM_PULL_U (items per thread, 1 / 2 / 4 / 8), QSIM_PULL_NT (non-temporal amplitude
     // traffic, default 1): read per launch (measurement sweeps)
     const char* ue = std::getenv("QSIM_PULL_U");
     const char* ne = std::getenv("QSIM_PULL_NT");
-    const bool sparse = noise_sparse_words();  // (sparse words: the defaults, 4 items, non-temporal)
-    const int U = ue && !sparse ? std::atoi(ue) : 4;
-    const bool nt = sparse || ne == nullptr || std::atoi(ne) != 0;
-    const int Uc = U <= 2 ? 2 : (U >= 8 ? 8 : 4);
+    const bool sparse = noise_sparse_words();
+    // (sparse words: 2 items per thread by default — NoisySimulator 26q / 26 channels 1 169 -> 1 257
+    // gates/s: twice the work-groups interleave better with the next step's word map on the
+    // other stream; 8 items 956; dense words keep 4)
+    const int U = ue ? std::atoi(ue) : (sparse ? 2 : 4);
+    const bool nt = ne == nullptr || std::atoi(ne) != 0;
+    const int Uc = U <= 1 ? 1 : U == 2 ? 2 : (U >= 8 ? 8 : 4);
     const dim3 grid((unsigned)((a.items + 256 * Uc - 1) / (256 * Uc)));
     const bool w32 = chans.size() <= 16;
     if (fuse && sparse) {  // (the fused map writes dense words: build them apart instead)
@@ -1469,26 +1476,19 @@ void launch_pull_gate(const double2* src, double2* dst, int n, uint64_t batch, c
     }
 #define QSIM_PULL_LAUNCH(W_, UU, NTT)                                                                      \
     do {                                                                                                 \
-        if (pair) hipLaunchKernelGGL((k_pull_gate<W_, true, UU, NTT>), grid, dim3(256), 0, s, a, m);    \
+        if (sparse && pair) hipLaunchKernelGGL((k_pull_gate<W_, true, UU, NTT, false, true>), grid, dim3(256), 0, s, a, m); \
+        else if (sparse) hipLaunchKernelGGL((k_pull_gate<W_, false, UU, NTT, false, true>), grid, dim3(256), 0, s, a, m); \
+        else if (pair) hipLaunchKernelGGL((k_pull_gate<W_, true, UU, NTT>), grid, dim3(256), 0, s, a, m); \
         else hipLaunchKernelGGL((k_pull_gate<W_, false, UU, NTT>), grid, dim3(256), 0, s, a, m);        \
     } while (0)
 #define QSIM_PULL_LAUNCH_U(W_, NTT)                  \
     do {                                           \
-        if (Uc == 2) QSIM_PULL_LAUNCH(W_, 2, NTT);  \
+        if (Uc == 1) QSIM_PULL_LAUNCH(W_, 1, NTT);  \
+        else if (Uc == 2) QSIM_PULL_LAUNCH(W_, 2, NTT);  \
         else if (Uc == 8) QSIM_PULL_LAUNCH(W_, 8, NTT); \
         else QSIM_PULL_LAUNCH(W_, 4, NTT);         \
     } while (0)
-    if (sparse) {  // (4 items per thread, non-temporal amplitude traffic: the defaults)
-        if (w32) {
-            if (pair) hipLaunchKernelGGL((k_pull_gate<uint32_t, true, 4, true, false, true>), grid, dim3(256), 0, s, a, m);
-            else hipLaunchKernelGGL((k_pull_gate<uint32_t, false, 4, true, false, true>), grid, dim3(256), 0, s, a, m);
-        } else {
-            if (pair)
-                hipLaunchKernelGGL((k_pull_gate<unsigned long long, true, 4, true, false, true>), grid, dim3(256), 0, s, a, m);
-            else
-                hipLaunchKernelGGL((k_pull_gate<unsigned long long, false, 4, true, false, true>), grid, dim3(256), 0, s, a, m);
-        }
-    } else if (w32) {
+    if (w32) {
         if (nt) QSIM_PULL_LAUNCH_U(uint32_t, true);
         else QSIM_PULL_LAUNCH_U(uint32_t, false);
     } else {
