@@ -34,6 +34,10 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "cuda-quantum-simulator_amd"))
 resource.setrlimit(resource.RLIMIT_CORE, (0, 0))  # an abort fails fast, no core dump
+# Every measurement below is a cold one: no kernels or layout decisions from an on-disk cache of
+# earlier processes (csrc/hip/cache.hip).  The `first_run_cache` object measures that cache on its
+# own, in child processes with a private cache directory.
+os.environ.setdefault("QSIM_CACHE", "0")
 
 METRIC = "gates/s + achieved HBM GB/s (% peak), 100-gate H+CNOT circuit @ n qubits"
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
@@ -102,7 +106,7 @@ def parse():
     p.add_argument("--no-extras", action="store_true",
                    help="skip the default line's extra objects (seeds, default_mode, w_ref, "
                         "gate_table_20q, dm_14q, noisy_26q)")
-    p.add_argument("--extras", default="seeds,default_mode,w_ref,w_hc_28q,h_single,gate_table,dm,noisy",
+    p.add_argument("--extras", default="seeds,default_mode,w_ref,w_hc_28q,first_run_cache,h_single,gate_table,dm,noisy",
                    help="which extra objects of the default W-HC line to measure (comma list; "
                         "--no-extras: none)")
     p.add_argument("--noise", type=float, default=0.01)
@@ -327,6 +331,29 @@ def w_hc_28q(q, args, steps=10):
             "kernels": stats}
 
 
+def first_run_cache(n, seed):
+    """The first run of the same circuit in a NEW process, without and with the on-disk cache of
+    an earlier process (csrc/hip/cache.hip: pass-kernel code objects and the layout decision):
+    scripts/first_run.py in three child processes sharing one private cache directory — cold
+    (empty cache), warm (the first one's entries), and the library with the cache off."""
+    import subprocess
+    import tempfile
+    out = {"workload": f"first sim.run of W-HC seed {seed} at {n} qubits in a new process (jit = 2, "
+                       f"calibrated first run), private cache directory"}
+    with tempfile.TemporaryDirectory() as d:
+        env = dict(os.environ, QSIM_CACHE="1", QSIM_CACHE_DIR=d)
+        for tag in ("cold", "warm"):
+            r = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "first_run.py"), str(n), str(seed)],
+                               capture_output=True, text=True, timeout=600, env=env)
+            if r.returncode != 0:
+                out[tag] = {"error": r.stderr[-500:]}
+                return out
+            rec = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+            rec.pop("p0", None)
+            out[tag] = rec
+    return out
+
+
 def run_single(args):
     import qsim_amd as q
     n = args.qubits
@@ -439,6 +466,8 @@ def run_single(args):
             out["w_ref"] = w_ref(q, args)
         if "w_hc_28q" in ex:
             out["w_hc_28q"] = w_hc_28q(q, args)
+        if "first_run_cache" in ex:
+            out["first_run_cache"] = first_run_cache(n, args.seed)
         if "h_single" in ex:
             out["h_single_synced"] = h_single_synced(q)
         if "gate_table" in ex:

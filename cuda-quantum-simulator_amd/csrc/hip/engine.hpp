@@ -293,6 +293,14 @@ bool calibrate_mode_on();  // the calibration mode alone (QSIM_RELABEL_CALIBRATE
 int relabel_tries();  // QSIM_RELABEL_TRIES (default 7): random labelings planned per choice
 // Process-wide memo of layout choices per circuit (kind: 0 state, 1 batched with its run flags).
 // h != null / h >= 0: a decision that also chose the tile height (cross-height calibration).
+// On-disk cache across processes (cache.hip; QSIM_CACHE=0 off, QSIM_CACHE_DIR): hipRTC code objects
+// keyed by their source and options, layout decisions keyed like the in-process memo.
+std::string cache_dir();
+uint64_t cache_hash(const void* p, size_t n, uint64_t seed);
+bool jit_cache_load(const std::string& src, const std::string& opts, std::vector<char>& code);
+void jit_cache_store(const std::string& src, const std::string& opts, const std::vector<char>& code);
+bool layout_cache_load(int n, int kind, const void* key, size_t bytes, std::vector<int>& perm, int* h);
+void layout_cache_store(int n, int kind, const void* key, size_t bytes, int h, const std::vector<int>& perm);
 bool layout_memo_get(int n, int kind, const void* gates, size_t bytes, std::vector<int>& perm, int* h = nullptr);
 void layout_memo_put(int n, int kind, const void* gates, size_t bytes, const std::vector<int>& perm, int h = -1);
 bool calibrate_heights(int n);  // QSIM_CALIBRATE_HEIGHTS (capi.hip: choose_first_layout)

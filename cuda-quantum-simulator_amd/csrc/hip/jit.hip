@@ -594,12 +594,19 @@ bool jit_compile(const std::string& src, std::vector<char>& code, std::string& l
             std::fclose(f);
         }
     }
+    const char* opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17"};
+    // the code object of this source from the on-disk cache (cache.hip), when a process on this
+    // machine compiled it before
+    int vmaj = 0, vmin = 0;
+    (void)hiprtcVersion(&vmaj, &vmin);
+    const std::string okey = std::string(opts[0]) + " " + opts[1] + " " + opts[2] + " hiprtc " +
+                             std::to_string(vmaj) + "." + std::to_string(vmin);
+    if (jit_cache_load(src, okey, code)) return true;
     hiprtcProgram prog;
     if (hiprtcCreateProgram(&prog, src.c_str(), "qsim_pass.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS) {
         log = "hiprtcCreateProgram failed";
         return false;
     }
-    const char* opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17"};
     const hiprtcResult rc = hiprtcCompileProgram(prog, 3, opts);
     size_t ls = 0;
     hiprtcGetProgramLogSize(prog, &ls);
@@ -615,6 +622,7 @@ bool jit_compile(const std::string& src, std::vector<char>& code, std::string& l
         ok = cs > 0 && hiprtcGetCode(prog, code.data()) == HIPRTC_SUCCESS;
     }
     hiprtcDestroyProgram(&prog);
+    if (ok) jit_cache_store(src, okey, code);
     return ok;
 }
 

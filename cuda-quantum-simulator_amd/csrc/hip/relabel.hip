@@ -86,7 +86,18 @@ bool layout_memo_get(int n, int kind, const void* gates, size_t bytes, std::vect
             if (h) *h = e.h;
             return true;
         }
-    return false;
+    // a decision another process made on this machine (cache.hip), taken into this process's memo
+    int dh = -1;
+    std::vector<int> dp;
+    if (!layout_cache_load(n, kind, gates, bytes, dp, &dh)) return false;
+    if (g_memo.size() >= kMemo)
+        g_memo.erase(std::min_element(g_memo.begin(), g_memo.end(),
+                                      [](const MemoEntry& a, const MemoEntry& b) { return a.used < b.used; }));
+    const unsigned char* p = static_cast<const unsigned char*>(gates);
+    g_memo.push_back(MemoEntry{n, kind, std::vector<unsigned char>(p, p + bytes), dp, dh, ++g_memo_clock});
+    perm = dp;
+    if (h) *h = dh;
+    return true;
 }
 void layout_memo_put(int n, int kind, const void* gates, size_t bytes, const std::vector<int>& perm, int h) {
     std::lock_guard<std::mutex> l(g_memo_mu);
@@ -96,6 +107,7 @@ void layout_memo_put(int n, int kind, const void* gates, size_t bytes, const std
     kind = (kind * 16 + (h >= 0 ? 15 : tile_height_default())) * 2 + (tile_ctrl_out() ? 1 : 0);
     const unsigned char* p = static_cast<const unsigned char*>(gates);
     g_memo.push_back(MemoEntry{n, kind, std::vector<unsigned char>(p, p + bytes), perm, h, ++g_memo_clock});
+    layout_cache_store(n, kind, gates, bytes, h, perm);
 }
 
 // Cross-height calibration (QSIM_CALIBRATE_HEIGHTS, default 1; needs layout calibration, i.e.

@@ -156,6 +156,7 @@ _sig(hip, "qsim_batch_profile_get", [_P, c_int, c_char_p, c_size_t, POINTER(c_do
 _sig(hip, "qsim_noise_apply", [_P, c_int, c_int, c_double, c_uint64, c_uint64])
 _sig(hip, "qsim_noise_check_flips", [POINTER(c_uint64)])
 _sig(hip, "qsim_noise_gap_check", [c_double, c_uint64, c_uint64, POINTER(c_uint64), POINTER(c_uint64)])
+_sig(hip, "qsim_cache_stats", [POINTER(c_uint64), POINTER(c_uint64), POINTER(c_uint64), POINTER(c_uint64)])
 _sig(hip, "qsim_noise_gap_check_edges", [c_double, c_uint64, POINTER(c_uint64), POINTER(c_uint64),
                                          POINTER(c_uint64)])
 _sig(hip, "qsim_noisy_run", [_P, POINTER(qsim_gate), c_size_t, POINTER(qsim_noise_channel), c_size_t,

@@ -334,6 +334,11 @@ int qsim_noise_check_flips(uint64_t* flips);
  * floor(ln u / ln(1 - P)) in double, both capped at one 256-pair block (a walk only needs to know
  * a gap is past its block): *mismatches (0 expected) and *fallbacks. */
 int qsim_noise_gap_check(double p, uint64_t draws, uint64_t key, uint64_t* mismatches, uint64_t* fallbacks);
+/* On-disk cache across processes of the first-run costs (no reference counterpart: the reference
+ * compiles its kernels ahead of time and does no layout search): circuit-specialised pass kernels
+ * (hipRTC code objects) and layout decisions, in QSIM_CACHE_DIR (default $XDG_CACHE_HOME/qsim_amd
+ * or $HOME/.cache/qsim_amd; QSIM_CACHE=0 off).  Counters of this process: entries loaded / written. */
+int qsim_cache_stats(uint64_t* jit_hits, uint64_t* jit_stores, uint64_t* layout_hits, uint64_t* layout_stores);
 /* Tests: the same comparison on TARGETED draws — for every gap boundary m in [0, 256] (u_m =
  * exp(m ln(1 - P))) and both ends of the interval of doubles that round to the float nearest u_m,
  * 2 x half consecutive u values around each; *draws = how many were checked. */

@@ -21,6 +21,9 @@ resource.setrlimit(resource.RLIMIT_CORE, (0, 0))
 for p in (ROOT, PKG, ORACLE):
     if p not in sys.path:
         sys.path.insert(0, p)
+# Hermetic runs: no on-disk cache of kernels / layout decisions from earlier processes
+# (csrc/hip/cache.hip); tests/test_cache_gpu.py turns it on for its own child processes.
+os.environ.setdefault("QSIM_CACHE", "0")
 
 
 def pytest_configure(config):
