@@ -339,11 +339,13 @@ void launch_noise_after_gate(double2* st, int n, const std::vector<NoiseChan>& c
                              uint64_t& counter, hipStream_t s, Timer* tm, uint64_t batch, uint64_t traj0) {
     const int log_ppt = n - 1;
     // whole trajectories, >= 128 blocks of 256 pairs (QSIM_NOISE_UNIT_LOG: experiments, >= n - 1;
-    // W-BATCH config 4: one trajectory per work-group, 2^15 pairs, suffix push 0.140 -> 0.137 ms
-    // against two, profiles/r05/batch_unit/)
+    // W-BATCH config 4: two trajectories per work-group, 2^16 pairs — round 5 measured one
+    // trajectory faster for the push alone (0.137 vs 0.140 ms, profiles/r05/batch_unit/), but in
+    // the two-stream step two are: 1.953-1.958 M -> 1.976-1.982 M trajectory-gates/s over two
+    // runs each, four trajectories 1.956 M (r6p run))
     static const int unit_log_env = [] {
         const char* e = std::getenv("QSIM_NOISE_UNIT_LOG");
-        return e ? std::atoi(e) : 15;
+        return e ? std::atoi(e) : 16;
     }();
     const int log_unit = std::max(log_ppt, unit_log_env);
     const uint64_t pairs = batch << log_ppt, idx0 = traj0 << log_ppt;
