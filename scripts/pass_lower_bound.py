@@ -33,6 +33,7 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."
 
 
 SHARE = [4]  # relayout: qubits consecutive tiles share (the next pass's run: 2^share amplitudes)
+RUN = [4]    # fixed: run qubits every tile holds (r0: runs of 2^r0 amplitudes)
 
 
 def circuit_gates(n, depth, seed):
@@ -91,7 +92,7 @@ def feasible(n, gates, K, H, family, time_limit=600.0, n_high=None):
     if n_high is not None:
         rows.append(({Z0 + p: 1 for p in range(K)}, 0, n_high))
     if family == "fixed":
-        rows.append(({R0 + q: 1 for q in range(n)}, 4, np.inf))
+        rows.append(({R0 + q: 1 for q in range(n)}, RUN[0], np.inf))
         for q in range(n):
             for p in range(K):
                 rows.append(({R0 + q: 1, Y(q, p): -1}, -np.inf, 0))
@@ -136,9 +137,11 @@ def main():
                     help="mixed heights: at most this many passes of --height qubits, the rest one less")
     ap.add_argument("--share", type=int, default=4,
                     help="relayout family: qubits consecutive tiles share (run of 2^share amplitudes)")
+    ap.add_argument("--run", type=int, default=4, help="fixed family: run qubits shared by every tile (r0)")
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
     SHARE[0] = a.share
+    RUN[0] = a.run
     results = []
     for sd in [int(s) for s in a.seeds.split(",")]:
         gates = circuit_gates(a.qubits, a.depth, sd)
@@ -147,6 +150,7 @@ def main():
             v, dt, plan = feasible(a.qubits, gates, a.passes, a.height, fam, n_high=a.tall)
             r = {"seed": sd, "qubits": a.qubits, "passes": a.passes, "max_tile_qubits": a.height if fam != "relayout" else 12,
                  "tall_passes_max": a.tall, "relayout_share": a.share if fam == "relayout" else None,
+                 "fixed_run": a.run if fam == "fixed" else None,
                  "family": fam, "target_qubits": targets, "verdict": v, "seconds": dt}
             if plan:
                 r["tiles"] = plan["tiles"]
