@@ -240,3 +240,28 @@ def test_tile_noise_matches_oracle(qsim, oracle, gpu_ready, monkeypatch, lists, 
     sim.run(c)
     want2, _ = oracle.noisy_run(n, oracle.gates_of(c), channels, 3000 + seed, ctr, want)
     np.testing.assert_allclose(sim.getStateVector(), want2, atol=1e-12, rtol=0)
+
+
+@pytest.mark.parametrize("n,seed,p", [(12, 21, 0.3), (14, 22, 0.05), (16, 23, 0.01)])
+def test_pull_chains_match_oracle(qsim, oracle, gpu_ready, monkeypatch, n, seed, p):
+    """The pulled pass (k_pull_gate, sparse words) against the oracle with channels on every qubit
+    (X / Y / Z / depolarizing; p = 0.3: long chains through partners, overflow words), a repeated
+    channel, gates on qubit 11 and above, controls above the low qubits, SWAPs of two high qubits,
+    two runs.  (Round 6 also ran a tile form of this pass — in-tile partners from LDS, the gate in
+    LDS — through this test, 0.71 against 0.61 ms at 26 qubits: not kept)"""
+    monkeypatch.setenv("QSIM_NOISY_TILE", "0")
+    c = qsim.createRandomCircuit(n, 20, seed)
+    c.cnot(n - 1, 2).swap(3, n - 2).swap(n - 1, n - 2).cz(0, n - 1).toffoli(n - 1, n - 2, 4)
+    c.rx(n - 3, 0.4).h(11).cnot(5, 11)
+    if n > 12:
+        c.cnot(11, n - 1).swap(11, n - 1)
+    types = (0, 3, 4, 5)
+    channels = [(types[q % 4], q, p) for q in range(n)] + [(0, n - 1, p), (3, 0, p)]
+    sim = qsim.NoisySimulator(n, _model(qsim, channels))
+    sim.setSeed(4000 + seed)
+    sim.run(c)
+    want, ctr = oracle.noisy_run(n, oracle.gates_of(c), channels, 4000 + seed)
+    np.testing.assert_allclose(sim.getStateVector(), want, atol=1e-12, rtol=0)
+    sim.run(c)
+    want2, _ = oracle.noisy_run(n, oracle.gates_of(c), channels, 4000 + seed, ctr, want)
+    np.testing.assert_allclose(sim.getStateVector(), want2, atol=1e-12, rtol=0)
