@@ -106,7 +106,7 @@ def parse():
     p.add_argument("--no-extras", action="store_true",
                    help="skip the default line's extra objects (seeds, default_mode, w_ref, "
                         "gate_table_20q, dm_14q, noisy_26q)")
-    p.add_argument("--extras", default="seeds,default_mode,w_ref,w_hc_28q,first_run_cache,h_single,gate_table,dm,noisy",
+    p.add_argument("--extras", default="seeds,default_mode,w_ref,w_hc_28q,w_hc_seq,first_run_cache,h_single,gate_table,dm,noisy",
                    help="which extra objects of the default W-HC line to measure (comma list; "
                         "--no-extras: none)")
     p.add_argument("--noise", type=float, default=0.01)
@@ -331,6 +331,45 @@ def w_hc_28q(q, args, steps=10):
             "kernels": stats}
 
 
+def w_hc_seq(q, args, reps=4, steps=5):
+    """Consecutive W-HC circuits as ONE engine run (Simulator.runSequence; not the headline, whose
+    step is one run() of one circuit): `reps` copies of the line's circuit, and `reps` circuits of
+    consecutive seeds, each planned as a whole — a pass may hold the end of one circuit and the
+    start of the next.  Per sequence: calibrated first run on |0..0>, one warm-up, the median of
+    `steps` synchronised sequences; value = gates of the sequence / that median."""
+    from qsim_amd.plan import set_jit
+    set_jit(args.jit, -1)
+    n = args.qubits
+    out = {"workload": f"{reps} consecutive createRandomHCCircuit({n}, {args.depth}, .) per "
+                       f"Simulator.runSequence call (same mode as the line)", "runs": []}
+    for label, seeds in (("same", [args.seed] * reps), ("seeds", [args.seed + i for i in range(reps)])):
+        circs = [q.createRandomHCCircuit(n, args.depth, sd) for sd in seeds]
+        gates = sum(c.getGateCount() for c in circs)
+        sim = q.Simulator(n)
+        t0 = time.perf_counter()
+        sim.runSequence(circs)
+        sim.synchronize()
+        first = time.perf_counter() - t0
+        sim.runSequence(circs)
+        sim.synchronize()
+        ts_ = []
+        for _ in range(steps):
+            t0 = time.perf_counter()
+            sim.runSequence(circs)
+            sim.synchronize()
+            ts_.append(time.perf_counter() - t0)
+        med = _median(ts_)
+        info = sim.state.layoutInfo()
+        passes = sim.state.lastRunInfo()[0]
+        del sim
+        out["runs"].append({"circuits": label, "seeds": seeds, "gates": gates, "value": round(gates / med, 1),
+                            "unit": "gates/s", "ms_per_sequence": round(med * 1e3, 3),
+                            "passes": passes, "passes_per_circuit": round(passes / reps, 3),
+                            "relayout": info["relayout"], "tile_qubits": info["tile_qubits"],
+                            "first_run_ms": round(first * 1e3, 1)})
+    return out
+
+
 def first_run_cache(n, seed):
     """The first run of the same circuit in a NEW process, without and with the on-disk cache of
     an earlier process (csrc/hip/cache.hip: pass-kernel code objects and the layout decision):
@@ -466,6 +505,8 @@ def run_single(args):
             out["w_ref"] = w_ref(q, args)
         if "w_hc_28q" in ex:
             out["w_hc_28q"] = w_hc_28q(q, args)
+        if "w_hc_seq" in ex:
+            out["w_hc_seq"] = w_hc_seq(q, args)
         if "first_run_cache" in ex:
             out["first_run_cache"] = first_run_cache(n, args.seed)
         if "h_single" in ex:

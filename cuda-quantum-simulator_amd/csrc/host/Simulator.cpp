@@ -21,6 +21,18 @@ void Simulator::run(const Circuit& circuit) {
                    mode_ == RunMode::Fused ? QSIM_RUN_FUSED : QSIM_RUN_PER_GATE));
 }
 
+void Simulator::runSequence(const std::vector<Circuit>& circuits) {
+    std::vector<qsim_gate> gates;
+    for (const Circuit& c : circuits) {
+        if (c.getNumQubits() != state_.getNumQubits())
+            throw std::invalid_argument("Circuit qubit count doesn't match simulator");
+        const std::vector<qsim_gate> g = detail::toAbi(c);
+        gates.insert(gates.end(), g.begin(), g.end());
+    }
+    check(qsim_run(state_.handle(), gates.data(), gates.size(),
+                   mode_ == RunMode::Fused ? QSIM_RUN_FUSED : QSIM_RUN_PER_GATE));
+}
+
 void Simulator::applyGate(const GateOp& gate) {
     const qsim_gate g = detail::toAbi(gate);
     check(qsim_apply_gate(state_.handle(), &g));

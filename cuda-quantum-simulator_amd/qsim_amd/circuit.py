@@ -107,6 +107,14 @@ class Circuit:
     def append(self, op: GateOp) -> "Circuit":
         return self._add(op.type, op.qubits, op.parameter)
 
+    def extend(self, other: "Circuit") -> "Circuit":
+        """Append every gate of `other` (same qubit count) in order."""
+        if other.getNumQubits() != self._n:
+            raise ValueError("Circuit qubit count doesn't match")
+        self._gates.extend(GateOp(g.type, g.qubits, g.parameter) for g in other._gates)
+        self._abi = None
+        return self
+
     # -- access
     def getNumQubits(self) -> int: return self._n
     num_qubits = property(getNumQubits)

@@ -49,6 +49,16 @@ def device_info(device: int = 0):
     return {"name": name.value.decode(), "cu_count": cus.value, "total_mem": mem.value}
 
 
+def sequence_circuit(circuits, n: int) -> Circuit:
+    """The gates of `circuits` (each of n qubits) in order, as one circuit."""
+    seq = Circuit(n)
+    for c in circuits:
+        if c.getNumQubits() != n:
+            raise ValueError("Circuit qubit count doesn't match simulator")
+        seq.extend(c)
+    return seq
+
+
 class StateVector:
     def __init__(self, num_qubits: int, device: Optional[int] = None):
         if not is_valid_qubit_count(num_qubits):
@@ -238,6 +248,14 @@ class StateVector:
         arr, n = circuit.to_abi()
         _lib.check(_lib.hip.qsim_run(self._h, arr, n, int(mode)))
 
+    def runSequence(self, circuits, mode: RunMode = RunMode.Fused) -> None:
+        """Apply `circuits` one after the other as ONE engine run (no reference counterpart): the
+        planner sees their gates together, so a pass may hold the end of one circuit and the
+        start of the next — consecutive 100-gate W-HC circuits at 30 qubits plan into 2.5-2.75
+        passes each instead of 4.  The same state as run() on each in turn."""
+        seq = sequence_circuit(circuits, self._n)
+        self.run(seq, mode)
+
     def perm(self):
         """Current logical -> physical qubit map (identity unless a fused run relabeled)."""
         p = (_c.c_int32 * self._n)()
@@ -305,6 +323,10 @@ class Simulator:
         if circuit.getNumQubits() != self._state.getNumQubits():
             raise ValueError("Circuit qubit count doesn't match simulator")
         self._state.run(circuit, self._mode)
+
+    def runSequence(self, circuits) -> None:
+        """run() of each circuit in turn, planned as one (StateVector.runSequence)."""
+        self._state.runSequence(circuits, self._mode)
 
     def applyGate(self, op: GateOp) -> None: self._state.applyGate(op)
     def getStateVector(self) -> np.ndarray: return self._state.toHost()

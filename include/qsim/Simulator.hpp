@@ -31,6 +31,10 @@ public:
 
     void reset();
     void run(const Circuit& circuit);  // std::invalid_argument on qubit-count mismatch
+    // run() of each circuit in turn as ONE engine run (no reference counterpart): the planner
+    // sees their gates together, so a fused pass may hold the end of one and the start of the
+    // next (consecutive W-HC circuits at 30 qubits: 2.5-2.75 passes each instead of 4).
+    void runSequence(const std::vector<Circuit>& circuits);
     void applyGate(const GateOp& gate);
 
     std::vector<std::complex<double>> getStateVector() const;

@@ -215,6 +215,19 @@ TEST(Equivalence, FullGateSetWide) {  // all 17 gate types, targets across the 1
         expect_matches_oracle(c);
     }
 }
+TEST(Equivalence, RunSequence) {  // Simulator::runSequence (no reference counterpart) = run() in turn
+    for (int n : {9, 14, 20}) {
+        std::vector<qsim::Circuit> cs;
+        for (unsigned s = 0; s < 3; ++s) cs.push_back(qsim::createRandomHCCircuit(n, 60, 100 + s));
+        qsim::Simulator seq(n);
+        seq.runSequence(cs);
+        qsim_oracle::CPUSimulator cpu(n);
+        for (const qsim::Circuit& c : cs) cpu.run(c);
+        expect_state(seq.getStateVector(), cpu.getStateVector(), kEquivTol);
+    }
+    qsim::Simulator sim(3);
+    EXPECT_THROW(sim.runSequence({qsim::Circuit(3), qsim::Circuit(4)}), std::invalid_argument);
+}
 TEST(Equivalence, EmptyAndTrivialCircuits) {  // :318-339
     qsim::Circuit e(3), one(3), two(3);
     one.h(1);

@@ -116,3 +116,34 @@ def test_tile_constant_controls_execute_exactly(qsim, oracle, ctrl_out, n, seed)
     set_tile_ctrl_out(1)
     on, off = (got, other) if ctrl_out else (other, got)
     assert on[0] <= off[0] and on[1] <= off[1]
+
+
+def test_sequence_circuit_and_joint_plan(qsim):
+    """Simulator.runSequence's circuit (qsim_amd.simulator.sequence_circuit: the gates in order) and
+    why it pays: four consecutive 100-gate W-HC circuits at 30 qubits plan into at most 11 relayout
+    passes together against 4 each alone (host planner, no GPU)."""
+    from qsim_amd.plan import plan_relayout
+    from qsim_amd.simulator import sequence_circuit
+    cs = [qsim.createRandomHCCircuit(30, 100, sd) for sd in (42, 43, 44, 45)]
+    seq = sequence_circuit(cs, 30)
+    assert [(g.type, g.qubits) for g in seq.getGates()] == [(g.type, g.qubits) for c in cs for g in c.getGates()]
+    alone = [plan_relayout(c)[1] for c in cs]
+    assert alone == [4, 4, 4, 4]
+    assert 0 < plan_relayout(seq)[1] <= 11
+    with pytest.raises(ValueError):
+        sequence_circuit([cs[0], qsim.Circuit(29)], 30)
+    with pytest.raises(ValueError):
+        qsim.Circuit(30).extend(qsim.Circuit(29))
+
+
+def test_joint_plan_of_a_sequence_executes_exactly(qsim, oracle):
+    """The relayout plan of three consecutive W-HC circuits (what runSequence runs), executed on the
+    host as the pass kernels address the state, equals the oracle of the circuits in turn."""
+    from qsim_amd.plan import plan_exec_host, plan_relayout
+    from qsim_amd.simulator import sequence_circuit
+    n = 20
+    cs = [qsim.createRandomHCCircuit(n, 100, sd) for sd in (7, 8, 9)]
+    seq = sequence_circuit(cs, n)
+    assert plan_relayout(seq)[1] < sum(plan_relayout(c)[1] for c in cs)
+    st, perm, passes = plan_exec_host(seq, 1)
+    assert _err(st, oracle.run_cpu(n, oracle.gates_of(seq))) < 1e-12

@@ -105,3 +105,34 @@ def test_relayout_from_basis_state_then_readers_and_gates(qsim, oracle, gpu_read
     assert abs(sv.probBitZero(11) - probs[((idx >> 11) & 1) == 0].sum()) < 1e-12
     assert sv.perm() == list(range(n))
     assert _err(sv.toHost(), ref) < 1e-12
+
+
+@pytest.mark.parametrize("n", [22, 24])
+def test_run_sequence_matches_runs_and_oracle(qsim, oracle, gpu_ready, relayout_low, n):
+    """Simulator.runSequence: consecutive circuits planned as one engine run (a pass may hold the end
+    of one circuit and the start of the next — fewer passes than the runs one by one) give the
+    oracle's state of the circuits applied in turn, from a basis state (relayout plan) and again
+    on the evolved state; the same circuits run one by one agree."""
+    from qsim_amd.plan import plan_relayout
+    cs = [qsim.createRandomHCCircuit(n, 100, sd) for sd in (42, 43, 44)]
+    seq = qsim.Circuit(n)
+    for c in cs:
+        seq.extend(c)
+    assert seq.getGateCount() == 300
+    assert plan_relayout(seq)[1] < sum(plan_relayout(c)[1] for c in cs)
+    g = oracle.gates_of(seq)
+    a = qsim.Simulator(n)
+    a.runSequence(cs)
+    assert a.state.layoutInfo()["relayout"]
+    want = oracle.run_cpu(n, g)
+    assert _err(a.getStateVector(), want) < 1e-12
+    a.runSequence(cs)
+    want2 = oracle.run_cpu(n, g, want)
+    assert _err(a.getStateVector(), want2) < 1e-12
+    b = qsim.Simulator(n)
+    for _ in range(2):
+        for c in cs:
+            b.run(c)
+    assert _err(b.getStateVector(), want2) < 1e-12
+    with pytest.raises(ValueError):
+        a.runSequence([qsim.Circuit(n), qsim.Circuit(n - 1)])
