@@ -109,6 +109,12 @@ class DistributedSimulator:
         _lib.check(_lib.hip.qsim_dist_run(self._h, arr, cnt,
                                           _lib.QSIM_RUN_FUSED if fused else _lib.QSIM_RUN_PER_GATE))
 
+    def runSequence(self, circuits, fused: bool = True) -> None:
+        """run() of each circuit in turn as ONE sharded run (Simulator.runSequence): passes and
+        global<->local remaps are planned over all of their gates."""
+        from .simulator import sequence_circuit
+        self.run(sequence_circuit(circuits, self._n), fused)
+
     def synchronize(self) -> None: _lib.check(_lib.hip.qsim_dist_sync(self._h))
 
     def barrier(self) -> None:

@@ -59,6 +59,21 @@ def test_virtual_ranks_run_twice_and_reset(qsim, oracle, gpu_ready):
     assert abs(s[0] - 1) < 1e-15 and np.all(np.abs(s[1:]) == 0)
 
 
+@pytest.mark.parametrize("world,n", [(8, 16), (4, 20)])
+def test_virtual_ranks_run_sequence(qsim, oracle, gpu_ready, world, n):
+    """DistributedSimulator.runSequence: three circuits as one sharded run (remaps and passes planned
+    over all of them) equal the oracle of the circuits in turn, twice."""
+    from qsim_amd.dist import DistributedSimulator
+    cs = [qsim.createRandomHCCircuit(n, 100, sd) for sd in (42, 43)] + [qsim.createRandomCircuit(n, 60, 9)]
+    g = [x for c in cs for x in oracle.gates_of(c)]
+    d = DistributedSimulator.virtual(n, world)
+    d.runSequence(cs)
+    ref = oracle.run_cpu(n, g)
+    assert np.max(np.abs(d.getStateVector() - ref)) < 1e-12
+    d.runSequence(cs)
+    assert np.max(np.abs(d.getStateVector() - oracle.run_cpu(n, g, ref))) < 1e-12
+
+
 @pytest.mark.parametrize("world,n", [(4, 22), (8, 23), (2, 21)])
 def test_virtual_pipelined_remaps_match_single_gpu(qsim, gpu_ready, world, n):
     """Shards large enough that every remap is split into pipeline parts (transfers on the comm
