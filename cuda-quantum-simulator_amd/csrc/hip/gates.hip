@@ -152,7 +152,16 @@ struct GArgs {
     int t0, t1;
     int sub, d0_one;
     double2 m0, m1, m2, m3;
+    int bmap;           // work-group -> item-block order (QSIM_SLICE_BMAP / QSIM_SLICE_FAR_BMAP)
 };
+// 0: natural; 1: each XCD (blockIdx mod 8) streams one contiguous eighth; 2: consecutive
+// work-groups alternate between the two halves of the items
+__device__ __forceinline__ uint64_t slice_block(const GArgs& a) {
+    const uint64_t b = blockIdx.x, G = gridDim.x;
+    if (a.bmap == 1 && (G & 7ull) == 0ull) return (b & 7ull) * (G >> 3) + (b >> 3);
+    if (a.bmap == 2 && (G & 1ull) == 0ull) return (b & 1ull) * (G >> 1) + (b >> 1);
+    return b;
+}
 
 __device__ __forceinline__ uint64_t item_base(const GArgs& a, uint64_t item, int lane) {
     const uint64_t traj = item >> a.log_ipt;
@@ -167,8 +176,9 @@ __device__ __forceinline__ uint64_t item_base(const GArgs& a, uint64_t item, int
 template <int U, bool NT, int MODE>
 __device__ __forceinline__ void m1_slice_body(const GArgs& a) {
     const int lane = threadIdx.x & 63;
-    const uint64_t first = MODE == 2 ? (uint64_t)blockIdx.x * (4 * U) + (uint64_t)(threadIdx.x >> 6) * U
-                                     : (uint64_t)blockIdx.x * (4 * U) + (threadIdx.x >> 6);
+    const uint64_t bid = slice_block(a);
+    const uint64_t first = MODE == 2 ? bid * (4 * U) + (uint64_t)(threadIdx.x >> 6) * U
+                                     : bid * (4 * U) + (threadIdx.x >> 6);
     const uint64_t step = MODE == 2 ? 1 : 4;
     const uint64_t tb = 1ull << a.t0;
     double2 v0[U], v1[U];
@@ -227,7 +237,7 @@ __global__ __launch_bounds__(256) void k_m1_slice_c(GArgs a) { m1_slice_body<U, 
 template <int U, bool NT>
 __global__ __launch_bounds__(256) void k_m1_lane(GArgs a) {
     const int lane = threadIdx.x & 63;
-    const uint64_t first = (uint64_t)blockIdx.x * (4 * U) + (threadIdx.x >> 6);
+    const uint64_t first = slice_block(a) * (4 * U) + (threadIdx.x >> 6);
     const bool active = lane < a.nlanes;
     double2 v[U];
     uint64_t idx[U];
@@ -257,7 +267,7 @@ __global__ __launch_bounds__(256) void k_m1_lane(GArgs a) {
 template <int U, bool NT>
 __global__ __launch_bounds__(256) void k_diag(GArgs a) {
     const int lane = threadIdx.x & 63;
-    const uint64_t first = (uint64_t)blockIdx.x * (4 * U) + (threadIdx.x >> 6);
+    const uint64_t first = slice_block(a) * (4 * U) + (threadIdx.x >> 6);
     // a phase on the |1> side only (d0 == 1) with a low target: lanes on the |0> side never load
     const bool one_side = a.d0_one && a.t0 < 6 && !((lane >> a.t0) & 1);
     const bool lane_ok = lane < a.nlanes && ((lane & a.lane_ctrl) == a.lane_ctrl) && !one_side;
@@ -285,7 +295,7 @@ __global__ __launch_bounds__(256) void k_diag(GArgs a) {
 template <int U>
 __global__ __launch_bounds__(256) void k_swap_hh(GArgs a) {
     const int lane = threadIdx.x & 63;
-    const uint64_t first = (uint64_t)blockIdx.x * (4 * U) + (threadIdx.x >> 6);
+    const uint64_t first = slice_block(a) * (4 * U) + (threadIdx.x >> 6);
     const uint64_t ba = 1ull << a.t1, bb = 1ull << a.t0;
     double2 va[U], vb[U];
     uint64_t i[U];
@@ -312,7 +322,7 @@ __global__ __launch_bounds__(256) void k_swap_hh(GArgs a) {
 template <int U>
 __global__ __launch_bounds__(256) void k_swap_lh(GArgs a) {
     const int lane = threadIdx.x & 63;
-    const uint64_t first = (uint64_t)blockIdx.x * (4 * U) + (threadIdx.x >> 6);
+    const uint64_t first = slice_block(a) * (4 * U) + (threadIdx.x >> 6);
     const uint64_t b1 = 1ull << a.t1;
     double2 s0[U], s1[U];
     uint64_t i[U];
@@ -345,7 +355,7 @@ __global__ __launch_bounds__(256) void k_swap_lh(GArgs a) {
 template <int U>
 __global__ __launch_bounds__(256) void k_swap_ll(GArgs a) {
     const int lane = threadIdx.x & 63;
-    const uint64_t first = (uint64_t)blockIdx.x * (4 * U) + (threadIdx.x >> 6);
+    const uint64_t first = slice_block(a) * (4 * U) + (threadIdx.x >> 6);
     const bool active = lane < a.nlanes;
     double2 v[U];
     uint64_t idx[U];
@@ -457,9 +467,14 @@ static void add_fix(GArgs& a, int pos) {
 // Round-4 measurements (profiles/r04/w1q/): W-1Q 28q mean 0.7652 with this choice, 0.7613 with
 // round 3's (mode 0, 4 items), 0.7519 with the far range widened to targets >= 14; no variant
 // lifts targets 20-25 above 0.72.
+// Work-group order (QSIM_SLICE_BMAP, QSIM_SLICE_FAR_BMAP for the far targets; default 1, round 6):
+// work-groups are dispatched round-robin over the 8 XCDs, so with the natural order all eight
+// stream the same region at once; mode 1 gives each XCD one contiguous eighth of the items (2: the
+// two halves alternate).  28 qubits (profiles/r06/w1q/): targets 20-25 0.71 -> 0.74-0.755, lane
+// targets 0-5 0.76 -> 0.81, W-1Q 0.763 -> 0.787 of 8 TB/s.
 struct Tune {
     int slice_u = 1, lane_u = 2, diag_u = 2;
-    int slice_u_far = 2, far_lo = 20, far_hi = 25, far_mode = 2, far_min_n = 24;
+    int slice_u_far = 2, far_lo = 20, far_hi = 25, far_mode = 2, far_min_n = 24, far_bmap = 1, bmap = 1;
     bool nt = true;
     Tune() {
         auto env = [](const char* k, int d) {
@@ -472,6 +487,8 @@ struct Tune {
         far_hi = env("QSIM_SLICE_FAR_HI", far_hi);
         far_mode = env("QSIM_SLICE_FAR_MODE", far_mode);
         far_min_n = env("QSIM_SLICE_FAR_MIN_QUBITS", far_min_n);
+        far_bmap = env("QSIM_SLICE_FAR_BMAP", far_bmap);
+        bmap = env("QSIM_SLICE_BMAP", bmap);
         lane_u = env("QSIM_LANE_U", lane_u);
         diag_u = env("QSIM_DIAG_U", diag_u);
         nt = env("QSIM_NT", nt ? 1 : 0) != 0;
@@ -538,6 +555,7 @@ void launch_op(double2* st, int n, uint64_t batch, const Op& op, hipStream_t s, 
         a.items = batch << lb;
     };
     const Tune& T = tune();
+    a.bmap = T.bmap;
 #define QSIM_GO_U(KERNEL, UVAL, CHOICES)                                            \
     do {                                                                            \
         const int u_ = (UVAL);                                                      \
@@ -559,6 +577,7 @@ void launch_op(double2* st, int n, uint64_t batch, const Op& op, hipStream_t s, 
                 finish();
                 TimedLaunch tl(tm, "m1_slice", bytes, s, true);
                 const bool far = op.t0 >= T.far_lo && op.t0 <= T.far_hi && n >= T.far_min_n;
+                a.bmap = far ? T.far_bmap : T.bmap;
                 if (far && T.far_mode == 1) {
                     QSIM_GO_U(k_m1_slice_g, T.slice_u_far, QSIM_U248);
                 } else if (far && T.far_mode == 2) {

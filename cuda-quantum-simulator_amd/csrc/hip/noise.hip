@@ -205,6 +205,7 @@ struct UArgs {
     double2* st;
     uint64_t pairs, idx0;
     int log_ppt, log_unit, nch;
+    int bmap;  // work-group order (QSIM_NOISE_BMAP)
     FlipChan ch[kMaxUnitChannels];
 };
 // Why this is race-free (the round-2 "batched-load variant" that returned
@@ -226,9 +227,24 @@ struct UArgs {
 // kernel has no such store.  QSIM_NOISE_CHECK=1 runs it with every access range-checked on the
 // device (violations counted with atomics and turned into an error by the launcher);
 // tests/test_batched_refnoise_gpu.py runs that check on units that start and end mid-block.
+// Work-group order: 1 gives each of the 8 XCDs (blockIdx mod 8, round-robin dispatch) one
+// contiguous eighth of the grid (gates.hip slice_block), 0 the natural order.  QSIM_NOISE_BMAP
+// (in-tile gate + noise kernel and the suffix push, default 1: W-BATCH 1.980 -> 1.997 M
+// trajectory-gates/s, profiles/r06/xcd_order/); QSIM_PULL_BMAP (the pulled pass, default 0: its
+// partner reads hit L2 more when every XCD streams the same region, 1 259 vs 1 193 gates/s).
+__device__ __forceinline__ uint64_t xcd_block(int mode) {
+    const uint64_t b = blockIdx.x, G = gridDim.x;
+    if (mode == 1 && (G & 7ull) == 0ull) return (b & 7ull) * (G >> 3) + (b >> 3);
+    return b;
+}
+static int env_bmap(const char* k, int dflt) {  // (read per launch: tests switch it)
+    const char* e = std::getenv(k);
+    return e ? std::atoi(e) : dflt;
+}
+
 template <bool CHECK>
 __global__ __launch_bounds__(256) void k_noise_units(UArgs a, unsigned int* bad) {
-    const uint64_t base = ((a.idx0 >> a.log_unit) + blockIdx.x) << a.log_unit;
+    const uint64_t base = ((a.idx0 >> a.log_unit) + xcd_block(a.bmap)) << a.log_unit;
     const uint64_t lo = base > a.idx0 ? base : a.idx0;
     const uint64_t end = a.idx0 + a.pairs, top = base + (1ull << a.log_unit);
     const uint64_t hi = top < end ? top : end;
@@ -363,6 +379,7 @@ void launch_noise_after_gate(double2* st, int n, const std::vector<NoiseChan>& c
     for (size_t c0 = 0; c0 < chans.size(); c0 += kMaxUnitChannels) {
         UArgs u{};
         u.st = st;
+        u.bmap = env_bmap("QSIM_NOISE_BMAP", 1);
         u.pairs = pairs;
         u.idx0 = idx0;
         u.log_ppt = log_ppt;
@@ -487,6 +504,7 @@ struct GnArgs {
     int cap, lcap;         // cap = 2^lcap
     int skip;              // QSIM_NOISE_TILE_SKIP (measurement only, wrong states): 1 no flip
                            // codes written, 2 no pulled walks (outputs read in place), 3 both
+    int bmap;              // work-group order (QSIM_NOISE_BMAP)
 };
 __device__ __forceinline__ int gn_local_pos(int q, int u) { return q <= 10 ? q : (q == u ? 11 : -1); }
 
@@ -629,15 +647,16 @@ __global__ __launch_bounds__(256) void k_gate_noise_tile(GnArgs a) {
     __shared__ uint32_t cnt_s[kGnMaxPrefix];
     const int t = threadIdx.x;
     uint64_t traj = 0, loc = 0;
-    const uint64_t gbase = gn_tile_base(blockIdx.x, a.n, a.u, &traj, &loc);
+    const uint64_t tb = xcd_block(a.bmap);
+    const uint64_t gbase = gn_tile_base(tb, a.n, a.u, &traj, &loc);
     auto gidx = [&](int j) { return gbase | (uint64_t)(j & 2047) | ((uint64_t)(j >> 11) << a.u); };
     // 1. this tile's flip lists, then the tile's loads, all in flight during the flip phase (the
     // lists first: the flip phase then waits only for them — loads retire in order)
     constexpr int kSlots = kGnMaxPrefix;  // list slots per thread: np * cap <= 12 * 256
     uint16_t le[kSlots];
     const int nsl = a.list ? a.np << a.lcap : 0;  // slots of this tile (cap = 2^lcap per channel)
-    const uint16_t* L = a.list + (uint64_t)blockIdx.x * kGnMaxPrefix * (uint64_t)(1u << a.lcap);
-    const uint32_t* C = a.cnt + (uint64_t)blockIdx.x * kGnMaxPrefix;
+    const uint16_t* L = a.list + tb * kGnMaxPrefix * (uint64_t)(1u << a.lcap);
+    const uint32_t* C = a.cnt + tb * kGnMaxPrefix;
     uint32_t cl = 0;
     if (a.list && t < a.np) cl = C[t];
 #pragma unroll
@@ -828,6 +847,7 @@ static GnArgs gn_args(double2* st, int n, uint64_t traj0, const Op* op, const st
     *used_out = used;
     const char* sk = std::getenv("QSIM_NOISE_TILE_SKIP");  // (measurement only)
     a.skip = sk ? std::atoi(sk) : 0;
+    a.bmap = env_bmap("QSIM_NOISE_BMAP", 1);
     return a;
 }
 
@@ -1129,6 +1149,7 @@ __global__ __launch_bounds__(kWordThreads) void k_noise_words(MapArgs a) {
 struct PullArgs {
     const double2* src;
     double2* dst;
+    int bmap;            // work-group order (QSIM_PULL_BMAP; 0 with MAP)
     const void* words;
     uint64_t amps;       // amplitudes of this object (where sparse words keep their overflow words)
     uint64_t items;      // pairs (2x2 / diagonal) or amplitudes (SWAP / identity)
@@ -1245,7 +1266,7 @@ __global__ __launch_bounds__(256) void k_pull_gate(PullArgs a, MapArgs m) {
     } else {
         words.w = static_cast<const W*>(a.words);
     }
-    const uint64_t base = ((uint64_t)blockIdx.x * kPullU) << 8;
+    const uint64_t base = (xcd_block(a.bmap) * kPullU) << 8;
     // items is a multiple of 256, so each item group u (256 consecutive items) is wholly in or
     // wholly out of range for the whole work-group; groups past the end do nothing (a 9- or
     // 10-qubit state has fewer items than one work-group's kPullU groups)
@@ -1426,6 +1447,7 @@ void launch_pull_gate(const double2* src, double2* dst, int n, uint64_t batch, c
     a.dst = dst;
     a.words = words;
     a.amps = amps;
+    a.bmap = fuse ? 0 : env_bmap("QSIM_PULL_BMAP", 0);
     a.kind = op ? op->kind : -1;
     if (op) {
         a.sub = op->sub;

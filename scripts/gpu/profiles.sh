@@ -43,6 +43,8 @@ for rg in $REGIONS; do
     dm14) prof dm14 --workload dm --steps 5 || exit 1 ;;
     pmcnoisy)
       run_pmc noisy_26q python3 $R/bench.py --workload noisy --cpu-budget 0 --steps 2 --warmup 1 || exit 1 ;;
+    pmc1q)
+      run_pmc 1q_28q python3 $R/scripts/w1q28.py || exit 1 ;;
     pmcbatch)
       ( export QSIM_NOISE_SPLIT=1; run_pmc batch_ref_16q python3 $R/bench.py --workload batch --cpu-budget 0 --steps 2 --warmup 1 ) || exit 1 ;;
     pmc)
